@@ -1,0 +1,588 @@
+// track.hip -- GP2021-semantics E/P/L tracking correlator on gfx950.
+//
+// Replaces the per-sample loop of Sim_GP2021_int
+// (reference osgnss_next_step/src/correlator/correlator.c:148-316) with a
+// closed-form, sample-parallel formulation that is bit-exact with it:
+//
+//  * carrier NCO: phase before sample n = P0 + n*cinc (mod 2^32); the 8-phase
+//    LO index is its top 3 bits (correlator.c:203-215).
+//  * code NCO: rollovers before sample n = (K0 + n*kinc2) >> 32 in 64-bit
+//    (kinc2 = code_incr << 1, correlator.c:245), so every thread can start
+//    its run of samples anywhere without walking the previous ones.
+//  * half-chip / dump logic (correlator.c:246-283) is a function of the
+//    rollover count r: until the first dump the half-chip is hc0 + r (uint16);
+//    the first dump comes at rollover j1, then every D = slew + 2046
+//    rollovers.  The E/P/L bits after the dump rollover are loaded from the
+//    PRE-reset index (>= 2046, the reference's row over-read) and half-chip 0
+//    of the new epoch keeps them (no reload), which hc_after() reproduces.
+//  * accumulation is int32 two's-complement, so per-thread partial sums can
+//    be combined in any order: each thread keeps at most two epochs' sums
+//    (a run of 64 samples can straddle at most one dump, D >= 2046), the
+//    wavefront reduces them with cross-lane shuffles and one lane per wave
+//    adds into an LDS slot per epoch.
+//
+// One workgroup = one channel x one call.  256 threads x 64 samples covers a
+// 1-ms chunk at 16.368 Msps; IF is read as 16-byte vector loads.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "gnsscorr_internal.h"
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      gnsscorr_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                         __LINE__);                                                     \
+      return GNSSCORR_EDEVICE;                                                          \
+    }                                                                                   \
+  } while (0)
+
+namespace {
+
+constexpr int kRun = 64;              // samples per thread
+constexpr int kMaxThreads = 1024;
+constexpr int kMaxNsamp = kRun * kMaxThreads;
+constexpr int kMaxEpochs = kMaxNsamp / GNSSCORR_OSG_ROW + 2;
+constexpr uint64_t kNever = ~0ull;
+
+// 8-phase LO (correlator.c:203-204) as 4-bit two's-complement nibbles.
+constexpr uint32_t kLutI = 0xEEF1221Fu;  // i_lo = {-1, 1, 2, 2, 1,-1,-2,-2}
+constexpr uint32_t kLutQ = 0x1FEEF122u;  // q_lo = { 2, 2, 1,-1,-2,-2,-1, 1}
+
+struct Chan {
+  uint32_t P0, K0, cinc, kinc2, hc0, D;
+  uint64_t j1;       // rollover index of the first dump (kNever: none)
+  int base;          // prn * 2046 into the packed table
+};
+
+// Half-chip counter, table load index and epoch after r rollovers.
+__device__ __forceinline__ void hc_after(const Chan& c, uint64_t r, uint32_t& hc, uint32_t& ld,
+                                         uint32_t& epoch) {
+  if (r < c.j1) {
+    epoch = 0;
+    hc = (uint32_t)((c.hc0 + r) & 0xFFFFu);
+    ld = hc;
+  } else {
+    uint32_t m = (uint32_t)(r - c.j1);
+    epoch = 1 + m / c.D;
+    uint32_t q = m % c.D;
+    hc = q;
+    ld = q ? q : (m == 0 ? (uint32_t)((c.hc0 + c.j1) & 0xFFFFu) : c.D);
+  }
+}
+
+__device__ __forceinline__ uint32_t n_dumps_after(const Chan& c, uint64_t r) {
+  return r >= c.j1 ? 1 + (uint32_t)(r - c.j1) / c.D : 0u;
+}
+
+__device__ __forceinline__ void msbit_step(int& ms, int& bit) {
+  // correlator.c:275-280
+  ms++;
+  if (ms == 20) bit = (bit + 1) % 50;
+  ms %= 20;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ int sbyte(int x, int b) { return __builtin_amdgcn_sbfe(x, 8 * b, 8); }
+
+struct Acc {
+  uint32_t a[6];
+};
+
+template <bool IQ>
+__device__ __forceinline__ void corr_sample(int I, int Q, uint32_t& phase, uint32_t& kph,
+                                            const Chan& c, uint32_t& hc, int& lb, int& pb,
+                                            int& eb, Acc& cur, Acc& first, bool& switched,
+                                            const uint32_t* __restrict__ pk) {
+  const uint32_t off = (phase >> 27) & 0x1Cu;
+  const int il = __builtin_amdgcn_sbfe((int)kLutI, off, 4);
+  const int ql = __builtin_amdgcn_sbfe((int)kLutQ, off, 4);
+  int ival, qval;
+  if (IQ) {
+    ival = il * I + ql * Q;   // correlator.c:215
+    qval = ql * I - il * Q;   // correlator.c:214
+  } else {
+    ival = I * il;            // correlator.c:222-223
+    qval = I * ql;
+  }
+  cur.a[0] += (uint32_t)(lb * ival);
+  cur.a[1] += (uint32_t)(lb * qval);
+  cur.a[2] += (uint32_t)(pb * ival);
+  cur.a[3] += (uint32_t)(pb * qval);
+  cur.a[4] += (uint32_t)(eb * ival);
+  cur.a[5] += (uint32_t)(eb * qval);
+  phase += c.cinc;
+  const uint32_t nk = kph + c.kinc2;
+  const bool carry = nk < kph;
+  kph = nk;
+  if (carry) {
+    hc = (hc + 1u) & 0xFFFFu;
+    const uint32_t ld = hc;
+    if (hc >= c.D) {  // dump (correlator.c:251-281)
+#pragma unroll
+      for (int k = 0; k < 6; k++) { first.a[k] = cur.a[k]; cur.a[k] = 0; }
+      switched = true;
+      hc = 0;
+    }
+    const uint32_t w = pk[c.base + (int)ld];
+    lb = (int)(int8_t)(w & 0xFFu);
+    pb = (int)(int8_t)((w >> 8) & 0xFFu);
+    eb = (int)(int8_t)((w >> 16) & 0xFFu);
+  }
+}
+
+template <bool IQ>
+__global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
+    const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp,
+    const gnsscorr_nco_cmd* __restrict__ cmds, gnsscorr_chan_state* __restrict__ state,
+    gnsscorr_track_result* __restrict__ res, int32_t* __restrict__ all_dumps, int max_dumps,
+    const uint32_t* __restrict__ pk, int64_t tic_count) {
+  __shared__ int32_t s_sum[kMaxEpochs][6];
+  const int chn = blockIdx.x;
+  const gnsscorr_nco_cmd cmd = cmds[chn];
+  gnsscorr_chan_state st = state[chn];
+  if (cmd.epoch_load >= 0) {  // epoch set, correlator.c:177-182
+    const int v = cmd.epoch_load & 0xFFFF;
+    st.msbit_reg = v;
+    st.ms_counter = v & 0xff;
+    st.bit_counter = v >> 8;
+  }
+  if (cmd.prn <= 0 || cmd.prn > 32) {  // idle channel (correlator.c:185)
+    if (threadIdx.x == 0) {
+      gnsscorr_track_result r;
+      memset(&r, 0, sizeof r);
+      r.n_dumps = cmd.prn > 32 ? -1 : 0;
+      r.msbit_reg = st.msbit_reg;
+      res[chn] = r;
+      state[chn] = st;
+    }
+    return;
+  }
+
+  Chan c;
+  c.P0 = st.carrier_phase;
+  c.K0 = st.code_phase;
+  c.cinc = cmd.carrier_incr;
+  c.kinc2 = cmd.code_incr << 1;
+  c.hc0 = st.half_chip & 0xFFFFu;
+  c.D = (cmd.slew & 0xFFFFu) + 2046u;
+  {
+    const uint32_t h1 = (c.hc0 + 1u) & 0xFFFFu;
+    if (h1 >= c.D) c.j1 = 1;
+    else if (c.D <= 0xFFFFu) c.j1 = 1ull + (c.D - h1);
+    else c.j1 = kNever;  // uint16 half-chip can never reach D
+  }
+  c.base = cmd.prn * GNSSCORR_OSG_ROW;
+
+  const uint64_t Rtot = ((uint64_t)c.K0 + (uint64_t)nsamp * c.kinc2) >> 32;
+  const uint32_t ndump = n_dumps_after(c, Rtot);
+  const int n_epochs = (int)ndump + 1;
+
+  for (int i = threadIdx.x; i < n_epochs * 6; i += blockDim.x) (&s_sum[0][0])[i] = 0;
+  __syncthreads();
+
+  // ---- per-thread run of kRun samples --------------------------------------
+  Acc cur, first;
+#pragma unroll
+  for (int k = 0; k < 6; k++) { cur.a[k] = 0; first.a[k] = 0; }
+  bool switched = false;
+  int e0 = 0;
+  const int n0 = threadIdx.x * kRun;
+  if (n0 < nsamp) {
+    const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
+    uint32_t kph = (uint32_t)X;
+    uint32_t phase = c.P0 + (uint32_t)n0 * c.cinc;
+    uint32_t hc, ld, ep;
+    hc_after(c, X >> 32, hc, ld, ep);
+    e0 = (int)ep;
+    const uint32_t w = pk[c.base + (int)ld];
+    int lb = (int)(int8_t)(w & 0xFFu);
+    int pb = (int)(int8_t)((w >> 8) & 0xFFu);
+    int eb = (int)(int8_t)((w >> 16) & 0xFFu);
+    constexpr int kBps = IQ ? 2 : 1;
+    const int8_t* src = ifbuf + (int64_t)cmd.stream * stream_stride * kBps + (int64_t)n0 * kBps;
+    if (n0 + kRun <= nsamp) {
+      const int4* v = reinterpret_cast<const int4*>(src);
+      constexpr int kVec = kRun * kBps / 16;
+#pragma unroll
+      for (int j = 0; j < kVec; j++) {
+        const int4 q = v[j];
+        const int words[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int wd = 0; wd < 4; wd++) {
+          const int x = words[wd];
+          if (IQ) {
+            corr_sample<IQ>(sbyte(x, 0), sbyte(x, 1), phase, kph, c, hc, lb, pb, eb, cur, first,
+                            switched, pk);
+            corr_sample<IQ>(sbyte(x, 2), sbyte(x, 3), phase, kph, c, hc, lb, pb, eb, cur, first,
+                            switched, pk);
+          } else {
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+              corr_sample<IQ>(sbyte(x, b), 0, phase, kph, c, hc, lb, pb, eb, cur, first,
+                              switched, pk);
+          }
+        }
+      }
+    } else {
+      for (int n = n0; n < nsamp; n++) {
+        const int I = src[(n - n0) * kBps];
+        const int Q = IQ ? src[(n - n0) * kBps + 1] : 0;
+        corr_sample<IQ>(I, Q, phase, kph, c, hc, lb, pb, eb, cur, first, switched, pk);
+      }
+    }
+  }
+
+  // ---- epoch-segmented reduction ------------------------------------------
+  // thread contributes (e0, switched ? first : cur) and (e0+1, cur) if switched
+  const int e_hi_mine = e0 + (switched ? 1 : 0);
+  const int e_lo = wave_min(n0 < nsamp ? e0 : 0x7fffffff);
+  const int e_hi = wave_max(n0 < nsamp ? e_hi_mine : -1);
+  const int lane = threadIdx.x & 63;
+  for (int e = e_lo; e <= e_hi; e++) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      uint32_t v = 0;
+      if (e == e0) v += switched ? first.a[k] : cur.a[k];
+      if (switched && e == e0 + 1) v += cur.a[k];
+      const int s = wave_sum((int)v);
+      if (lane == 0) atomicAdd(&s_sum[e][k], s);
+    }
+  }
+  __syncthreads();
+
+  // ---- per-channel epilogue (one thread) ------------------------------------
+  if (threadIdx.x != 0) return;
+  gnsscorr_track_result r;
+  memset(&r, 0, sizeof r);
+  r.n_dumps = (int)ndump;
+  int ms = st.ms_counter, bit = st.bit_counter, msbit = st.msbit_reg;
+
+  const bool tic_here = tic_count >= 0 && tic_count < nsamp;
+  uint32_t nd_tic = 0;
+  uint64_t Rt = 0;
+  if (tic_here) {
+    Rt = ((uint64_t)c.K0 + (uint64_t)(tic_count + 1) * c.kinc2) >> 32;
+    nd_tic = n_dumps_after(c, Rt);
+  }
+  int msbit_at_tic = msbit;
+  for (uint32_t d = 0; d < ndump; d++) {
+    uint32_t v[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+      v[k] = (uint32_t)s_sum[d][k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
+    if (all_dumps && (int)d < max_dumps)
+      for (int k = 0; k < 6; k++) all_dumps[((int64_t)chn * max_dumps + d) * 6 + k] = (int32_t)v[k];
+    if (d + 1 == ndump)
+      for (int k = 0; k < 6; k++) r.dump[k] = (int32_t)v[k];
+    msbit_step(ms, bit);
+    msbit = ms + (bit << 8);
+    if (d + 1 == nd_tic) msbit_at_tic = msbit;
+  }
+  uint32_t nacc[6];
+  for (int k = 0; k < 6; k++)
+    nacc[k] = (uint32_t)s_sum[ndump][k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
+
+  const uint64_t Wtot = ((uint64_t)c.P0 + (uint64_t)nsamp * c.cinc) >> 32;
+  uint32_t cycle_end;
+  if (tic_here) {  // TIC latch after sample tic_count (correlator.c:286-303)
+    const uint64_t t1 = (uint64_t)tic_count + 1;
+    const uint64_t Wt = ((uint64_t)c.P0 + t1 * c.cinc) >> 32;
+    const uint32_t cyc = st.carrier_cycle + (uint32_t)Wt;
+    uint32_t hct, ldt, ept;
+    hc_after(c, Rt, hct, ldt, ept);
+    r.tic = 1;
+    r.tic_regs[0] = (int32_t)hct;
+    r.tic_regs[1] = (int32_t)(cyc & 0xffffu);
+    r.tic_regs[2] = (int32_t)((c.P0 + (uint32_t)t1 * c.cinc) >> 22);
+    r.tic_regs[3] = msbit_at_tic;
+    r.tic_regs[4] = (int32_t)((uint32_t)((uint64_t)c.K0 + t1 * c.kinc2) >> 22);
+    r.tic_regs[5] = (int32_t)(cyc >> 16);
+    cycle_end = (uint32_t)(Wtot - Wt);
+  } else {
+    cycle_end = st.carrier_cycle + (uint32_t)Wtot;
+  }
+  uint32_t hce, lde, epe;
+  hc_after(c, Rtot, hce, lde, epe);
+
+  r.msbit_reg = msbit;
+  res[chn] = r;
+
+  st.carrier_phase = c.P0 + (uint32_t)nsamp * c.cinc;
+  st.carrier_cycle = cycle_end;
+  st.code_phase = (uint32_t)((uint64_t)c.K0 + (uint64_t)nsamp * c.kinc2);
+  st.half_chip = hce;
+  for (int k = 0; k < 6; k++) st.acc[k] = (int32_t)nacc[k];
+  st.ms_counter = ms;
+  st.bit_counter = bit;
+  st.msbit_reg = msbit;
+  state[chn] = st;
+}
+
+}  // namespace
+
+// ============================================================================
+// context / C ABI
+// ============================================================================
+struct gnsscorr_track_ctx {
+  gnsscorr_track_cfg cfg;
+  hipStream_t stream = nullptr;
+  uint32_t* d_pk = nullptr;
+  gnsscorr_chan_state* d_state = nullptr;
+  gnsscorr_nco_cmd* d_cmds = nullptr;
+  gnsscorr_track_result* d_res = nullptr;
+  int32_t* d_dumps = nullptr;
+  int8_t* d_if = nullptr;
+  size_t if_cap = 0;
+  int max_dumps = 0;
+  int64_t tic = 0, tic_ref = 0;
+};
+
+static int set_dev(int dev) {
+  HIP_TRY(hipSetDevice(dev));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_track_cfg* cfg) {
+  if (!out || !cfg || cfg->n_channels < 1 || cfg->max_nsamp < 1 || cfg->max_nsamp > kMaxNsamp) {
+    gnsscorr_set_error("gnsscorr_track_create: bad config (n_channels>=1, 1<=max_nsamp<=%d)",
+                       kMaxNsamp);
+    return GNSSCORR_EINVAL;
+  }
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    gnsscorr_set_error("gnsscorr_track_create: no HIP device");
+    return GNSSCORR_ENODEV;
+  }
+  if (cfg->device < 0 || cfg->device >= ndev) {
+    gnsscorr_set_error("gnsscorr_track_create: device %d out of range", cfg->device);
+    return GNSSCORR_EINVAL;
+  }
+  int rc = set_dev(cfg->device);
+  if (rc) return rc;
+  auto* c = new gnsscorr_track_ctx();
+  c->cfg = *cfg;
+  c->max_dumps = cfg->max_nsamp / GNSSCORR_OSG_ROW + 2;
+  c->tic_ref = (int64_t)(cfg->samp_rate * cfg->tic_period);
+  c->tic = c->tic_ref;
+  const int C = cfg->n_channels;
+  auto fail = [&](int code) {
+    gnsscorr_track_destroy(c);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_pk, sizeof(uint32_t) * GNSSCORR_OSG_PK_LEN) != hipSuccess ||
+      hipMalloc(&c->d_state, sizeof(gnsscorr_chan_state) * C) != hipSuccess ||
+      hipMalloc(&c->d_cmds, sizeof(gnsscorr_nco_cmd) * C) != hipSuccess ||
+      hipMalloc(&c->d_res, sizeof(gnsscorr_track_result) * C) != hipSuccess ||
+      hipMalloc(&c->d_dumps, sizeof(int32_t) * 6 * (size_t)C * c->max_dumps) != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_track_create: device allocation failed");
+    return fail(GNSSCORR_ENOMEM);
+  }
+  uint32_t* pk = (uint32_t*)malloc(sizeof(uint32_t) * GNSSCORR_OSG_PK_LEN);
+  if (!pk) return fail(GNSSCORR_ENOMEM);
+  gnsscorr_osg_packed_table(pk);
+  hipError_t e = hipMemcpy(c->d_pk, pk, sizeof(uint32_t) * GNSSCORR_OSG_PK_LEN, hipMemcpyHostToDevice);
+  free(pk);
+  if (e != hipSuccess || hipMemset(c->d_state, 0, sizeof(gnsscorr_chan_state) * C) != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_track_create: upload failed: %s", hipGetErrorString(e));
+    return fail(GNSSCORR_EDEVICE);
+  }
+  *out = c;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track_destroy(gnsscorr_track_ctx* c) {
+  if (!c) return GNSSCORR_OK;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->d_pk, c->d_state, c->d_cmds, c->d_res, c->d_dumps, c->d_if};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track_max_dumps(const gnsscorr_track_ctx* c) { return c ? c->max_dumps : 0; }
+
+extern "C" int64_t gnsscorr_track_next_tic(gnsscorr_track_ctx* c, int64_t nsamp) {
+  // correlator.c:155-165
+  if (c->tic < nsamp) {
+    const int64_t t = c->tic;
+    c->tic += c->tic_ref - nsamp;
+    return t;
+  }
+  c->tic -= nsamp;
+  return -1;
+}
+
+static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int64_t nsamp,
+                  const gnsscorr_nco_cmd* d_cmds, gnsscorr_track_result* d_res,
+                  int32_t* d_dumps, int64_t tic_count) {
+  if (nsamp < 1 || nsamp > c->cfg.max_nsamp) {
+    gnsscorr_set_error("nsamp %lld outside [1, max_nsamp=%d]", (long long)nsamp, c->cfg.max_nsamp);
+    return GNSSCORR_EINVAL;
+  }
+  const int bps = c->cfg.iq ? 2 : 1;
+  if (((uintptr_t)d_if & 15) || ((stride * bps) & 15)) {
+    gnsscorr_set_error("IF base and stream stride must be 16-byte aligned");
+    return GNSSCORR_EINVAL;
+  }
+  int threads = (int)((nsamp + kRun - 1) / kRun);
+  threads = (threads + 63) & ~63;
+  dim3 grid(c->cfg.n_channels), block(threads);
+  if (c->cfg.iq)
+    hipLaunchKernelGGL(osg_track_kernel<true>, grid, block, 0, c->stream, d_if, stride,
+                       (int)nsamp, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps, c->d_pk,
+                       tic_count);
+  else
+    hipLaunchKernelGGL(osg_track_kernel<false>, grid, block, 0, c->stream, d_if, stride,
+                       (int)nsamp, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps, c->d_pk,
+                       tic_count);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track(gnsscorr_track_ctx* c, const int8_t* h_if, int64_t stride,
+                              int n_streams, int64_t nsamp, const gnsscorr_nco_cmd* h_cmds,
+                              gnsscorr_track_result* h_res, int32_t* h_all_dumps, int* tic_fired) {
+  if (!c || !h_if || !h_cmds || !h_res || n_streams < 1 || nsamp < 1) {
+    gnsscorr_set_error("gnsscorr_track: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  const int C = c->cfg.n_channels;
+  for (int i = 0; i < C; i++) {
+    if (h_cmds[i].prn < 0 || h_cmds[i].prn > 32 || h_cmds[i].stream < 0 ||
+        h_cmds[i].stream >= n_streams) {
+      gnsscorr_set_error("gnsscorr_track: channel %d: prn %d / stream %d invalid", i,
+                         h_cmds[i].prn, h_cmds[i].stream);
+      return GNSSCORR_EINVAL;
+    }
+  }
+  if (n_streams == 1) stride = 0;
+  if (n_streams > 1 && stride < nsamp) {
+    gnsscorr_set_error("gnsscorr_track: stream_stride < nsamp");
+    return GNSSCORR_EINVAL;
+  }
+  int rc = set_dev(c->cfg.device);
+  if (rc) return rc;
+  const int bps = c->cfg.iq ? 2 : 1;
+  // device copy with a 16-byte aligned stride
+  const int64_t dstride = n_streams > 1 ? ((stride * bps + 15) & ~15LL) / bps : 0;
+  const size_t need = (size_t)((n_streams - 1) * dstride + ((nsamp * bps + 15) & ~15LL) / bps) * bps;
+  if (need > c->if_cap) {
+    if (c->d_if) (void)hipFree(c->d_if);
+    c->d_if = nullptr;
+    c->if_cap = 0;
+    HIP_TRY(hipMalloc(&c->d_if, need));
+    c->if_cap = need;
+  }
+  if (n_streams == 1 || dstride == stride) {
+    HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)((n_streams - 1) * stride + nsamp) * bps,
+                           hipMemcpyHostToDevice, c->stream));
+  } else {
+    HIP_TRY(hipMemcpy2DAsync(c->d_if, dstride * bps, h_if, stride * bps, nsamp * bps, n_streams,
+                             hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_TRY(hipMemcpyAsync(c->d_cmds, h_cmds, sizeof(gnsscorr_nco_cmd) * C, hipMemcpyHostToDevice,
+                         c->stream));
+  const int64_t tic = gnsscorr_track_next_tic(c, nsamp);
+  rc = launch(c, c->d_if, dstride, nsamp, c->d_cmds, c->d_res, h_all_dumps ? c->d_dumps : nullptr,
+              tic);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(h_res, c->d_res, sizeof(gnsscorr_track_result) * C,
+                         hipMemcpyDeviceToHost, c->stream));
+  if (h_all_dumps)
+    HIP_TRY(hipMemcpyAsync(h_all_dumps, c->d_dumps, sizeof(int32_t) * 6 * (size_t)C * c->max_dumps,
+                           hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (tic_fired) *tic_fired = tic >= 0;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track_dev(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride,
+                                  int64_t nsamp, const gnsscorr_nco_cmd* d_cmds,
+                                  gnsscorr_track_result* d_res, int32_t* d_all_dumps,
+                                  int64_t tic_count) {
+  if (!c || !d_if || !d_cmds || !d_res) {
+    gnsscorr_set_error("gnsscorr_track_dev: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  int rc = set_dev(c->cfg.device);
+  if (rc) return rc;
+  return launch(c, d_if, stride, nsamp, d_cmds, d_res, d_all_dumps, tic_count);
+}
+
+extern "C" int gnsscorr_track_replay_dev(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride,
+                                         int64_t nsamp, int n_steps,
+                                         const gnsscorr_nco_cmd* d_cmds,
+                                         gnsscorr_track_result* d_res) {
+  if (!c || !d_if || !d_cmds || !d_res || n_steps < 1) {
+    gnsscorr_set_error("gnsscorr_track_replay_dev: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  int rc = set_dev(c->cfg.device);
+  if (rc) return rc;
+  const int bps = c->cfg.iq ? 2 : 1;
+  const int C = c->cfg.n_channels;
+  for (int k = 0; k < n_steps; k++) {
+    const int64_t tic = gnsscorr_track_next_tic(c, nsamp);
+    rc = launch(c, d_if + (int64_t)k * nsamp * bps, stride, nsamp, d_cmds + (int64_t)k * C,
+                d_res + (int64_t)k * C, nullptr, tic);
+    if (rc) return rc;
+  }
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track_get_state(gnsscorr_track_ctx* c, gnsscorr_chan_state* h) {
+  if (!c || !h) return GNSSCORR_EINVAL;
+  int rc = set_dev(c->cfg.device);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(h, c->d_state, sizeof(gnsscorr_chan_state) * c->cfg.n_channels,
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track_set_state(gnsscorr_track_ctx* c, const gnsscorr_chan_state* h) {
+  if (!c || !h) return GNSSCORR_EINVAL;
+  int rc = set_dev(c->cfg.device);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_state, h, sizeof(gnsscorr_chan_state) * c->cfg.n_channels,
+                         hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_track_sync(gnsscorr_track_ctx* c) {
+  if (!c) return GNSSCORR_EINVAL;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" void* gnsscorr_track_stream(gnsscorr_track_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int gnsscorr_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}

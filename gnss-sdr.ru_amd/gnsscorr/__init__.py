@@ -1,0 +1,416 @@
+"""gnsscorr -- Python (ctypes) view of libgnsscorr.so, the MI355X GNSS correlator.
+
+This module is plumbing for tests and benchmarks: every computation happens in
+the HIP kernels behind the C ABI declared in include/gnsscorr.h.  There is no
+CPU fallback -- if the shared library (or a GPU, for compute calls) is
+missing, the calls raise.
+
+Two views are provided:
+
+* ``TrackCtx`` / ``AcqCtx``: the batched API (explicit state, many channels).
+* ``OSG``: the reference's GP2021 register interface (correlator_init,
+  Sim_GP2021_int, REG_read/REG_write + the gp2021.c accessors ch_carrier,
+  ch_code, ch_code_slew, ch_cntl, ch_epoch_load, ch_{i,q}_{early,prompt,late},
+  accum_status), so host-loop tests read like the reference's own
+  osgnss_next_step.c main loop.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgnsscorr.so")
+
+# ---------------------------------------------------------------- structs
+NCO_CMD = np.dtype([("prn", "<i4"), ("carrier_incr", "<u4"), ("code_incr", "<u4"),
+                    ("slew", "<u4"), ("epoch_load", "<i4"), ("stream", "<i4")])
+CHAN_STATE = np.dtype([("carrier_phase", "<u4"), ("carrier_cycle", "<u4"),
+                       ("code_phase", "<u4"), ("half_chip", "<u4"), ("acc", "<i4", (6,)),
+                       ("ms_counter", "<i4"), ("bit_counter", "<i4"), ("msbit_reg", "<i4"),
+                       ("pad", "<i4")])
+TRACK_RESULT = np.dtype([("n_dumps", "<i4"), ("dump", "<i4", (6,)), ("msbit_reg", "<i4"),
+                         ("tic", "<i4"), ("tic_regs", "<i4", (6,)), ("pad", "<i4")])
+ACQ_ROW = np.dtype([("peak", "<f4"), ("argmax", "<i4"), ("second", "<f4"), ("block", "<i4")])
+ACQ_RESULT = np.dtype([("peak", "<f4"), ("second", "<f4"), ("metric", "<f4"), ("bin", "<i4"),
+                       ("code_phase", "<i4"), ("pad", "<i4"), ("carr_freq", "<f8")])
+SIG = np.dtype([("system", "<i4"), ("prn", "<i4"), ("fch", "<i4"), ("data_bits", "<i4"),
+                ("code_phase", "<f8"), ("doppler", "<f8"), ("cn0", "<f8"),
+                ("carr_phase", "<f8")])
+assert NCO_CMD.itemsize == 24 and CHAN_STATE.itemsize == 56 and TRACK_RESULT.itemsize == 64
+assert ACQ_ROW.itemsize == 16 and ACQ_RESULT.itemsize == 32 and SIG.itemsize == 48
+
+ACQ_BEST_OF_BLOCKS = 0
+ACQ_NONCOHERENT = 1
+
+
+class TrackCfg(C.Structure):
+    _fields_ = [("n_channels", C.c_int), ("iq", C.c_int), ("device", C.c_int),
+                ("max_nsamp", C.c_int), ("samp_rate", C.c_double), ("tic_period", C.c_double)]
+
+
+class AcqCfg(C.Structure):
+    _fields_ = [("samp_rate", C.c_double), ("n_samples", C.c_int), ("device", C.c_int),
+                ("max_freqs", C.c_int), ("max_blocks", C.c_int), ("max_codes", C.c_int)]
+
+
+# every symbol include/gnsscorr.h + include/gnsscorr_osg.h declare
+EXPORTED_FUNCTIONS = [
+    "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
+    "gnsscorr_track_create", "gnsscorr_track_destroy", "gnsscorr_track_max_dumps",
+    "gnsscorr_track", "gnsscorr_track_dev", "gnsscorr_track_next_tic",
+    "gnsscorr_track_replay_dev", "gnsscorr_track_get_state", "gnsscorr_track_set_state",
+    "gnsscorr_track_sync", "gnsscorr_track_stream",
+    "gnsscorr_acq_create", "gnsscorr_acq_destroy", "gnsscorr_acq_set_codes",
+    "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
+    "gnsscorr_acq_sync", "gnsscorr_acq_stream",
+    "gnsscorr_ifgen", "gnsscorr_ca_code", "gnsscorr_st_code", "gnsscorr_sample_code",
+    "correlator_init", "Sim_GP2021_int", "gnsscorr_osg_configure", "gnsscorr_osg_get_state",
+]
+EXPORTED_DATA = ["REG_read", "REG_write", "Carrier_DCO_Delta", "Code_DCO_Delta",
+                 "gps_code_ref", "gps_carrier_ref", "glonass_code_ref",
+                 "glonass_carrier_ref", "d_freq"]
+
+_lib = None
+
+
+class GnssCorrError(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """Load libgnsscorr.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GnssCorrError(f"{LIB_PATH} not built (run `make -C gnss-sdr.ru_amd`)")
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    P, I, I64, D, U64 = C.c_void_p, C.c_int, C.c_int64, C.c_double, C.c_uint64
+    sig = {
+        "gnsscorr_last_error": (C.c_char_p, []),
+        "gnsscorr_version": (C.c_char_p, []),
+        "gnsscorr_device_count": (I, []),
+        "gnsscorr_track_create": (I, [C.POINTER(P), C.POINTER(TrackCfg)]),
+        "gnsscorr_track_destroy": (I, [P]),
+        "gnsscorr_track_max_dumps": (I, [P]),
+        "gnsscorr_track": (I, [P, P, I64, I, I64, P, P, P, C.POINTER(I)]),
+        "gnsscorr_track_dev": (I, [P, P, I64, I64, P, P, P, I64]),
+        "gnsscorr_track_next_tic": (I64, [P, I64]),
+        "gnsscorr_track_replay_dev": (I, [P, P, I64, I64, I, P, P]),
+        "gnsscorr_track_get_state": (I, [P, P]),
+        "gnsscorr_track_set_state": (I, [P, P]),
+        "gnsscorr_track_sync": (I, [P]),
+        "gnsscorr_track_stream": (P, [P]),
+        "gnsscorr_acq_create": (I, [C.POINTER(P), C.POINTER(AcqCfg)]),
+        "gnsscorr_acq_destroy": (I, [P]),
+        "gnsscorr_acq_set_codes": (I, [P, I, P]),
+        "gnsscorr_acq_search": (I, [P, P, I, I, I, I, P, I, I, P, P, I, P, P]),
+        "gnsscorr_acq_search_dev": (I, [P, P, I, I, I, I, P, I, I, P, P, I, P, P]),
+        "gnsscorr_acq_power_row": (I, [P, P, I, I, I, D, I, P]),
+        "gnsscorr_acq_sync": (I, [P]),
+        "gnsscorr_acq_stream": (P, [P]),
+        "gnsscorr_ifgen": (I, [P, I64, I, D, D, D, I, P, U64]),
+        "gnsscorr_ca_code": (I, [I, P]),
+        "gnsscorr_st_code": (I, [P]),
+        "gnsscorr_sample_code": (I, [P, I, D, D, I, P]),
+        "correlator_init": (None, [D]),
+        "Sim_GP2021_int": (None, [P, C.c_long]),
+        "gnsscorr_osg_configure": (I, [D, D, D, D, I, I, I, I, D, I]),
+        "gnsscorr_osg_get_state": (I, [P]),
+    }
+    for name, (res, args) in sig.items():
+        if not hasattr(L, name):
+            continue  # reported by tests/test_abi.py
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().gnsscorr_last_error().decode(errors="replace")
+        raise GnssCorrError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    return int(lib().gnsscorr_device_count())
+
+
+# ---------------------------------------------------------------- host utils
+def ca_code(prn: int) -> np.ndarray:
+    out = np.empty(1023, np.int8)
+    _check(lib().gnsscorr_ca_code(prn, _ptr(out)), "gnsscorr_ca_code")
+    return out
+
+
+def st_code() -> np.ndarray:
+    out = np.empty(511, np.int8)
+    _check(lib().gnsscorr_st_code(_ptr(out)), "gnsscorr_st_code")
+    return out
+
+
+def sample_code(chips: np.ndarray, code_rate: float, fs: float, n: int) -> np.ndarray:
+    chips = np.ascontiguousarray(chips, np.int8)
+    out = np.empty(n, np.int8)
+    _check(lib().gnsscorr_sample_code(_ptr(chips), len(chips), code_rate, fs, n, _ptr(out)),
+           "gnsscorr_sample_code")
+    return out
+
+
+def make_sigs(sigs) -> np.ndarray:
+    """sigs: list of dicts with keys of SIG (missing keys default to 0)."""
+    a = np.zeros(len(sigs), SIG)
+    for i, s in enumerate(sigs):
+        for k, v in s.items():
+            a[i][k] = v
+    return a
+
+
+def ifgen(nsamp: int, sigs=(), fs=16.368e6, if_gps=2.42e6, if_glo=1.0e6, iq=True,
+          seed=0x5EED0000) -> np.ndarray:
+    """Deterministic synthetic 2-bit IF as int8 (interleaved I,Q when iq)."""
+    sa = make_sigs(sigs) if not isinstance(sigs, np.ndarray) else sigs
+    out = np.empty(nsamp * (2 if iq else 1), np.int8)
+    _check(lib().gnsscorr_ifgen(_ptr(out), nsamp, int(iq), fs, if_gps, if_glo, len(sa),
+                                _ptr(sa) if len(sa) else None, seed), "gnsscorr_ifgen")
+    return out
+
+
+# ---------------------------------------------------------------- tracking
+class TrackCtx:
+    """Batched GP2021-semantics tracking correlator context (one per GPU)."""
+
+    def __init__(self, n_channels: int, iq: bool = True, device: int = 0,
+                 max_nsamp: int = 65536, samp_rate: float = 16.368e6,
+                 tic_period: float = 0.0):
+        self.n_channels = n_channels
+        self.iq = bool(iq)
+        cfg = TrackCfg(n_channels, int(iq), device, max_nsamp, samp_rate, tic_period)
+        h = C.c_void_p()
+        _check(lib().gnsscorr_track_create(C.byref(h), C.byref(cfg)), "gnsscorr_track_create")
+        self.h = h
+        self.max_dumps = lib().gnsscorr_track_max_dumps(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gnsscorr_track_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def track(self, if_samples: np.ndarray, nsamp: int, cmds: np.ndarray, n_streams: int = 1,
+              stream_stride: int = 0, all_dumps: bool = False):
+        if_samples = np.ascontiguousarray(if_samples, np.int8)
+        cmds = np.ascontiguousarray(cmds, NCO_CMD)
+        assert len(cmds) == self.n_channels
+        res = np.zeros(self.n_channels, TRACK_RESULT)
+        dumps = np.zeros((self.n_channels, self.max_dumps, 6), np.int32) if all_dumps else None
+        tic = C.c_int(0)
+        _check(lib().gnsscorr_track(self.h, _ptr(if_samples), stream_stride, n_streams, nsamp,
+                                    _ptr(cmds), _ptr(res),
+                                    _ptr(dumps) if dumps is not None else None, C.byref(tic)),
+               "gnsscorr_track")
+        return (res, bool(tic.value), dumps) if all_dumps else (res, bool(tic.value))
+
+    def track_dev(self, d_if: int, stream_stride: int, nsamp: int, d_cmds: int, d_res: int,
+                  d_dumps: int = 0, tic_count: int = -1):
+        _check(lib().gnsscorr_track_dev(self.h, d_if, stream_stride, nsamp, d_cmds, d_res,
+                                        d_dumps or None, tic_count), "gnsscorr_track_dev")
+
+    def replay_dev(self, d_if: int, stream_stride: int, nsamp: int, n_steps: int, d_cmds: int,
+                   d_res: int):
+        _check(lib().gnsscorr_track_replay_dev(self.h, d_if, stream_stride, nsamp, n_steps,
+                                               d_cmds, d_res), "gnsscorr_track_replay_dev")
+
+    def next_tic(self, nsamp: int) -> int:
+        return int(lib().gnsscorr_track_next_tic(self.h, nsamp))
+
+    def get_state(self) -> np.ndarray:
+        st = np.zeros(self.n_channels, CHAN_STATE)
+        _check(lib().gnsscorr_track_get_state(self.h, _ptr(st)), "gnsscorr_track_get_state")
+        return st
+
+    def set_state(self, st: np.ndarray):
+        st = np.ascontiguousarray(st, CHAN_STATE)
+        _check(lib().gnsscorr_track_set_state(self.h, _ptr(st)), "gnsscorr_track_set_state")
+
+    def sync(self):
+        _check(lib().gnsscorr_track_sync(self.h), "gnsscorr_track_sync")
+
+    @property
+    def stream(self) -> int:
+        return lib().gnsscorr_track_stream(self.h)
+
+
+# ---------------------------------------------------------------- acquisition
+class AcqCtx:
+    """Parallel code-phase acquisition context (SoftGNSS acquisition.sci semantics)."""
+
+    def __init__(self, samp_rate: float = 16.368e6, n_samples: int = 16368, device: int = 0,
+                 max_freqs: int = 1024, max_blocks: int = 16, max_codes: int = 64):
+        cfg = AcqCfg(samp_rate, n_samples, device, max_freqs, max_blocks, max_codes)
+        h = C.c_void_p()
+        _check(lib().gnsscorr_acq_create(C.byref(h), C.byref(cfg)), "gnsscorr_acq_create")
+        self.h = h
+        self.n = n_samples
+        self.fs = samp_rate
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gnsscorr_acq_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def set_codes(self, codes: np.ndarray):
+        codes = np.ascontiguousarray(codes, np.int8).reshape(-1, self.n)
+        _check(lib().gnsscorr_acq_set_codes(self.h, codes.shape[0], _ptr(codes)),
+               "gnsscorr_acq_set_codes")
+
+    def search(self, if_samples, n_blocks, freqs, group_code, group_freq, spc=16, iq=True,
+               mode=ACQ_BEST_OF_BLOCKS):
+        if_samples = np.ascontiguousarray(if_samples, np.int8)
+        freqs = np.ascontiguousarray(freqs, np.float64)
+        group_code = np.ascontiguousarray(group_code, np.int32)
+        group_freq = np.ascontiguousarray(group_freq, np.int32).reshape(len(group_code), -1)
+        G, B = group_freq.shape
+        rows = np.zeros(G * B, ACQ_ROW)
+        res = np.zeros(G, ACQ_RESULT)
+        _check(lib().gnsscorr_acq_search(self.h, _ptr(if_samples), int(iq), n_blocks, mode,
+                                         len(freqs), _ptr(freqs), G, B, _ptr(group_code),
+                                         _ptr(group_freq), spc, _ptr(rows), _ptr(res)),
+               "gnsscorr_acq_search")
+        return res, rows.reshape(G, B)
+
+    def search_dev(self, d_if, n_blocks, n_freqs, d_freqs, n_groups, n_bins, d_group_code,
+                   d_group_freq, d_rows, d_res, spc=16, iq=True, mode=ACQ_BEST_OF_BLOCKS):
+        _check(lib().gnsscorr_acq_search_dev(self.h, d_if, int(iq), n_blocks, mode, n_freqs,
+                                             d_freqs, n_groups, n_bins, d_group_code,
+                                             d_group_freq, spc, d_rows, d_res),
+               "gnsscorr_acq_search_dev")
+
+    def power_row(self, if_samples, n_blocks, block, freq, code, iq=True) -> np.ndarray:
+        if_samples = np.ascontiguousarray(if_samples, np.int8)
+        out = np.empty(self.n, np.float32)
+        _check(lib().gnsscorr_acq_power_row(self.h, _ptr(if_samples), int(iq), n_blocks, block,
+                                            freq, code, _ptr(out)), "gnsscorr_acq_power_row")
+        return out
+
+    def sync(self):
+        _check(lib().gnsscorr_acq_sync(self.h), "gnsscorr_acq_sync")
+
+    @property
+    def stream(self) -> int:
+        return lib().gnsscorr_acq_stream(self.h)
+
+
+# ---------------------------------------------------------------- legacy OSG view
+class OSG:
+    """The reference's GP2021 register interface, backed by libgnsscorr.
+
+    Accessors mirror osgnss_next_step/src/gp2021/gp2021.c:11-130 (same
+    arithmetic, including the NCO word scaling and the `short` truncation of
+    from_gps)."""
+
+    MAX_DIGIT = 32
+
+    def __init__(self, samp_rate=16.0e6, gps_if=2.42e6, glonass_if=0.0, sys_clock_mult=5.0,
+                 carrier_bits=30, code_bits=29, n_channels=12, use_iq=True,
+                 freq_bin_width=1000.0, device=0):
+        L = lib()
+        _check(L.gnsscorr_osg_configure(samp_rate, gps_if, glonass_if, sys_clock_mult,
+                                        carrier_bits, code_bits, n_channels, int(use_iq),
+                                        freq_bin_width, device), "gnsscorr_osg_configure")
+        self.mult = sys_clock_mult
+        self.n_channels = n_channels
+        self.carrier_bits = carrier_bits
+        self.code_bits = code_bits
+        self.REG_read = (C.c_int * 256).in_dll(L, "REG_read")
+        self.REG_write = (C.c_int * 256).in_dll(L, "REG_write")
+
+    def get_state(self, n_channels: int = 12) -> np.ndarray:
+        st = np.zeros(n_channels, CHAN_STATE)
+        _check(lib().gnsscorr_osg_get_state(_ptr(st)), "gnsscorr_osg_get_state")
+        return st
+
+    def chan_state(self):
+        st = self.get_state(self.n_channels)
+        return dict(carrier_phase=st["carrier_phase"].copy(),
+                    carrier_cycle=st["carrier_cycle"].copy(),
+                    code_phase=st["code_phase"].copy(), half_chip=st["half_chip"].copy(),
+                    acc=st["acc"].copy())
+
+    def correlator_init(self, tic_period: float = 0.0):
+        lib().correlator_init(tic_period)
+
+    def sim(self, IF: np.ndarray, nsamp: int):
+        IF = np.ascontiguousarray(IF, np.int8)
+        lib().Sim_GP2021_int(_ptr(IF), nsamp)
+
+    @property
+    def gps_carrier_ref(self):
+        return C.c_long.in_dll(lib(), "gps_carrier_ref").value
+
+    @property
+    def gps_code_ref(self):
+        return C.c_long.in_dll(lib(), "gps_code_ref").value
+
+    @property
+    def d_freq(self):
+        return C.c_long.in_dll(lib(), "d_freq").value
+
+    # --- gp2021.c accessors ---
+    def _outpwd(self, add, data):
+        self.REG_write[add & 0xFF] = int(data) & 0xFFFF
+
+    def _from_gps(self, add):
+        v = self.REG_read[add] & 0xFFFF
+        return v - 0x10000 if v >= 0x8000 else v
+
+    def ch_cntl(self, ch, data):
+        self._outpwd(ch << 3, data)
+
+    def ch_code_slew(self, ch, data):
+        self._outpwd((ch << 3) + 0x84, data)
+
+    def ch_epoch_load(self, ch, data):
+        self._outpwd((ch << 3) + 7, data)
+
+    def ch_carrier(self, ch, freq):
+        f = int(float(freq << (self.MAX_DIGIT - self.carrier_bits)) * self.mult)
+        self._outpwd((ch << 3) + 3, (f >> 16) & 0xFFFF)
+        self._outpwd((ch << 3) + 4, f & 0xFFFF)
+
+    def ch_code(self, ch, freq):
+        f = int(float(freq << (self.MAX_DIGIT - self.code_bits)) * self.mult)
+        self._outpwd((ch << 3) + 5, (f >> 16) & 0xFFFF)
+        self._outpwd((ch << 3) + 6, f & 0xFFFF)
+
+    def accum_status(self):
+        return self._from_gps(0x82)
+
+    def ch_i_late(self, ch):
+        return self._from_gps((ch << 3) + 0x84)
+
+    def ch_q_late(self, ch):
+        return self._from_gps((ch << 3) + 0x85)
+
+    def ch_i_prompt(self, ch):
+        return self._from_gps((ch << 3) + 0x86)
+
+    def ch_q_prompt(self, ch):
+        return self._from_gps((ch << 3) + 0x87)
+
+    def ch_i_early(self, ch):
+        return self._from_gps((ch << 3) + 0x88)
+
+    def ch_q_early(self, ch):
+        return self._from_gps((ch << 3) + 0x89)

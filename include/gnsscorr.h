@@ -1,0 +1,243 @@
+/*
+ * gnsscorr.h -- C ABI of the MI355X-native GNSS correlator (libgnsscorr.so).
+ *
+ * Two layers:
+ *
+ *  1. Batched API (gnsscorr_*): explicit contexts, explicit per-channel state,
+ *     device- or host-resident IF buffers, status codes.  Used by the legacy
+ *     shim below, by bench.py and by multi-GPU runners.
+ *
+ *  2. Legacy OSGPS register API (include/gnsscorr_osg.h): the exact symbols
+ *     the reference's host side links against
+ *       correlator_init / Sim_GP2021_int / REG_read / REG_write
+ *     (reference osgnss_next_step/src/correlator/correlator.h:4-9), so the
+ *     reference gp2021.c accessors and osgpsisr.c DLL/PLL link unchanged.
+ *
+ * All functions return 0 on success or a negative GNSSCORR_E* code.
+ * Pointers named d_* are HIP device pointers; h_* are host pointers.
+ * No torch types cross this boundary.
+ */
+#ifndef GNSSCORR_H
+#define GNSSCORR_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNSSCORR_OK           0
+#define GNSSCORR_EINVAL      -1   /* bad argument / shape                          */
+#define GNSSCORR_ENOMEM      -2   /* device or host allocation failed              */
+#define GNSSCORR_EDEVICE     -3   /* HIP runtime error (see gnsscorr_last_error)   */
+#define GNSSCORR_ENODEV      -4   /* no HIP device visible                         */
+
+/* Human-readable description of the last error on this thread. */
+const char *gnsscorr_last_error(void);
+/* Library version string. */
+const char *gnsscorr_version(void);
+/* Number of visible HIP devices (0 on a CPU-only host; never initialises
+ * more than hipGetDeviceCount does). */
+int gnsscorr_device_count(void);
+
+/* ======================================================================
+ * Tracking correlator (GP2021 integer semantics)
+ * Replaces: Sim_GP2021_int, osgnss_next_step/src/correlator/correlator.c:148-316
+ * ==================================================================== */
+
+#define GNSSCORR_OSG_ROW 2046      /* half-chips per C/A period */
+
+typedef struct gnsscorr_track_ctx gnsscorr_track_ctx;
+
+typedef struct {
+  int    n_channels;     /* channels in this context (any number >= 1)           */
+  int    iq;             /* 1: interleaved int8 I,Q (use_iq_processing=1, globals.h:56)
+                            0: int8 I only                                       */
+  int    device;         /* HIP device ordinal                                    */
+  int    max_nsamp;      /* largest nsamp per call (sizes the dump buffers)       */
+  double samp_rate;      /* Hz, only used for tic_ref (correlator.c:124)          */
+  double tic_period;     /* s; reference passes (int)0.1 == 0 (globals.h:52)     */
+} gnsscorr_track_cfg;
+
+/* What gp2021.c writes into REG_write for one channel (gp2021.c:75-130). */
+typedef struct {
+  int32_t  prn;          /* SATCNTL: 1..32, 0 = channel off                      */
+  uint32_t carrier_incr; /* (REG_write[3]<<16)+REG_write[4]: per-sample carrier word */
+  uint32_t code_incr;    /* (REG_write[5]<<16)+REG_write[6]; the NCO adds code_incr<<1 */
+  uint32_t slew;         /* REG_write[(ch<<3)+0x84], 0..65535                    */
+  int32_t  epoch_load;   /* -1: none; else REG_write[(ch<<3)+7] (16-bit)         */
+  int32_t  stream;       /* IF stream index this channel correlates              */
+} gnsscorr_nco_cmd;
+
+/* struct gp2021_channel (correlator.c:36-47) + the ms/bit counters. */
+typedef struct {
+  uint32_t carrier_phase;
+  uint32_t carrier_cycle;
+  uint32_t code_phase;
+  uint32_t half_chip;    /* uint16 semantics */
+  int32_t  acc[6];       /* partial epoch: IL QL IP QP IE QE (REG_read order)    */
+  int32_t  ms_counter;
+  int32_t  bit_counter;
+  int32_t  msbit_reg;    /* REG_read[(ch<<3)+7]                                  */
+  int32_t  pad;
+} gnsscorr_chan_state;
+
+/* Per channel result of one call (what lands in REG_read). */
+typedef struct {
+  int32_t  n_dumps;      /* integrate-and-dump events in this call               */
+  int32_t  dump[6];      /* LAST dump: IL QL IP QP IE QE (REG_read[(ch<<3)+0x84..]) */
+  int32_t  msbit_reg;    /* REG_read[(ch<<3)+7] after the call                   */
+  int32_t  tic;          /* 1 if the TIC latched this channel in this call       */
+  int32_t  tic_regs[6];  /* REG_read[(ch<<3)+1..6] latched at the TIC            */
+  int32_t  pad;
+} gnsscorr_track_result;
+
+int gnsscorr_track_create(gnsscorr_track_ctx **out, const gnsscorr_track_cfg *cfg);
+int gnsscorr_track_destroy(gnsscorr_track_ctx *ctx);
+/* Max dumps one call can produce: floor(max_nsamp/2046)+2.  The optional
+ * all-dumps buffer of gnsscorr_track() is n_channels * this * 6 int32. */
+int gnsscorr_track_max_dumps(const gnsscorr_track_ctx *ctx);
+
+/* One correlator call (one "interrupt") over nsamp samples for every channel.
+ * h_if: host IF, n_streams streams of stream_stride samples each (bytes =
+ * samples * (iq ? 2 : 1)); channel c reads stream cmds[c].stream.
+ * NCO words take effect at the start of the call (reference semantics).
+ * h_res: n_channels results; h_all_dumps: optional (may be NULL).
+ * Returns whether the TIC fired through *tic_fired (may be NULL). */
+int gnsscorr_track(gnsscorr_track_ctx *ctx, const int8_t *h_if, int64_t stream_stride,
+                   int n_streams, int64_t nsamp, const gnsscorr_nco_cmd *h_cmds,
+                   gnsscorr_track_result *h_res, int32_t *h_all_dumps, int *tic_fired);
+
+/* Device-resident variant: IF, commands and results stay in HBM; the call is
+ * asynchronous on the context stream (no host sync).  d_cmds / d_res /
+ * d_all_dumps are device arrays sized as in gnsscorr_track().
+ * tic_count: sample index of the TIC in this call or -1 (host computes it with
+ * gnsscorr_track_next_tic()). */
+int gnsscorr_track_dev(gnsscorr_track_ctx *ctx, const int8_t *d_if, int64_t stream_stride,
+                       int64_t nsamp, const gnsscorr_nco_cmd *d_cmds,
+                       gnsscorr_track_result *d_res, int32_t *d_all_dumps, int64_t tic_count);
+/* Advances the context's TIC counter by nsamp (correlator.c:155-165) and
+ * returns the TIC sample index for that call, or -1. */
+int64_t gnsscorr_track_next_tic(gnsscorr_track_ctx *ctx, int64_t nsamp);
+
+/* Open-loop replay: n_steps consecutive calls of nsamp samples; step k reads
+ * IF at d_if + k*nsamp*(iq?2:1) of every stream and commands
+ * d_cmds[k*n_channels ..]; results d_res[k*n_channels ..].  Asynchronous. */
+int gnsscorr_track_replay_dev(gnsscorr_track_ctx *ctx, const int8_t *d_if, int64_t stream_stride,
+                              int64_t nsamp, int n_steps, const gnsscorr_nco_cmd *d_cmds,
+                              gnsscorr_track_result *d_res);
+
+int gnsscorr_track_get_state(gnsscorr_track_ctx *ctx, gnsscorr_chan_state *h_state);
+int gnsscorr_track_set_state(gnsscorr_track_ctx *ctx, const gnsscorr_chan_state *h_state);
+int gnsscorr_track_sync(gnsscorr_track_ctx *ctx);
+/* The HIP stream (hipStream_t) the context launches on. */
+void *gnsscorr_track_stream(gnsscorr_track_ctx *ctx);
+
+/* ======================================================================
+ * Parallel code-phase acquisition (SoftGNSS acquisition.sci semantics)
+ * Replaces: GPS  POSTPROCESSING_SCILAB_RECEIVERS/GPS/L1/acquisition.sci:46-192
+ *           GLO  POSTPROCESSING_SCILAB_RECEIVERS/GLONASS/L1/acquisition.sci:46-198
+ * ==================================================================== */
+
+typedef struct gnsscorr_acq_ctx gnsscorr_acq_ctx;
+
+typedef struct {
+  double samp_rate;       /* settings.samplingFreq                                 */
+  int    n_samples;       /* samplesPerCode = round(fs/(codeFreq/codeLength)); must be
+                             16368 (= 16*3*11*31) in this build                     */
+  int    device;
+  int    max_freqs;       /* capacity of the carrier-frequency table               */
+  int    max_blocks;      /* capacity of 1-ms IF blocks per search                 */
+  int    max_codes;       /* capacity of the code table                            */
+} gnsscorr_acq_cfg;
+
+/* Statistics of one correlation row (code x carrier frequency [x block]). */
+typedef struct {
+  float   peak;           /* max |ifft|^2 of the row                               */
+  int32_t argmax;         /* 0-based sample index of the first maximum             */
+  float   second;         /* max outside the open +-spc window around argmax       */
+  int32_t block;          /* which block the stats come from (best-of-blocks mode) */
+} gnsscorr_acq_row;
+
+/* Per search group (one PRN / FCH), acquisition.sci:141-186. */
+typedef struct {
+  float   peak;           /* peakSize                                              */
+  float   second;         /* secondPeakSize                                        */
+  float   metric;         /* peakSize / secondPeakSize                             */
+  int32_t bin;            /* 0-based frequencyBinIndex-1                           */
+  int32_t code_phase;     /* 1-based codePhase (as acquisition.sci returns it)     */
+  int32_t pad;
+  double  carr_freq;      /* carrier frequency of the winning bin [Hz]             */
+} gnsscorr_acq_result;
+
+#define GNSSCORR_ACQ_BEST_OF_BLOCKS 0  /* SoftGNSS: keep the block with larger max */
+#define GNSSCORR_ACQ_NONCOHERENT    1  /* sum |.|^2 over blocks before the search  */
+
+int gnsscorr_acq_create(gnsscorr_acq_ctx **out, const gnsscorr_acq_cfg *cfg);
+int gnsscorr_acq_destroy(gnsscorr_acq_ctx *ctx);
+/* Upload n_codes sampled code replicas (n_samples int8 values of +-1 each,
+ * e.g. makeCaTable.sci / makeStTable.sci rows); their spectra are computed on
+ * the device and kept resident. */
+int gnsscorr_acq_set_codes(gnsscorr_acq_ctx *ctx, int n_codes, const int8_t *h_codes);
+
+/* Search.  IF: n_blocks consecutive blocks of n_samples complex samples,
+ * interleaved int8 I,Q (iq=1) or int8 real (iq=0).  freqs: n_freqs carrier
+ * frequencies [Hz] (wipe-off exp(i*2*pi*f*t), t = n/fs).  Groups: n_groups
+ * searches, each of n_bins rows: group g uses code group_code[g] and
+ * frequency index group_freq[g*n_bins + b] for bin b.
+ * spc = samplesPerCodeChip (exclusion half-width for the second peak).
+ * Outputs: h_rows (n_groups*n_bins, may be NULL), h_res (n_groups). */
+int gnsscorr_acq_search(gnsscorr_acq_ctx *ctx, const int8_t *h_if, int iq, int n_blocks,
+                        int mode, int n_freqs, const double *h_freqs, int n_groups,
+                        int n_bins, const int32_t *h_group_code, const int32_t *h_group_freq,
+                        int spc, gnsscorr_acq_row *h_rows, gnsscorr_acq_result *h_res);
+
+/* Device-resident variant (asynchronous; d_rows / d_res device arrays).  The
+ * group tables and frequencies are device arrays too. */
+int gnsscorr_acq_search_dev(gnsscorr_acq_ctx *ctx, const int8_t *d_if, int iq, int n_blocks,
+                            int mode, int n_freqs, const double *d_freqs, int n_groups,
+                            int n_bins, const int32_t *d_group_code, const int32_t *d_group_freq,
+                            int spc, gnsscorr_acq_row *d_rows, gnsscorr_acq_result *d_res);
+
+/* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples floats. */
+int gnsscorr_acq_power_row(gnsscorr_acq_ctx *ctx, const int8_t *h_if, int iq, int n_blocks,
+                           int block, double freq, int code, float *h_power);
+int gnsscorr_acq_sync(gnsscorr_acq_ctx *ctx);
+void *gnsscorr_acq_stream(gnsscorr_acq_ctx *ctx);
+
+/* ======================================================================
+ * Host utilities (deterministic synthetic IF, code tables)
+ * ==================================================================== */
+
+/* One planted signal. */
+typedef struct {
+  int32_t system;         /* 0 = GPS L1 C/A, 1 = GLONASS L1OF (ST code)            */
+  int32_t prn;            /* GPS PRN 1..32 (unused for GLONASS)                    */
+  int32_t fch;            /* GLONASS frequency channel -7..6                       */
+  int32_t data_bits;      /* 1: modulate random 50 bps (GPS) / 100 sym/s (GLO) bits */
+  double  code_phase;     /* code phase at sample 0 [chips]                        */
+  double  doppler;        /* carrier Doppler [Hz] (code Doppler follows)           */
+  double  cn0;            /* C/N0 [dB-Hz]                                          */
+  double  carr_phase;     /* carrier phase at sample 0 [rad]                       */
+} gnsscorr_sig;
+
+/* Synthetic IF: nsamp complex samples (iq=1: 2*nsamp int8) or real (iq=0),
+ * at fs with GPS IF `if_gps`, GLONASS IF `if_glo` (+ fch*562.5 kHz), plus
+ * complex AWGN, quantised to the 2-bit levels {-3,-1,+1,+3}
+ * (gps_source.cpp:692).  Deterministic for a given seed (64-bit LCG). */
+int gnsscorr_ifgen(int8_t *h_out, int64_t nsamp, int iq, double fs, double if_gps,
+                   double if_glo, int n_sigs, const gnsscorr_sig *sigs, uint64_t seed);
+
+/* GPS C/A code as +-1 chips (generateCAcode.sci:42-87 form), prn 1..32. */
+int gnsscorr_ca_code(int prn, int8_t *h_chips1023);
+/* GLONASS ST code as +-1 chips (generateSTcode.sci:35-42). */
+int gnsscorr_st_code(int8_t *h_chips511);
+/* Sample a +-1 chip sequence with the makeCaTable.sci:64-72 rule:
+ * out[k-1] = chips[ceil(k*ts/tc)-1], last index forced to code_len. */
+int gnsscorr_sample_code(const int8_t *h_chips, int code_len, double code_rate, double fs,
+                         int n_samples, int8_t *h_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNSSCORR_H */

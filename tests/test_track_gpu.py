@@ -1,0 +1,168 @@
+"""GPU parity: HIP tracking correlator vs the reference semantics.
+
+* OSG register-level shim (Sim_GP2021_int on the GPU) replays every golden
+  scenario bit-exact: all 256 REG_read words after every call and the final
+  gp2021_channel state (reference correlator.c:148-316 via
+  tests/golden/make_osg_golden.py).
+* Batched API with hundreds of channels on several IF streams vs the scalar
+  oracle (oracle/osg_corr.c, itself pinned to the reference).
+* Size-independent properties at full size: chunking invariance (one 1-ms
+  call == two 0.5-ms calls), replay == sequential calls, zero IF -> zero sums.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import osg_scenarios as S
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", list(S.SCENARIOS))
+def test_osg_shim_matches_golden(gpu, name):
+    scn = S.get(name)
+    g = np.load(os.path.join(GOLD, f"osg_{name}.npz"))
+    osg = gpu.OSG(samp_rate=16.0e6, n_channels=12, use_iq=scn["iq"])
+    for k in range(256):
+        osg.REG_read[k] = 0
+        osg.REG_write[k] = 0
+    osg.correlator_init(scn["tic_period"])
+    regs, st = S.run(osg, scn)
+    bad = np.argwhere(regs != g["reg_read"])
+    assert bad.size == 0, f"first mismatches (call, reg): {bad[:8].tolist()}"
+    for k in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+        np.testing.assert_array_equal(st[k], g[k], err_msg=k)
+
+
+def _oracle_channels(oracle, if_streams, nsamp, cmds_per_call, iq=True):
+    """Run each batched channel through its own emulated GP2021 (channel 0)."""
+    n_calls, C = cmds_per_call.shape
+    out = np.zeros((n_calls, C, 6), np.int32)
+    nd = np.zeros((n_calls, C), np.int32)
+    state = []
+    bps = 2 if iq else 1
+    for c in range(C):
+        o = oracle.OracleOSG(1, iq, 16.368e6, 0.0)
+        rw = o.REG_write
+        rw[7] = -1
+        for k in range(n_calls):
+            cm = cmds_per_call[k, c]
+            rw[0] = cm["prn"]
+            rw[3], rw[4] = int(cm["carrier_incr"]) >> 16, int(cm["carrier_incr"]) & 0xFFFF
+            rw[5], rw[6] = int(cm["code_incr"]) >> 16, int(cm["code_incr"]) & 0xFFFF
+            rw[0x84] = cm["slew"]
+            s = if_streams[cm["stream"]]
+            o.sim(s[k * nsamp * bps:(k + 1) * nsamp * bps], nsamp)
+            if o.REG_read[0x82] & 1:
+                nd[k, c] = 1
+                out[k, c] = o.REG_read[0x84:0x8A]
+        state.append(o.chan_state())
+    return out, nd, state
+
+
+def _random_cmds(rng, n_calls, C, n_streams, slew=False):
+    cmds = np.zeros((n_calls, C), np.dtype(
+        [("prn", "<i4"), ("carrier_incr", "<u4"), ("code_incr", "<u4"), ("slew", "<u4"),
+         ("epoch_load", "<i4"), ("stream", "<i4")]))
+    prn = rng.integers(0, 33, size=C)
+    stream = rng.integers(0, n_streams, size=C)
+    for k in range(n_calls):
+        cmds[k]["prn"] = prn
+        cmds[k]["stream"] = stream
+        cmds[k]["carrier_incr"] = 635008600 + rng.integers(-2_000_000, 2_000_000, size=C)
+        cmds[k]["code_incr"] = (6710886 + rng.integers(-100, 100, size=C)) * 40
+        cmds[k]["slew"] = rng.integers(0, 30, size=C) * (rng.random(C) < 0.2) if slew else 0
+        cmds[k]["epoch_load"] = -1
+    return cmds
+
+
+@pytest.mark.parametrize("nsamp", [16368, 8380, 5000])
+def test_batched_many_channels_vs_oracle(gpu, oracle, nsamp):
+    rng = np.random.default_rng(7 + nsamp)
+    C, n_streams, n_calls = 96, 3, 4
+    streams = [S.synth_if(nsamp * n_calls, 100 + i, [(i + 1, 50 * i, 0, 3)]) for i in range(n_streams)]
+    cmds = _random_cmds(rng, n_calls, C, n_streams, slew=True)
+    ref, ref_nd, ref_state = _oracle_channels(oracle, streams, nsamp, cmds)
+    ctx = gpu.TrackCtx(C, iq=True, max_nsamp=nsamp)
+    # streams laid out with a 16-byte aligned stride
+    stride = ((nsamp * n_calls * 2 + 15) // 16) * 16 // 2
+    buf = np.zeros(stride * 2 * n_streams, np.int8)
+    for i, s in enumerate(streams):
+        buf[i * stride * 2: i * stride * 2 + len(s)] = s
+    for k in range(n_calls):
+        # each call reads its chunk: advance the base by k*nsamp samples
+        chunk = buf[k * nsamp * 2:]
+        res, _ = ctx.track(chunk, nsamp, cmds[k], n_streams=n_streams, stream_stride=stride)
+        got_nd = (res["n_dumps"] > 0).astype(np.int32)
+        np.testing.assert_array_equal(got_nd, ref_nd[k])
+        m = got_nd == 1
+        np.testing.assert_array_equal(res["dump"][m], ref[k][m])
+    st = ctx.get_state()
+    for c in range(C):
+        for key in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+            np.testing.assert_array_equal(st[key][c], ref_state[c][key][0], err_msg=f"{key} ch{c}")
+
+
+def test_chunking_invariance_full_size(gpu):
+    """One 16368-sample call == two 8184-sample calls (4096 channels)."""
+    rng = np.random.default_rng(3)
+    C = 4096
+    IF = S.synth_if(16368, 5, [(3, 100, 0, 3)])
+    cm = _random_cmds(rng, 1, C, 1)[0]
+    a = gpu.TrackCtx(C, max_nsamp=16368)
+    b = gpu.TrackCtx(C, max_nsamp=16368)
+    ra, _, da = a.track(IF, 16368, cm, all_dumps=True)
+    rb1, _, db1 = b.track(IF[:16368], 8184, cm, all_dumps=True)
+    rb2, _, db2 = b.track(IF[16368:], 8184, cm, all_dumps=True)
+    sa, sb = a.get_state(), b.get_state()
+    for key in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+        np.testing.assert_array_equal(sa[key], sb[key], err_msg=key)
+    # dumps: concatenation of the two halves' dumps equals the single call's
+    for c in range(0, C, 97):
+        da_c = da[c, :ra["n_dumps"][c]]
+        db_c = np.concatenate([db1[c, :rb1["n_dumps"][c]], db2[c, :rb2["n_dumps"][c]]])
+        np.testing.assert_array_equal(da_c, db_c)
+
+
+def test_zero_if_gives_zero(gpu):
+    C = 64
+    ctx = gpu.TrackCtx(C, max_nsamp=16368)
+    cm = _random_cmds(np.random.default_rng(1), 1, C, 1)[0]
+    for _ in range(3):
+        res, _ = ctx.track(np.zeros(16368 * 2, np.int8), 16368, cm)
+    assert (res["dump"] == 0).all()
+    assert (ctx.get_state()["acc"] == 0).all()
+
+
+def test_replay_equals_sequential(gpu):
+    import torch
+    rng = np.random.default_rng(9)
+    C, K, nsamp = 256, 6, 16368
+    IF = S.synth_if(nsamp * K, 77, [(5, 10, 0, 3)])
+    cmds = _random_cmds(rng, K, C, 1)
+    seq = gpu.TrackCtx(C, max_nsamp=nsamp)
+    seq_res = []
+    for k in range(K):
+        r, _ = seq.track(IF[k * nsamp * 2:(k + 1) * nsamp * 2], nsamp, cmds[k])
+        seq_res.append(r)
+    rep = gpu.TrackCtx(C, max_nsamp=nsamp)
+    d_if = torch.from_numpy(IF.copy()).cuda()
+    d_cmds = torch.from_numpy(cmds.view(np.uint8).copy()).cuda()
+    d_res = torch.zeros(K * C * gpu.TRACK_RESULT.itemsize, dtype=torch.uint8, device="cuda")
+    rep.replay_dev(d_if.data_ptr(), 0, nsamp, K, d_cmds.data_ptr(), d_res.data_ptr())
+    rep.sync()
+    got = d_res.cpu().numpy().view(gpu.TRACK_RESULT).reshape(K, C)
+    for k in range(K):
+        np.testing.assert_array_equal(got[k]["n_dumps"], seq_res[k]["n_dumps"])
+        np.testing.assert_array_equal(got[k]["dump"], seq_res[k]["dump"])
+    np.testing.assert_array_equal(rep.get_state()["acc"], seq.get_state()["acc"])
+
+
+def test_track_rejects_bad_prn(gpu):
+    ctx = gpu.TrackCtx(4, max_nsamp=1024)
+    cm = _random_cmds(np.random.default_rng(0), 1, 4, 1)[0]
+    cm["prn"][2] = 40
+    with pytest.raises(gpu.GnssCorrError):
+        ctx.track(np.zeros(2048, np.int8), 1024, cm)
