@@ -1,0 +1,764 @@
+// acq.hip -- parallel code-phase acquisition on gfx950 (SoftGNSS semantics).
+//
+// Reference: POSTPROCESSING_SCILAB_RECEIVERS/GPS/L1/acquisition.sci:46-192
+// (GLONASS: GLONASS/L1/acquisition.sci:46-198).  Per search group (PRN or
+// FCH) and frequency bin:  X = fft(exp(i f 2 pi t) .* block),
+// |ifft(X .* conj(fft(code)))|^2 for each 1-ms block, keep the block with the
+// larger maximum, then peak / code phase / second peak outside +-1 chip.
+//
+// MI355X design
+//  * N = samplesPerCode = 16368 = 16 * 3 * 11 * 31.  The four factors are
+//    pairwise coprime, so the DFT is done as a Good-Thomas prime-factor FFT:
+//    a 4-D DFT of shape 16 x 3 x 11 x 31 with NO inter-stage twiddles.  The
+//    Ruritanian input map n(p) and CRT output map k(p) are pure index
+//    permutations; they are folded into where data is read and written.
+//  * One 1-ms row (16368 complex fp32 = 128 KiB) lives in LDS for the whole
+//    transform; 528 work-items (9 wavefronts) each own one radix-16, one
+//    3x11 or one radix-31 butterfly per pass: 3 LDS passes per transform.
+//  * The IFFT is computed as a forward FFT of conj(Y) (|ifft(Y)| = |fft(conj Y)|/N),
+//    so one kernel body serves both directions.
+//  * Forward spectra of the wiped-off IF (shared by all codes) and of every
+//    code replica are written to HBM already permuted into the correlation
+//    kernel's LDS order (sigma = n^-1 o k), so the hot kernel streams both
+//    operands with fully coalesced 8-byte loads and needs no gathers.
+//  * The hot kernel fuses: conj(X)*F, 3 FFT passes, |.|^2, the per-row
+//    max/argmax (first occurrence in natural order), the second peak outside
+//    the +-spc window, and the best-of-blocks or non-coherent combine over
+//    blocks -- the 16368-point power row never leaves registers.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "gnsscorr_internal.h"
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      gnsscorr_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                         __LINE__);                                                     \
+      return GNSSCORR_EDEVICE;                                                          \
+    }                                                                                   \
+  } while (0)
+
+namespace {
+
+constexpr int N = 16368;
+constexpr int M16 = N / 16, M3 = N / 3, M11 = N / 11, M31 = N / 31;  // 1023 5456 1488 528
+// CRT idempotents e_i = 1 mod N_i, 0 mod N_j (checked on the host at create)
+constexpr int E16 = 15345, E3 = 10912, E11 = 5952, E31 = 528;
+constexpr int kThreads = 512;           // 8 wavefronts -> up to 256 VGPRs each
+constexpr int kGroups31 = N / 31;       // 528 radix-31 groups
+constexpr int kLeft = kGroups31 - kThreads;  // 16 groups done as direct dot products
+
+constexpr float kCos11[11] = {1.000000000e+00f, 8.412535328e-01f, 4.154150130e-01f, -1.423148383e-01f, -6.548607339e-01f, -9.594929736e-01f, -9.594929736e-01f, -6.548607339e-01f, -1.423148383e-01f, 4.154150130e-01f, 8.412535328e-01f};
+constexpr float kSin11[11] = {0.000000000e+00f, 5.406408175e-01f, 9.096319954e-01f, 9.898214419e-01f, 7.557495744e-01f, 2.817325568e-01f, -2.817325568e-01f, -7.557495744e-01f, -9.898214419e-01f, -9.096319954e-01f, -5.406408175e-01f};
+constexpr float kCos31[31] = {1.000000000e+00f, 9.795299413e-01f, 9.189578116e-01f, 8.207634412e-01f, 6.889669191e-01f, 5.289640103e-01f, 3.473052528e-01f, 1.514277775e-01f, -5.064916884e-02f, -2.506525323e-01f, -4.403941516e-01f, -6.121059825e-01f, -7.587581227e-01f, -8.743466161e-01f, -9.541392564e-01f, -9.948693234e-01f, -9.948693234e-01f, -9.541392564e-01f, -8.743466161e-01f, -7.587581227e-01f, -6.121059825e-01f, -4.403941516e-01f, -2.506525323e-01f, -5.064916884e-02f, 1.514277775e-01f, 3.473052528e-01f, 5.289640103e-01f, 6.889669191e-01f, 8.207634412e-01f, 9.189578116e-01f, 9.795299413e-01f};
+constexpr float kSin31[31] = {0.000000000e+00f, 2.012985201e-01f, 3.943558551e-01f, 5.712682151e-01f, 7.247927872e-01f, 8.486442575e-01f, 9.377521321e-01f, 9.884683243e-01f, 9.987165072e-01f, 9.680771189e-01f, 8.978045396e-01f, 7.907757369e-01f, 6.513724827e-01f, 4.853019625e-01f, 2.993631230e-01f, 1.011683220e-01f, -1.011683220e-01f, -2.993631230e-01f, -4.853019625e-01f, -6.513724827e-01f, -7.907757369e-01f, -8.978045396e-01f, -9.680771189e-01f, -9.987165072e-01f, -9.884683243e-01f, -9.377521321e-01f, -8.486442575e-01f, -7.247927872e-01f, -5.712682151e-01f, -3.943558551e-01f, -2.012985201e-01f};
+constexpr float kCos16[16] = {1.0f, 9.238795325e-01f, 7.071067812e-01f, 3.826834324e-01f, 0.0f, -3.826834324e-01f, -7.071067812e-01f, -9.238795325e-01f, -1.0f, -9.238795325e-01f, -7.071067812e-01f, -3.826834324e-01f, 0.0f, 3.826834324e-01f, 7.071067812e-01f, 9.238795325e-01f};
+constexpr float kSin16[16] = {0.0f, 3.826834324e-01f, 7.071067812e-01f, 9.238795325e-01f, 1.0f, 9.238795325e-01f, 7.071067812e-01f, 3.826834324e-01f, 0.0f, -3.826834324e-01f, -7.071067812e-01f, -9.238795325e-01f, -1.0f, -9.238795325e-01f, -7.071067812e-01f, -3.826834324e-01f};
+constexpr float kSqrt3_2 = 8.660254038e-01f;
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+
+// ---- small forward DFTs (W = exp(-2 pi i / P)) --------------------------------
+__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d) {
+  const float2 t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = csub(b, d);
+  a = cadd(t0, t2);
+  c = csub(t0, t2);
+  b = make_float2(t1.x + t3.y, t1.y - t3.x);  // t1 - i t3
+  d = make_float2(t1.x - t3.y, t1.y + t3.x);  // t1 + i t3
+}
+
+// In place: on return x[k] = X[k].
+__device__ __forceinline__ void dft16(float2 (&x)[16]) {
+#pragma unroll
+  for (int n2 = 0; n2 < 4; n2++) dft4(x[n2], x[4 + n2], x[8 + n2], x[12 + n2]);
+#pragma unroll
+  for (int k1 = 1; k1 < 4; k1++)
+#pragma unroll
+    for (int n2 = 1; n2 < 4; n2++) {
+      const int m = n2 * k1;
+      const float c = kCos16[m], s = -kSin16[m];
+      const float2 v = x[4 * k1 + n2];
+      x[4 * k1 + n2] = make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+    }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; k1++) dft4(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3]);
+  // X[k1 + 4 k2] sits in slot 4 k1 + k2: transpose the 4x4 block
+  float2 y[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) y[i] = x[i];
+#pragma unroll
+  for (int k1 = 0; k1 < 4; k1++)
+#pragma unroll
+    for (int k2 = 0; k2 < 4; k2++) x[k1 + 4 * k2] = y[4 * k1 + k2];
+}
+
+__device__ __forceinline__ void dft3(float2& x0, float2& x1, float2& x2) {
+  const float2 s = cadd(x1, x2), d = csub(x1, x2);
+  const float2 t = make_float2(x0.x - 0.5f * s.x, x0.y - 0.5f * s.y);
+  x0 = cadd(x0, s);
+  x1 = make_float2(t.x + kSqrt3_2 * d.y, t.y - kSqrt3_2 * d.x);
+  x2 = make_float2(t.x - kSqrt3_2 * d.y, t.y + kSqrt3_2 * d.x);
+}
+
+template <int P>
+__device__ __forceinline__ float ctab(int k) { return P == 11 ? kCos11[k] : kCos31[k]; }
+template <int P>
+__device__ __forceinline__ float stab(int k) { return P == 11 ? kSin11[k] : kSin31[k]; }
+
+// Symmetric prime-length DFT: X_m = A_m - i B_m, X_{P-m} = A_m + i B_m with
+// A_m = x0 + sum_j cos(2 pi jm/P)(x_j + x_{P-j}), B_m = sum_j sin(..)(x_j - x_{P-j}).
+template <int P>
+__device__ __forceinline__ void dftp(float2 (&x)[P]) {
+  constexpr int H = (P - 1) / 2;
+  float2 s[H + 1], d[H + 1];
+#pragma unroll
+  for (int j = 1; j <= H; j++) {
+    s[j] = cadd(x[j], x[P - j]);
+    d[j] = csub(x[j], x[P - j]);
+  }
+  const float2 x0 = x[0];
+  float2 X0 = x0;
+#pragma unroll
+  for (int j = 1; j <= H; j++) X0 = cadd(X0, s[j]);
+  x[0] = X0;
+#pragma unroll
+  for (int m = 1; m <= H; m++) {
+    float ar = x0.x, ai = x0.y, br = 0.f, bi = 0.f;
+#pragma unroll
+    for (int j = 1; j <= H; j++) {
+      const int q = (j * m) % P;
+      const float c = ctab<P>(q), sn = stab<P>(q);
+      ar = fmaf(c, s[j].x, ar);
+      ai = fmaf(c, s[j].y, ai);
+      br = fmaf(sn, d[j].x, br);
+      bi = fmaf(sn, d[j].y, bi);
+    }
+    x[m] = make_float2(ar + bi, ai - br);
+    x[P - m] = make_float2(ar - bi, ai + br);
+  }
+}
+
+// Same DFT, but only |X_m|^2 * scale is produced (final pass of the
+// correlation kernel): halves the live registers of the output side.
+template <int P>
+__device__ __forceinline__ void dftp_power(const float2 (&x)[P], float scale, float (&pw)[P]) {
+  constexpr int H = (P - 1) / 2;
+  float2 s[H + 1], d[H + 1];
+#pragma unroll
+  for (int j = 1; j <= H; j++) {
+    s[j] = cadd(x[j], x[P - j]);
+    d[j] = csub(x[j], x[P - j]);
+  }
+  const float2 x0 = x[0];
+  float2 X0 = x0;
+#pragma unroll
+  for (int j = 1; j <= H; j++) X0 = cadd(X0, s[j]);
+  pw[0] = (X0.x * X0.x + X0.y * X0.y) * scale;
+#pragma unroll
+  for (int m = 1; m <= H; m++) {
+    float ar = x0.x, ai = x0.y, br = 0.f, bi = 0.f;
+#pragma unroll
+    for (int j = 1; j <= H; j++) {
+      const int q = (j * m) % P;
+      const float c = ctab<P>(q), sn = stab<P>(q);
+      ar = fmaf(c, s[j].x, ar);
+      ai = fmaf(c, s[j].y, ai);
+      br = fmaf(sn, d[j].x, br);
+      bi = fmaf(sn, d[j].y, bi);
+    }
+    const float r1 = ar + bi, i1 = ai - br, r2 = ar - bi, i2 = ai + br;
+    pw[m] = (r1 * r1 + i1 * i1) * scale;
+    pw[P - m] = (r2 * r2 + i2 * i2) * scale;
+  }
+}
+
+// ---- index maps --------------------------------------------------------------
+// LDS position p = a*1023 + (b*11 + c)*31 + d
+__device__ __forceinline__ int in_index(int p) {  // Ruritanian input map n(p)
+  const int d = p % 31, c = (p / 31) % 11, b = (p / 341) % 3, a = p / 1023;
+  int n = a * M16 + b * M3 + c * M11 + d * M31;
+  n %= N;
+  return n;
+}
+
+// ---- the three in-LDS passes (16, 3x11, 31) ----------------------------------
+__device__ __forceinline__ void pass16(float2* lds, int t) {
+  for (int g = t; g < M16; g += kThreads) {
+    float2 x[16];
+#pragma unroll
+    for (int a = 0; a < 16; a++) x[a] = lds[a * M16 + g];
+    dft16(x);
+#pragma unroll
+    for (int a = 0; a < 16; a++) lds[a * M16 + g] = x[a];
+  }
+}
+
+__device__ __forceinline__ void pass33(float2* lds, int t) {
+  if (t >= 16 * 31) return;
+  const int a = t / 31, d = t % 31;
+  float2* base = lds + a * M16 + d;
+  float2 v[3][11];
+#pragma unroll
+  for (int b = 0; b < 3; b++)
+#pragma unroll
+    for (int c = 0; c < 11; c++) v[b][c] = base[(b * 11 + c) * 31];
+#pragma unroll
+  for (int c = 0; c < 11; c++) dft3(v[0][c], v[1][c], v[2][c]);
+#pragma unroll
+  for (int b = 0; b < 3; b++) dftp<11>(v[b]);
+#pragma unroll
+  for (int b = 0; b < 3; b++)
+#pragma unroll
+    for (int c = 0; c < 11; c++) base[(b * 11 + c) * 31] = v[b][c];
+}
+
+// dim-31 pass, leftover groups 512..527: thread t < 496 computes output m of
+// group 512 + t/31 as a direct 31-term DFT sum (twiddles from an LDS table).
+__device__ __forceinline__ float2 dft31_single(const float2* lds, const float2* tw, int t) {
+  const int grp = kThreads + t / 31, m = t % 31;
+  const float2* x = lds + grp * 31;
+  float re = 0.f, im = 0.f;
+  int q = 0;
+#pragma unroll
+  for (int j = 0; j < 31; j++) {
+    const float2 v = x[j], w = tw[q];  // w = exp(-2 pi i q / 31)
+    re = fmaf(v.x, w.x, fmaf(-v.y, w.y, re));
+    im = fmaf(v.x, w.y, fmaf(v.y, w.x, im));
+    q += m;
+    if (q >= 31) q -= 31;
+  }
+  return make_float2(re, im);
+}
+
+__device__ __forceinline__ void init_tw31(float2* tw) {
+  if (threadIdx.x < 31) tw[threadIdx.x] = make_float2(kCos31[threadIdx.x], -kSin31[threadIdx.x]);
+}
+
+// natural output index of LDS position t*31 + d': k = (a E16 + b E3 + c E11 + d' E31) mod N
+__device__ __forceinline__ int out_base(int t) {
+  const int a = t / 33, bc = t % 33, b = bc / 11, c = bc % 11;
+  return (int)(((long)a * E16 + (long)b * E3 + (long)c * E11) % N);
+}
+
+// ---- forward spectra: wiped-off IF rows and code rows --------------------------
+// mode 0: IF row = (freq_id, block); x[n] = IF[block][n] * exp(i f ((n*2)*pi)*ts)
+// mode 1: code row c; x[n] = code[c][n]
+__global__ __launch_bounds__(kThreads) void acq_forward_kernel(
+    const int8_t* __restrict__ src, int iq, int n_blocks, const double* __restrict__ freqs,
+    double ts, int mode, const int* __restrict__ sigma, float2* __restrict__ out) {
+  __shared__ float2 lds[N];
+  __shared__ float2 tw[32];
+  const int row = blockIdx.x;
+  const int t = threadIdx.x;
+  init_tw31(tw);
+  if (mode == 0) {
+    const int fid = row / n_blocks, blk = row % n_blocks;
+    const double f = freqs[fid];
+    const int8_t* s = src + (long)blk * N * (iq ? 2 : 1);
+    for (int p = t; p < N; p += kThreads) {
+      const int n = in_index(p);
+      const double I = iq ? (double)s[2 * n] : (double)s[n];
+      const double Q = iq ? (double)s[2 * n + 1] : 0.0;
+      // acquisition.sci:61-62, 107: phasePoints = (0:N-1)*2*%pi*ts; exp(i f pp)
+      const double th = f * ((((double)n * 2.0) * M_PI) * ts);
+      double sn, cs;
+      sincos(th, &sn, &cs);
+      lds[p] = make_float2((float)(I * cs - Q * sn), (float)(I * sn + Q * cs));
+    }
+  } else {
+    const int8_t* s = src + (long)row * N;
+    for (int p = t; p < N; p += kThreads) lds[p] = make_float2((float)s[in_index(p)], 0.f);
+  }
+  __syncthreads();
+  pass16(lds, t);
+  __syncthreads();
+  pass33(lds, t);
+  __syncthreads();
+  float2* o = out + (long)row * N;
+  float2 y = make_float2(0.f, 0.f);
+  const bool extra = t < kLeft * 31;
+  if (extra) y = dft31_single(lds, tw, t);
+  {
+    float2 x[31];
+#pragma unroll
+    for (int d = 0; d < 31; d++) x[d] = lds[t * 31 + d];
+    dftp<31>(x);
+#pragma unroll
+    for (int d = 0; d < 31; d++) o[sigma[t * 31 + d]] = x[d];
+  }
+  if (extra) o[sigma[kThreads * 31 + t]] = y;
+}
+
+// ---- block-level reductions ---------------------------------------------------
+struct PeakSlot {
+  float v;
+  int k;
+};
+
+__device__ __forceinline__ bool better(float v1, int k1, float v0, int k0) {
+  return v1 > v0 || (v1 == v0 && k1 < k0);
+}
+
+// max value, smallest natural index among equals; result broadcast to all threads
+__device__ __forceinline__ void block_argmax(float& v, int& k, PeakSlot* scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(v, o, 64);
+    const int k2 = __shfl_xor(k, o, 64);
+    if (better(v2, k2, v, k)) { v = v2; k = k2; }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) scratch[w] = PeakSlot{v, k};
+  __syncthreads();
+  v = scratch[0].v;
+  k = scratch[0].k;
+#pragma unroll
+  for (int i = 1; i < kThreads / 64; i++)
+    if (better(scratch[i].v, scratch[i].k, v, k)) { v = scratch[i].v; k = scratch[i].k; }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  v = scratch[0];
+#pragma unroll
+  for (int i = 1; i < kThreads / 64; i++) v = fmaxf(v, scratch[i]);
+  __syncthreads();
+  return v;
+}
+
+// ---- the hot kernel: one (group, bin) row per workgroup ------------------------
+// Every thread owns radix-31 group t (positions t*31 .. t*31+30) and threads
+// t < 496 also own one output of the 16 leftover groups (position 512*31 + t).
+template <int MODE, bool DUMP>
+__global__ __launch_bounds__(kThreads) void acq_corr_kernel(
+    const float2* __restrict__ X, const float2* __restrict__ F, int n_blocks,
+    const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins,
+    int spc, gnsscorr_acq_row* __restrict__ rows, float* __restrict__ dump_power,
+    int dump_block) {
+  __shared__ float2 lds[N];
+  __shared__ float2 tw[32];
+  __shared__ PeakSlot s_pk[kThreads / 64];
+  __shared__ float s_mx[kThreads / 64];
+  const int rowid = blockIdx.x;
+  const int g = rowid / n_bins, bin = rowid % n_bins;
+  const int code = group_code[g];
+  const int fid = group_freq[g * n_bins + bin];
+  const int t = threadIdx.x;
+  const float inv_n2 = 1.0f / ((float)N * (float)N);
+  const bool extra = t < kLeft * 31;
+  const int kb = out_base(t);
+  // natural index of the leftover output owned by this thread
+  const int kx = (int)(((long)out_base(kThreads + t / 31) + (long)(t % 31) * E31) % N);
+  init_tw31(tw);
+
+  constexpr bool kNonCoh = MODE == GNSSCORR_ACQ_NONCOHERENT;
+  constexpr int kAcc = kNonCoh ? 32 : 1;
+  float pacc[kAcc];
+#pragma unroll
+  for (int d = 0; d < kAcc; d++) pacc[d] = 0.f;
+  float best_pk = -1.f, best_sec = 0.f;
+  int best_k = 0, best_blk = 0;
+
+  const float2* Fc = F + (long)code * N;
+  for (int blk = 0; blk < n_blocks; blk++) {
+    const float2* Xb = X + ((long)fid * n_blocks + blk) * N;
+    // D = conj(X) * F  (= conj(X * conj(F)), acquisition.sci:116)
+    for (int p = t; p < N; p += kThreads) {
+      const float2 x = Xb[p], f = Fc[p];
+      lds[p] = make_float2(x.x * f.x + x.y * f.y, x.x * f.y - x.y * f.x);
+    }
+    __syncthreads();
+    pass16(lds, t);
+    __syncthreads();
+    pass33(lds, t);
+    __syncthreads();
+    float pw[32];  // pw[31] = this thread's leftover output (or -1)
+    {
+      const float2 y = extra ? dft31_single(lds, tw, t) : make_float2(0.f, 0.f);
+      pw[31] = extra ? (y.x * y.x + y.y * y.y) * inv_n2 : -1.f;
+      float2 x[31];
+#pragma unroll
+      for (int d = 0; d < 31; d++) x[d] = lds[t * 31 + d];
+      dftp<31>(x);
+#pragma unroll
+      for (int d = 0; d < 31; d++) pw[d] = (x[d].x * x[d].x + x[d].y * x[d].y) * inv_n2;
+    }
+    if (DUMP && blk == dump_block) {
+      int k = kb;
+#pragma unroll
+      for (int d = 0; d < 31; d++) {
+        dump_power[(long)rowid * N + k] = pw[d];
+        k += E31;
+        if (k >= N) k -= N;
+      }
+      if (extra) dump_power[(long)rowid * N + kx] = pw[31];
+    }
+    if (kNonCoh) {
+#pragma unroll
+      for (int d = 0; d < 32; d++) pacc[d % kAcc] += pw[d];
+      __syncthreads();  // LDS is rewritten by the next block
+      if (blk + 1 < n_blocks) continue;
+#pragma unroll
+      for (int d = 0; d < 31; d++) pw[d] = pacc[d % kAcc];
+      pw[31] = extra ? pacc[31 % kAcc] : -1.f;
+    }
+    // row maximum with the first (smallest natural index) occurrence
+    float v = pw[31];
+    int kk = extra ? kx : 0x7fffffff;
+    {
+      int k = kb;
+#pragma unroll
+      for (int d = 0; d < 31; d++) {
+        if (better(pw[d], k, v, kk)) { v = pw[d]; kk = k; }
+        k += E31;
+        if (k >= N) k -= N;
+      }
+    }
+    block_argmax(v, kk, s_pk);
+    // second peak outside the open window (argmax - spc, argmax + spc), circular
+    float sv = -1.f;
+    {
+      int k = kb;
+#pragma unroll
+      for (int d = 0; d < 32; d++) {
+        const int kd = d == 31 ? kx : k;
+        int dist = kd - kk;
+        if (dist < 0) dist += N;
+        if ((d < 31 || extra) && dist >= spc && dist <= N - spc) sv = fmaxf(sv, pw[d]);
+        k += E31;
+        if (k >= N) k -= N;
+      }
+    }
+    sv = block_max(sv, s_mx);
+    // acquisition.sci:126-132: a later block replaces the kept one unless the
+    // kept block's max is strictly larger
+    if (blk == 0 || !(best_pk > v)) {
+      best_pk = v;
+      best_k = kk;
+      best_sec = sv;
+      best_blk = blk;
+    }
+  }
+  if (t == 0) {
+    gnsscorr_acq_row r;
+    r.peak = best_pk;
+    r.argmax = best_k;
+    r.second = best_sec;
+    r.block = kNonCoh ? -1 : best_blk;
+    rows[rowid] = r;
+  }
+}
+
+// acquisition.sci:141-186 per group: frequencyBinIndex = first row with the
+// largest max; codePhase = first column holding it; metric = peak / second.
+__global__ void acq_select_kernel(const gnsscorr_acq_row* __restrict__ rows, int n_groups,
+                                  int n_bins, const int* __restrict__ group_freq,
+                                  const double* __restrict__ freqs,
+                                  gnsscorr_acq_result* __restrict__ res) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const gnsscorr_acq_row* r = rows + (long)g * n_bins;
+  float pk = r[0].peak;
+  int bin = 0;
+  for (int b = 1; b < n_bins; b++)
+    if (r[b].peak > pk) { pk = r[b].peak; bin = b; }
+  int cp = 0x7fffffff;
+  for (int b = 0; b < n_bins; b++)
+    if (r[b].peak == pk && r[b].argmax < cp) cp = r[b].argmax;
+  gnsscorr_acq_result o;
+  o.peak = pk;
+  o.second = r[bin].second;
+  o.metric = pk / r[bin].second;
+  o.bin = bin;
+  o.code_phase = cp + 1;
+  // 1 if an exact tie put the global first column in another row than the
+  // winning row's own argmax (second peak then centred on the row's argmax)
+  o.pad = cp != r[bin].argmax;
+  o.carr_freq = freqs[group_freq[(long)g * n_bins + bin]];
+  res[g] = o;
+}
+
+// ---- host-side index tables ---------------------------------------------------
+static int host_in_index(int p) {
+  const int d = p % 31, c = (p / 31) % 11, b = (p / 341) % 3, a = p / 1023;
+  return (a * M16 + b * M3 + c * M11 + d * M31) % N;
+}
+static int host_out_index(int p) {
+  const int d = p % 31, c = (p / 31) % 11, b = (p / 341) % 3, a = p / 1023;
+  return (int)(((long)a * E16 + (long)b * E3 + (long)c * E11 + (long)d * E31) % N);
+}
+
+}  // namespace
+
+// ============================================================================
+// context / C ABI
+// ============================================================================
+struct gnsscorr_acq_ctx {
+  gnsscorr_acq_cfg cfg;
+  hipStream_t stream = nullptr;
+  int* d_sigma = nullptr;
+  float2* d_F = nullptr;     // code spectra, permuted, [max_codes][N]
+  float2* d_X = nullptr;     // IF spectra, permuted, [max_freqs*max_blocks][N]
+  int n_codes = 0;
+  // host-API staging
+  int8_t* d_if = nullptr;
+  double* d_freqs = nullptr;
+  int* d_gcode = nullptr;
+  int* d_gfreq = nullptr;
+  gnsscorr_acq_row* d_rows = nullptr;
+  gnsscorr_acq_result* d_res = nullptr;
+  float* d_dump = nullptr;
+  size_t cap_rows = 0, cap_res = 0, cap_gcode = 0, cap_gfreq = 0;
+};
+
+static int grow(void** p, size_t* cap, size_t need, size_t elem) {
+  if (need <= *cap) return GNSSCORR_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(p, need * elem));
+  *cap = need;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cfg* cfg) {
+  if (!out || !cfg || cfg->n_samples != N || cfg->max_freqs < 1 || cfg->max_blocks < 1 ||
+      cfg->max_codes < 1 || cfg->samp_rate <= 0) {
+    gnsscorr_set_error("gnsscorr_acq_create: bad config (n_samples must be %d)", N);
+    return GNSSCORR_EINVAL;
+  }
+  *out = nullptr;
+  // self-check of the prime-factor maps: both must be bijections
+  {
+    static int checked = 0;
+    if (!checked) {
+      char* seen = (char*)calloc(2 * N, 1);
+      for (int p = 0; p < N; p++) { seen[host_in_index(p)]++; seen[N + host_out_index(p)]++; }
+      for (int i = 0; i < 2 * N; i++)
+        if (seen[i] != 1) { free(seen); gnsscorr_set_error("PFA map check failed"); return GNSSCORR_EINVAL; }
+      free(seen);
+      checked = 1;
+    }
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    gnsscorr_set_error("gnsscorr_acq_create: no HIP device");
+    return GNSSCORR_ENODEV;
+  }
+  if (cfg->device < 0 || cfg->device >= ndev) {
+    gnsscorr_set_error("gnsscorr_acq_create: device %d out of range", cfg->device);
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(cfg->device));
+  auto* c = new gnsscorr_acq_ctx();
+  c->cfg = *cfg;
+  auto fail = [&](int code) {
+    gnsscorr_acq_destroy(c);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_sigma, sizeof(int) * N) != hipSuccess ||
+      hipMalloc(&c->d_F, sizeof(float2) * N * (size_t)cfg->max_codes) != hipSuccess ||
+      hipMalloc(&c->d_X, sizeof(float2) * N * (size_t)cfg->max_freqs * cfg->max_blocks) != hipSuccess ||
+      hipMalloc(&c->d_if, (size_t)N * 2 * cfg->max_blocks) != hipSuccess ||
+      hipMalloc(&c->d_freqs, sizeof(double) * cfg->max_freqs) != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_acq_create: device allocation failed");
+    return fail(GNSSCORR_ENOMEM);
+  }
+  // sigma(p) = n^-1(k(p)): where the forward FFT's output k(p) must be stored
+  // so that the correlation kernel reads its input n(p') linearly
+  int* inv_in = (int*)malloc(sizeof(int) * N);
+  int* sigma = (int*)malloc(sizeof(int) * N);
+  for (int p = 0; p < N; p++) inv_in[host_in_index(p)] = p;
+  for (int p = 0; p < N; p++) sigma[p] = inv_in[host_out_index(p)];
+  hipError_t e = hipMemcpy(c->d_sigma, sigma, sizeof(int) * N, hipMemcpyHostToDevice);
+  free(inv_in);
+  free(sigma);
+  if (e != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_acq_create: %s", hipGetErrorString(e));
+    return fail(GNSSCORR_EDEVICE);
+  }
+  *out = c;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_destroy(gnsscorr_acq_ctx* c) {
+  if (!c) return GNSSCORR_OK;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->d_sigma, c->d_F, c->d_X, c->d_if, c->d_freqs, c->d_gcode,
+                  c->d_gfreq, c->d_rows, c->d_res, c->d_dump};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const int8_t* h_codes) {
+  if (!c || !h_codes || n_codes < 1 || n_codes > c->cfg.max_codes) {
+    gnsscorr_set_error("gnsscorr_acq_set_codes: bad arguments (n_codes %d, max %d)", n_codes,
+                       c ? c->cfg.max_codes : 0);
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  int8_t* d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)n_codes * N));
+  HIP_TRY(hipMemcpyAsync(d, h_codes, (size_t)n_codes * N, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(acq_forward_kernel, dim3(n_codes), dim3(kThreads), 0, c->stream, d, 0, 1,
+                     (const double*)nullptr, 0.0, 1, c->d_sigma, c->d_F);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipFree(d));
+  c->n_codes = n_codes;
+  return GNSSCORR_OK;
+}
+
+static int search_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int mode,
+                         int n_freqs, const double* d_freqs, int n_groups, int n_bins,
+                         const int32_t* d_gcode, const int32_t* d_gfreq, int spc,
+                         gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res, float* d_dump,
+                         int dump_block) {
+  if (n_blocks < 1 || n_blocks > c->cfg.max_blocks || n_freqs < 1 || n_freqs > c->cfg.max_freqs ||
+      n_groups < 1 || n_bins < 1 || spc < 1 || spc > N / 2 || c->n_codes < 1 ||
+      (mode != GNSSCORR_ACQ_BEST_OF_BLOCKS && mode != GNSSCORR_ACQ_NONCOHERENT)) {
+    gnsscorr_set_error("gnsscorr_acq_search: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  hipLaunchKernelGGL(acq_forward_kernel, dim3(n_freqs * n_blocks), dim3(kThreads), 0, c->stream,
+                     d_if, iq, n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, 0, c->d_sigma, c->d_X);
+  HIP_TRY(hipGetLastError());
+#define ACQ_CORR_LAUNCH(M, D)                                                                  \
+  hipLaunchKernelGGL((acq_corr_kernel<M, D>), dim3(n_groups * n_bins), dim3(kThreads), 0,       \
+                     c->stream, c->d_X, c->d_F, n_blocks, d_gcode, d_gfreq, n_bins, spc, d_rows, \
+                     d_dump, dump_block)
+  if (d_dump)
+    ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
+  else if (mode == GNSSCORR_ACQ_NONCOHERENT)
+    ACQ_CORR_LAUNCH(GNSSCORR_ACQ_NONCOHERENT, false);
+  else
+    ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, false);
+#undef ACQ_CORR_LAUNCH
+  HIP_TRY(hipGetLastError());
+  if (d_res) {
+    hipLaunchKernelGGL(acq_select_kernel, dim3((n_groups + 63) / 64), dim3(64), 0, c->stream,
+                       d_rows, n_groups, n_bins, d_gfreq, d_freqs, d_res);
+    HIP_TRY(hipGetLastError());
+  }
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_search_dev(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq,
+                                       int n_blocks, int mode, int n_freqs, const double* d_freqs,
+                                       int n_groups, int n_bins, const int32_t* d_group_code,
+                                       const int32_t* d_group_freq, int spc,
+                                       gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res) {
+  if (!c || !d_if || !d_freqs || !d_group_code || !d_group_freq || !d_rows) {
+    gnsscorr_set_error("gnsscorr_acq_search_dev: null argument");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  return search_launch(c, d_if, iq, n_blocks, mode, n_freqs, d_freqs, n_groups, n_bins,
+                       d_group_code, d_group_freq, spc, d_rows, d_res, nullptr, -1);
+}
+
+static int stage_host(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blocks, int n_freqs,
+                      const double* h_freqs, int n_groups, int n_bins, const int32_t* h_gcode,
+                      const int32_t* h_gfreq) {
+  if (n_blocks < 1 || n_blocks > c->cfg.max_blocks || n_freqs < 1 || n_freqs > c->cfg.max_freqs) {
+    gnsscorr_set_error("gnsscorr_acq_search: n_blocks/n_freqs outside the context capacity");
+    return GNSSCORR_EINVAL;
+  }
+  for (int g = 0; g < n_groups; g++) {
+    if (h_gcode[g] < 0 || h_gcode[g] >= c->n_codes) {
+      gnsscorr_set_error("gnsscorr_acq_search: group %d code %d not uploaded", g, h_gcode[g]);
+      return GNSSCORR_EINVAL;
+    }
+    for (int b = 0; b < n_bins; b++) {
+      const int f = h_gfreq[(long)g * n_bins + b];
+      if (f < 0 || f >= n_freqs) {
+        gnsscorr_set_error("gnsscorr_acq_search: group %d bin %d freq index %d invalid", g, b, f);
+        return GNSSCORR_EINVAL;
+      }
+    }
+  }
+  const size_t R = (size_t)n_groups * n_bins;
+  int rc;
+  if ((rc = grow((void**)&c->d_rows, &c->cap_rows, R, sizeof(gnsscorr_acq_row)))) return rc;
+  if ((rc = grow((void**)&c->d_res, &c->cap_res, n_groups, sizeof(gnsscorr_acq_result)))) return rc;
+  if ((rc = grow((void**)&c->d_gcode, &c->cap_gcode, n_groups, sizeof(int)))) return rc;
+  if ((rc = grow((void**)&c->d_gfreq, &c->cap_gfreq, R, sizeof(int)))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)n_blocks * N * (iq ? 2 : 1),
+                         hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_freqs, h_freqs, sizeof(double) * n_freqs, hipMemcpyHostToDevice,
+                         c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_gcode, h_gcode, sizeof(int) * n_groups, hipMemcpyHostToDevice,
+                         c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_gfreq, h_gfreq, sizeof(int) * R, hipMemcpyHostToDevice, c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_search(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blocks,
+                                   int mode, int n_freqs, const double* h_freqs, int n_groups,
+                                   int n_bins, const int32_t* h_group_code,
+                                   const int32_t* h_group_freq, int spc,
+                                   gnsscorr_acq_row* h_rows, gnsscorr_acq_result* h_res) {
+  if (!c || !h_if || !h_freqs || !h_group_code || !h_group_freq || n_groups < 1 || n_bins < 1) {
+    gnsscorr_set_error("gnsscorr_acq_search: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  int rc = stage_host(c, h_if, iq, n_blocks, n_freqs, h_freqs, n_groups, n_bins, h_group_code,
+                      h_group_freq);
+  if (rc) return rc;
+  rc = search_launch(c, c->d_if, iq, n_blocks, mode, n_freqs, c->d_freqs, n_groups, n_bins,
+                     c->d_gcode, c->d_gfreq, spc, c->d_rows, c->d_res, nullptr, -1);
+  if (rc) return rc;
+  if (h_rows)
+    HIP_TRY(hipMemcpyAsync(h_rows, c->d_rows, sizeof(gnsscorr_acq_row) * n_groups * n_bins,
+                           hipMemcpyDeviceToHost, c->stream));
+  if (h_res)
+    HIP_TRY(hipMemcpyAsync(h_res, c->d_res, sizeof(gnsscorr_acq_result) * n_groups,
+                           hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq,
+                                      int n_blocks, int block, double freq, int code,
+                                      float* h_power) {
+  if (!c || !h_if || !h_power || block < 0 || block >= n_blocks || code < 0 ||
+      code >= c->n_codes) {
+    gnsscorr_set_error("gnsscorr_acq_power_row: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  const int32_t gc = code, gf = 0;
+  int rc = stage_host(c, h_if, iq, n_blocks, 1, &freq, 1, 1, &gc, &gf);
+  if (rc) return rc;
+  if (!c->d_dump) HIP_TRY(hipMalloc(&c->d_dump, sizeof(float) * N));
+  rc = search_launch(c, c->d_if, iq, n_blocks, GNSSCORR_ACQ_BEST_OF_BLOCKS, 1, c->d_freqs, 1, 1,
+                     c->d_gcode, c->d_gfreq, 16, c->d_rows, nullptr, c->d_dump, block);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(h_power, c->d_dump, sizeof(float) * N, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_sync(gnsscorr_acq_ctx* c) {
+  if (!c) return GNSSCORR_EINVAL;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" void* gnsscorr_acq_stream(gnsscorr_acq_ctx* c) { return c ? (void*)c->stream : nullptr; }

@@ -188,9 +188,12 @@ int gnsscorr_ifgen(int8_t *out, int64_t nsamp, int iq, double fs, double if_gps,
         bi = ((bi % 4096) + 4096) % 4096;
         if ((bits[s][(bi >> 5) & 63] >> (bi & 31)) & 1u) v = -v;
       }
+      /* The reference front-end's complex IF is spectrum-inverted: the signal
+       * sits at -f (acquisition.sci:107-111 and the GP2021 mixer,
+       * correlator.c:213-215, both wipe off with exp(+i 2 pi f t)). */
       double ph = 2.0 * M_PI * fcar[s] * t + sigs[s].carr_phase;
       re += v * cos(ph);
-      im += v * sin(ph);
+      im -= v * sin(ph);
     }
     double u1 = lcg_unif(&g), u2 = lcg_unif(&g);
     double rad = sqrt(-2.0 * log(u1));

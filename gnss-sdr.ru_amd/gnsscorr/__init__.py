@@ -65,6 +65,9 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_acq_create", "gnsscorr_acq_destroy", "gnsscorr_acq_set_codes",
     "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
     "gnsscorr_acq_sync", "gnsscorr_acq_stream",
+    "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
+    "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
+    "gnsscorr_event_elapsed_ms", "gnsscorr_event_destroy", "gnsscorr_dev_fill_if2",
     "gnsscorr_ifgen", "gnsscorr_ca_code", "gnsscorr_st_code", "gnsscorr_sample_code",
     "correlator_init", "Sim_GP2021_int", "gnsscorr_osg_configure", "gnsscorr_osg_get_state",
 ]
@@ -86,7 +89,7 @@ def lib() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise GnssCorrError(f"{LIB_PATH} not built (run `make -C gnss-sdr.ru_amd`)")
-    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    L = C.CDLL(LIB_PATH)  # RTLD_LOCAL: never interpose REG_read etc. into other libraries
     P, I, I64, D, U64 = C.c_void_p, C.c_int, C.c_int64, C.c_double, C.c_uint64
     sig = {
         "gnsscorr_last_error": (C.c_char_p, []),
@@ -111,6 +114,16 @@ def lib() -> C.CDLL:
         "gnsscorr_acq_power_row": (I, [P, P, I, I, I, D, I, P]),
         "gnsscorr_acq_sync": (I, [P]),
         "gnsscorr_acq_stream": (P, [P]),
+        "gnsscorr_dev_alloc": (I, [I, C.c_size_t, C.POINTER(P)]),
+        "gnsscorr_dev_free": (I, [I, P]),
+        "gnsscorr_memcpy_htod": (I, [I, P, P, C.c_size_t]),
+        "gnsscorr_memcpy_dtoh": (I, [I, P, P, C.c_size_t]),
+        "gnsscorr_dev_synchronize": (I, [I]),
+        "gnsscorr_event_create": (I, [I, C.POINTER(P)]),
+        "gnsscorr_event_record": (I, [P, P]),
+        "gnsscorr_event_elapsed_ms": (I, [P, P, C.POINTER(C.c_float)]),
+        "gnsscorr_event_destroy": (I, [P]),
+        "gnsscorr_dev_fill_if2": (I, [I, P, C.c_size_t, U64]),
         "gnsscorr_ifgen": (I, [P, I64, I, D, D, D, I, P, U64]),
         "gnsscorr_ca_code": (I, [I, P]),
         "gnsscorr_st_code": (I, [P]),
@@ -142,6 +155,78 @@ def _ptr(a: np.ndarray) -> int:
 
 def device_count() -> int:
     return int(lib().gnsscorr_device_count())
+
+
+# ---------------------------------------------------------------- device memory
+class DevBuf:
+    """A HIP device allocation owned by libgnsscorr (no other GPU runtime)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.device = device
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        _check(lib().gnsscorr_dev_alloc(device, self.nbytes, C.byref(p)), "gnsscorr_dev_alloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_array(cls, a: np.ndarray, device: int = 0) -> "DevBuf":
+        a = np.ascontiguousarray(a)
+        b = cls(max(a.nbytes, 1), device)
+        b.upload(a)
+        return b
+
+    def upload(self, a: np.ndarray, offset: int = 0):
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        _check(lib().gnsscorr_memcpy_htod(self.device, self.ptr + offset, _ptr(a), a.nbytes),
+               "gnsscorr_memcpy_htod")
+
+    def download(self, dtype, count: int = -1, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        if count < 0:
+            count = (self.nbytes - offset) // dt.itemsize
+        out = np.empty(count, dt)
+        _check(lib().gnsscorr_memcpy_dtoh(self.device, _ptr(out), self.ptr + offset, out.nbytes),
+               "gnsscorr_memcpy_dtoh")
+        return out
+
+    def fill_if2(self, seed: int):
+        _check(lib().gnsscorr_dev_fill_if2(self.device, self.ptr, self.nbytes, seed),
+               "gnsscorr_dev_fill_if2")
+
+    def free(self):
+        if getattr(self, "ptr", None):
+            lib().gnsscorr_dev_free(self.device, self.ptr)
+            self.ptr = None
+
+    __del__ = free
+
+
+def dev_synchronize(device: int = 0):
+    _check(lib().gnsscorr_dev_synchronize(device), "gnsscorr_dev_synchronize")
+
+
+class Event:
+    """hipEvent_t wrapper for timing on a specific HIP stream."""
+
+    def __init__(self, device: int = 0):
+        p = C.c_void_p()
+        _check(lib().gnsscorr_event_create(device, C.byref(p)), "gnsscorr_event_create")
+        self.h = p
+
+    def record(self, stream: int):
+        _check(lib().gnsscorr_event_record(self.h, stream), "gnsscorr_event_record")
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = C.c_float()
+        _check(lib().gnsscorr_event_elapsed_ms(self.h, end.h, C.byref(ms)),
+               "gnsscorr_event_elapsed_ms")
+        return float(ms.value)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().gnsscorr_event_destroy(self.h)
+            self.h = None
 
 
 # ---------------------------------------------------------------- host utils

@@ -206,6 +206,22 @@ int gnsscorr_acq_sync(gnsscorr_acq_ctx *ctx);
 void *gnsscorr_acq_stream(gnsscorr_acq_ctx *ctx);
 
 /* ======================================================================
+ * Device buffers / events (so hosts need no other GPU runtime)
+ * ==================================================================== */
+int gnsscorr_dev_alloc(int device, size_t bytes, void **d_ptr);
+int gnsscorr_dev_free(int device, void *d_ptr);
+int gnsscorr_memcpy_htod(int device, void *d_dst, const void *h_src, size_t bytes);
+int gnsscorr_memcpy_dtoh(int device, void *h_dst, const void *d_src, size_t bytes);
+int gnsscorr_dev_synchronize(int device);
+int gnsscorr_event_create(int device, void **ev);
+int gnsscorr_event_record(void *ev, void *stream);
+int gnsscorr_event_elapsed_ms(void *start, void *stop, float *ms);
+int gnsscorr_event_destroy(void *ev);
+/* Fill a device buffer with pseudo-random 2-bit levels {-3,-1,1,3}
+ * (benchmark input of the recorded-IF shape; not a signal model). */
+int gnsscorr_dev_fill_if2(int device, int8_t *d_buf, size_t bytes, uint64_t seed);
+
+/* ======================================================================
  * Host utilities (deterministic synthetic IF, code tables)
  * ==================================================================== */
 
@@ -222,6 +238,8 @@ typedef struct {
 } gnsscorr_sig;
 
 /* Synthetic IF: nsamp complex samples (iq=1: 2*nsamp int8) or real (iq=0),
+ * each signal at -(IF + Doppler) in complex baseband (the reference's IQ
+ * convention: its wipe-offs multiply by exp(+i 2 pi f t)),
  * at fs with GPS IF `if_gps`, GLONASS IF `if_glo` (+ fch*562.5 kHz), plus
  * complex AWGN, quantised to the 2-bit levels {-3,-1,+1,+3}
  * (gps_source.cpp:692).  Deterministic for a given seed (64-bit LCG). */

@@ -1,0 +1,64 @@
+"""CPU: the C-ABI library loads and exports every symbol include/*.h declares
+(no compute calls: there is no GPU in this container)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDRS = [os.path.join(ROOT, "include", h) for h in ("gnsscorr.h", "gnsscorr_osg.h")]
+
+
+def _declared():
+    funcs, data = set(), set()
+    for h in HDRS:
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
+            name = m.group(1)
+            if name not in ("defined",):
+                funcs.add(name)
+        for m in re.finditer(r"^extern\s+(?:int|double|long)\s+([^;(]+);", txt, flags=re.M):
+            data.update(re.sub(r"\[.*?\]", "", x).strip() for x in m.group(1).split(","))
+    return funcs, data
+
+
+def test_headers_parse():
+    funcs, data = _declared()
+    assert {"correlator_init", "Sim_GP2021_int", "gnsscorr_track", "gnsscorr_acq_search"} <= funcs
+    assert {"REG_read", "REG_write", "gps_carrier_ref"} <= data
+
+
+def test_library_exports_every_declared_symbol(gc):
+    L = C.CDLL(gc.LIB_PATH)
+    funcs, data = _declared()
+    missing = [f for f in sorted(funcs | data) if not hasattr(L, f)]
+    assert not missing, missing
+    # the Python binding lists exactly the header's symbols
+    assert set(gc.EXPORTED_FUNCTIONS) == funcs
+    assert set(gc.EXPORTED_DATA) == data
+
+
+def test_reg_arrays_are_256_ints(gc):
+    L = gc.lib()
+    rr = (C.c_int * 256).in_dll(L, "REG_read")
+    rr[0x82] = 5
+    assert rr[0x82] == 5
+    rr[0x82] = 0
+
+
+def test_version_and_errors(gc):
+    assert b"gfx950" in gc.lib().gnsscorr_version()
+    # bad config is rejected on the host before any device call
+    cfg = gc.TrackCfg(0, 1, 0, 1024, 16.368e6, 0.0)
+    h = C.c_void_p()
+    assert gc.lib().gnsscorr_track_create(C.byref(h), C.byref(cfg)) == -1
+    assert b"bad config" in gc.lib().gnsscorr_last_error()
+
+
+def test_product_has_no_oracle_dependency(gc):
+    """The shipped library must not link or embed the oracle / reference code."""
+    so = open(gc.LIB_PATH, "rb").read()
+    for needle in (b"osgo_", b"liboracle", b"libosg_ref", b"ref_harness"):
+        assert needle not in so

@@ -137,7 +137,6 @@ def test_zero_if_gives_zero(gpu):
 
 
 def test_replay_equals_sequential(gpu):
-    import torch
     rng = np.random.default_rng(9)
     C, K, nsamp = 256, 6, 16368
     IF = S.synth_if(nsamp * K, 77, [(5, 10, 0, 3)])
@@ -148,12 +147,12 @@ def test_replay_equals_sequential(gpu):
         r, _ = seq.track(IF[k * nsamp * 2:(k + 1) * nsamp * 2], nsamp, cmds[k])
         seq_res.append(r)
     rep = gpu.TrackCtx(C, max_nsamp=nsamp)
-    d_if = torch.from_numpy(IF.copy()).cuda()
-    d_cmds = torch.from_numpy(cmds.view(np.uint8).copy()).cuda()
-    d_res = torch.zeros(K * C * gpu.TRACK_RESULT.itemsize, dtype=torch.uint8, device="cuda")
-    rep.replay_dev(d_if.data_ptr(), 0, nsamp, K, d_cmds.data_ptr(), d_res.data_ptr())
+    d_if = gpu.DevBuf.from_array(IF)
+    d_cmds = gpu.DevBuf.from_array(cmds)
+    d_res = gpu.DevBuf(K * C * gpu.TRACK_RESULT.itemsize)
+    rep.replay_dev(d_if.ptr, 0, nsamp, K, d_cmds.ptr, d_res.ptr)
     rep.sync()
-    got = d_res.cpu().numpy().view(gpu.TRACK_RESULT).reshape(K, C)
+    got = d_res.download(gpu.TRACK_RESULT).reshape(K, C)
     for k in range(K):
         np.testing.assert_array_equal(got[k]["n_dumps"], seq_res[k]["n_dumps"])
         np.testing.assert_array_equal(got[k]["dump"], seq_res[k]["dump"])
