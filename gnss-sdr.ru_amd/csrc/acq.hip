@@ -510,6 +510,7 @@ struct gnsscorr_acq_ctx {
   float2* d_F = nullptr;     // code spectra, permuted, [max_codes][N]
   float2* d_X = nullptr;     // IF spectra, permuted, [max_freqs*max_blocks][N]
   int n_codes = 0;
+  int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra
   // host-API staging
   int8_t* d_if = nullptr;
   double* d_freqs = nullptr;
@@ -624,20 +625,40 @@ extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const in
   return GNSSCORR_OK;
 }
 
-static int search_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int mode,
-                         int n_freqs, const double* d_freqs, int n_groups, int n_bins,
-                         const int32_t* d_gcode, const int32_t* d_gfreq, int spc,
-                         gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res, float* d_dump,
-                         int dump_block) {
+static int check_search(gnsscorr_acq_ctx* c, int n_blocks, int n_freqs, int mode) {
   if (n_blocks < 1 || n_blocks > c->cfg.max_blocks || n_freqs < 1 || n_freqs > c->cfg.max_freqs ||
-      n_groups < 1 || n_bins < 1 || spc < 1 || spc > N / 2 || c->n_codes < 1 ||
+      c->n_codes < 1 ||
       (mode != GNSSCORR_ACQ_BEST_OF_BLOCKS && mode != GNSSCORR_ACQ_NONCOHERENT)) {
-    gnsscorr_set_error("gnsscorr_acq_search: bad arguments");
+    gnsscorr_set_error("gnsscorr_acq: bad arguments (blocks %d/%d, freqs %d/%d, codes %d)",
+                       n_blocks, c->cfg.max_blocks, n_freqs, c->cfg.max_freqs, c->n_codes);
     return GNSSCORR_EINVAL;
   }
+  return GNSSCORR_OK;
+}
+
+static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks,
+                          int n_freqs, const double* d_freqs) {
+  int rc = check_search(c, n_blocks, n_freqs, GNSSCORR_ACQ_BEST_OF_BLOCKS);
+  if (rc) return rc;
   hipLaunchKernelGGL(acq_forward_kernel, dim3(n_freqs * n_blocks), dim3(kThreads), 0, c->stream,
                      d_if, iq, n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, 0, c->d_sigma, c->d_X);
   HIP_TRY(hipGetLastError());
+  c->spec_blocks = n_blocks;
+  c->spec_freqs = n_freqs;
+  return GNSSCORR_OK;
+}
+
+static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
+                            const double* d_freqs, const int32_t* d_gcode,
+                            const int32_t* d_gfreq, int spc, gnsscorr_acq_row* d_rows,
+                            gnsscorr_acq_result* d_res, float* d_dump, int dump_block) {
+  int rc = check_search(c, n_blocks, c->spec_freqs > 0 ? c->spec_freqs : 1, mode);
+  if (rc) return rc;
+  if (n_groups < 1 || n_bins < 1 || spc < 1 || spc > N / 2 || n_blocks != c->spec_blocks) {
+    gnsscorr_set_error("gnsscorr_acq_correlate: bad arguments (groups %d, bins %d, spc %d, "
+                       "blocks %d vs spectra %d)", n_groups, n_bins, spc, n_blocks, c->spec_blocks);
+    return GNSSCORR_EINVAL;
+  }
 #define ACQ_CORR_LAUNCH(M, D)                                                                  \
   hipLaunchKernelGGL((acq_corr_kernel<M, D>), dim3(n_groups * n_bins), dim3(kThreads), 0,       \
                      c->stream, c->d_X, c->d_F, n_blocks, d_gcode, d_gfreq, n_bins, spc, d_rows, \
@@ -655,6 +676,55 @@ static int search_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_
                        d_rows, n_groups, n_bins, d_gfreq, d_freqs, d_res);
     HIP_TRY(hipGetLastError());
   }
+  return GNSSCORR_OK;
+}
+
+static int search_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int mode,
+                         int n_freqs, const double* d_freqs, int n_groups, int n_bins,
+                         const int32_t* d_gcode, const int32_t* d_gfreq, int spc,
+                         gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res, float* d_dump,
+                         int dump_block) {
+  int rc = spectra_launch(c, d_if, iq, n_blocks, n_freqs, d_freqs);
+  if (rc) return rc;
+  return correlate_launch(c, n_blocks, mode, n_groups, n_bins, d_freqs, d_gcode, d_gfreq, spc,
+                          d_rows, d_res, d_dump, dump_block);
+}
+
+extern "C" int gnsscorr_acq_spectra_dev(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq,
+                                        int n_blocks, int n_freqs, const double* d_freqs) {
+  if (!c || !d_if || !d_freqs) {
+    gnsscorr_set_error("gnsscorr_acq_spectra_dev: null argument");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  return spectra_launch(c, d_if, iq, n_blocks, n_freqs, d_freqs);
+}
+
+extern "C" int gnsscorr_acq_correlate_dev(gnsscorr_acq_ctx* c, int n_blocks, int mode,
+                                          const double* d_freqs, int n_groups, int n_bins,
+                                          const int32_t* d_group_code,
+                                          const int32_t* d_group_freq, int spc,
+                                          gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res) {
+  if (!c || !d_group_code || !d_group_freq || !d_rows || (d_res && !d_freqs)) {
+    gnsscorr_set_error("gnsscorr_acq_correlate_dev: null argument");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  return correlate_launch(c, n_blocks, mode, n_groups, n_bins, d_freqs, d_group_code,
+                          d_group_freq, spc, d_rows, d_res, nullptr, -1);
+}
+
+extern "C" int gnsscorr_acq_select_dev(gnsscorr_acq_ctx* c, int n_groups, int n_bins,
+                                       const double* d_freqs, const int32_t* d_group_freq,
+                                       const gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res) {
+  if (!c || !d_freqs || !d_group_freq || !d_rows || !d_res || n_groups < 1 || n_bins < 1) {
+    gnsscorr_set_error("gnsscorr_acq_select_dev: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  hipLaunchKernelGGL(acq_select_kernel, dim3((n_groups + 63) / 64), dim3(64), 0, c->stream, d_rows,
+                     n_groups, n_bins, d_group_freq, d_freqs, d_res);
+  HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
 

@@ -64,6 +64,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_track_sync", "gnsscorr_track_stream",
     "gnsscorr_acq_create", "gnsscorr_acq_destroy", "gnsscorr_acq_set_codes",
     "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
+    "gnsscorr_acq_spectra_dev", "gnsscorr_acq_correlate_dev", "gnsscorr_acq_select_dev",
     "gnsscorr_acq_sync", "gnsscorr_acq_stream",
     "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
     "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
@@ -112,6 +113,9 @@ def lib() -> C.CDLL:
         "gnsscorr_acq_search": (I, [P, P, I, I, I, I, P, I, I, P, P, I, P, P]),
         "gnsscorr_acq_search_dev": (I, [P, P, I, I, I, I, P, I, I, P, P, I, P, P]),
         "gnsscorr_acq_power_row": (I, [P, P, I, I, I, D, I, P]),
+        "gnsscorr_acq_spectra_dev": (I, [P, P, I, I, I, P]),
+        "gnsscorr_acq_correlate_dev": (I, [P, I, I, P, I, I, P, P, I, P, P]),
+        "gnsscorr_acq_select_dev": (I, [P, I, I, P, P, P, P]),
         "gnsscorr_acq_sync": (I, [P]),
         "gnsscorr_acq_stream": (P, [P]),
         "gnsscorr_dev_alloc": (I, [I, C.c_size_t, C.POINTER(P)]),
@@ -381,6 +385,20 @@ class AcqCtx:
                                              d_freqs, n_groups, n_bins, d_group_code,
                                              d_group_freq, spc, d_rows, d_res),
                "gnsscorr_acq_search_dev")
+
+    def spectra_dev(self, d_if, n_blocks, n_freqs, d_freqs, iq=True):
+        _check(lib().gnsscorr_acq_spectra_dev(self.h, d_if, int(iq), n_blocks, n_freqs, d_freqs),
+               "gnsscorr_acq_spectra_dev")
+
+    def correlate_dev(self, n_blocks, d_freqs, n_groups, n_bins, d_group_code, d_group_freq,
+                      d_rows, d_res=None, spc=16, mode=ACQ_BEST_OF_BLOCKS):
+        _check(lib().gnsscorr_acq_correlate_dev(self.h, n_blocks, mode, d_freqs, n_groups, n_bins,
+                                                d_group_code, d_group_freq, spc, d_rows,
+                                                d_res or None), "gnsscorr_acq_correlate_dev")
+
+    def select_dev(self, n_groups, n_bins, d_freqs, d_group_freq, d_rows, d_res):
+        _check(lib().gnsscorr_acq_select_dev(self.h, n_groups, n_bins, d_freqs, d_group_freq,
+                                             d_rows, d_res), "gnsscorr_acq_select_dev")
 
     def power_row(self, if_samples, n_blocks, block, freq, code, iq=True) -> np.ndarray:
         if_samples = np.ascontiguousarray(if_samples, np.int8)

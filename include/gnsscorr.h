@@ -199,6 +199,23 @@ int gnsscorr_acq_search_dev(gnsscorr_acq_ctx *ctx, const int8_t *d_if, int iq, i
                             int n_bins, const int32_t *d_group_code, const int32_t *d_group_freq,
                             int spc, gnsscorr_acq_row *d_rows, gnsscorr_acq_result *d_res);
 
+/* The two stages of gnsscorr_acq_search_dev, for re-correlating resident
+ * spectra with another code set or timing the stages separately:
+ *  spectra:   wipe-off + FFT of every (freq, block), kept in the context
+ *  correlate: conj-multiply + IFFT + |.|^2 + peak search of every group row
+ *             (d_res may be NULL: rows only, no per-group selection). */
+int gnsscorr_acq_spectra_dev(gnsscorr_acq_ctx *ctx, const int8_t *d_if, int iq, int n_blocks,
+                             int n_freqs, const double *d_freqs);
+int gnsscorr_acq_correlate_dev(gnsscorr_acq_ctx *ctx, int n_blocks, int mode,
+                               const double *d_freqs, int n_groups, int n_bins,
+                               const int32_t *d_group_code, const int32_t *d_group_freq, int spc,
+                               gnsscorr_acq_row *d_rows, gnsscorr_acq_result *d_res);
+
+/* Per-group selection (acquisition.sci:141-186) over rows already computed. */
+int gnsscorr_acq_select_dev(gnsscorr_acq_ctx *ctx, int n_groups, int n_bins, const double *d_freqs,
+                            const int32_t *d_group_freq, const gnsscorr_acq_row *d_rows,
+                            gnsscorr_acq_result *d_res);
+
 /* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples floats. */
 int gnsscorr_acq_power_row(gnsscorr_acq_ctx *ctx, const int8_t *h_if, int iq, int n_blocks,
                            int block, double freq, int code, float *h_power);

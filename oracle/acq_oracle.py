@@ -165,3 +165,40 @@ def acquire(IF, fs, codes, freqs, group_freq, group_code=None, spc=16, n_blocks=
                         code_phase=code_phase, carr_freq=float(freqs[group_freq[g, bin_idx]])))
         rows_out.append(rows)
     return (out, rows_out) if return_rows else out
+
+
+def acquire_batched(IF, fs, codes, freqs, group_freq, group_code=None, spc=16, n_blocks=2,
+                    iq=True, workers=1):
+    """Same fp64 algorithm as acquire(), batched over bins with scipy's
+    multithreaded pocketfft.  Used as bench.py's CPU baseline only."""
+    import scipy.fft as sfft
+    codes = np.asarray(codes)
+    group_freq = np.asarray(group_freq)
+    G, B = group_freq.shape
+    if group_code is None:
+        group_code = np.arange(G)
+    N = codes.shape[1]
+    sig = _signal(IF, iq)[:n_blocks * N].reshape(n_blocks, N)
+    phase_points = np.arange(N) * 2 * np.pi * (1.0 / fs)
+    fidx = np.unique(group_freq)
+    carr = np.exp(1j * np.asarray(freqs)[fidx][:, None] * phase_points[None, :])
+    spec = sfft.fft(carr[:, None, :] * sig[None, :, :], axis=-1, workers=workers)
+    row_of = {int(f): i for i, f in enumerate(fidx)}
+    out = []
+    for g in range(G):
+        cf = np.conj(sfft.fft(codes[group_code[g]].astype(np.float64), workers=workers))
+        X = spec[[row_of[int(f)] for f in group_freq[g]]]          # (B, blocks, N)
+        P = np.abs(sfft.ifft(X * cf[None, None, :], axis=-1, workers=workers)) ** 2
+        mx = P.max(axis=-1)                                          # (B, blocks)
+        chosen = np.zeros(B, np.int64)
+        for k in range(1, n_blocks):
+            repl = ~(mx[np.arange(B), chosen] > mx[:, k])
+            chosen[repl] = k
+        results = P[np.arange(B), chosen]
+        row_max = results.max(axis=1)
+        bin_idx = int(np.argmax(row_max))
+        code_phase = int(np.argmax(results.max(axis=0))) + 1
+        second = _second_peak(results[bin_idx], code_phase, spc)
+        out.append(dict(peak=row_max.max(), second=second, metric=row_max.max() / second,
+                        bin=bin_idx, code_phase=code_phase))
+    return out

@@ -190,7 +190,7 @@ void osgo_sim(osgo_t *o, const int8_t *IF, long nsamp)
 
 /* ---- threaded CPU baseline ------------------------------------------------ */
 typedef struct {
-  int first, last, n_channels, n_calls; long nsamp; const int8_t *IF;
+  int first, last, n_channels, n_calls, if_calls; long nsamp; const int8_t *IF;
   long cf, kf; double work;
 } job_t;
 
@@ -205,9 +205,9 @@ static void *bench_worker(void *arg)
       osgo_ch_carrier(o, ch, j->cf + 13 * ch);
       osgo_ch_code(o, ch, j->kf);
     }
-    const int8_t *base = j->IF + (size_t)inst * (size_t)j->n_calls * (size_t)j->nsamp * 2;
+    const int8_t *base = j->IF + (size_t)inst * (size_t)j->if_calls * (size_t)j->nsamp * 2;
     for (int c = 0; c < j->n_calls; c++) {
-      osgo_sim(o, base + (size_t)c * (size_t)j->nsamp * 2, j->nsamp);
+      osgo_sim(o, base + (size_t)(c % j->if_calls) * (size_t)j->nsamp * 2, j->nsamp);
       j->work += (double)j->n_channels * (double)j->nsamp;
     }
   }
@@ -216,7 +216,7 @@ static void *bench_worker(void *arg)
 }
 
 double osgo_bench(int n_inst, int n_channels, const int8_t *IF, long nsamp, int n_calls,
-                  long carrier_freq, long code_freq, int threads)
+                  int if_calls, long carrier_freq, long code_freq, int threads)
 {
   if (!g_img_ready) build_tables();
   if (threads < 1) threads = 1;
@@ -227,6 +227,7 @@ double osgo_bench(int n_inst, int n_channels, const int8_t *IF, long nsamp, int 
     jobs[t].first = (int)((long)n_inst * t / threads);
     jobs[t].last  = (int)((long)n_inst * (t + 1) / threads);
     jobs[t].n_channels = n_channels; jobs[t].n_calls = n_calls; jobs[t].nsamp = nsamp;
+    jobs[t].if_calls = if_calls;
     jobs[t].IF = IF; jobs[t].cf = carrier_freq; jobs[t].kf = code_freq; jobs[t].work = 0;
     pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
   }

@@ -47,10 +47,11 @@ void osgo_ch_epoch_load(osgo_t *o, int ch, unsigned data);
 int  osgo_reg_read(const osgo_t *o, int addr);   /* from_gps: truncates to short */
 
 /* Multi-threaded CPU baseline: run `n_inst` independent correlator instances
- * (each n_channels, own IF stream of n_calls*nsamp complex samples) for
- * n_calls calls with OpenMP-free pthreads.  Returns total channel-samples. */
+ * (each n_channels on its own IF stream of if_calls*nsamp complex samples,
+ * replayed cyclically) for n_calls calls on `threads` pthreads.  Returns the
+ * total channel-samples processed. */
 double osgo_bench(int n_inst, int n_channels, const int8_t *IF, long nsamp, int n_calls,
-                  long carrier_freq, long code_freq, int threads);
+                  int if_calls, long carrier_freq, long code_freq, int threads);
 
 int  osgo_sizeof(void);
 #endif

@@ -51,8 +51,8 @@ class OracleOSG:
         L.osgo_table_bytes.restype = C.c_int
         L.osgo_table_image.argtypes = [C.c_void_p]
         L.osgo_bench.restype = C.c_double
-        L.osgo_bench.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_long, C.c_int, C.c_long,
-                                 C.c_long, C.c_int]
+        L.osgo_bench.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_long, C.c_int, C.c_int,
+                                 C.c_long, C.c_long, C.c_int]
         self.L = L
         self.buf = C.create_string_buffer(L.osgo_sizeof())
         self.p = C.cast(self.buf, C.c_void_p)
