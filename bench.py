@@ -100,8 +100,7 @@ def acq_step(ctx, b, ev=None):
     ctx.spectra_dev(b["d_if"].ptr, N_BLK, N_BINS, b["d_freqs"].ptr)
     if ev:
         ev[0].record(ctx.stream)
-    ctx.correlate_dev(N_BLK, b["d_freqs"].ptr, N_PRN, N_BINS, b["d_gcode"].ptr, b["d_gfreq"].ptr,
-                      b["d_rows"].ptr)
+    ctx.correlate_dev(N_BLK, b["d_freqs"].ptr, N_PRN, N_BINS, b["d_gcode"].ptr, b["d_gfreq"].ptr)
     if ev:
         ev[1].record(ctx.stream)
     ctx.select_dev(N_PRN, N_BINS, b["d_freqs"].ptr, b["d_gfreq"].ptr, b["d_rows"].ptr,

@@ -42,6 +42,12 @@
     }                                                                                   \
   } while (0)
 
+// Diagnostic hook: tools/acq_stamps.hip defines ACQ_STAMP(i) to record
+// s_memtime at phase boundaries; in the library it compiles to nothing.
+#ifndef ACQ_STAMP
+#define ACQ_STAMP(i)
+#endif
+
 namespace {
 
 constexpr int N = 16368;
@@ -49,6 +55,10 @@ constexpr int M16 = N / 16, M3 = N / 3, M11 = N / 11, M31 = N / 31;  // 1023 545
 // CRT idempotents e_i = 1 mod N_i, 0 mod N_j (checked on the host at create)
 constexpr int E16 = 15345, E3 = 10912, E11 = 5952, E31 = 528;
 constexpr int kThreads = 512;           // 8 wavefronts -> up to 256 VGPRs each
+// Spectra rows in HBM are padded to 16 planes x 1024 complex (128 KiB) so the
+// radix-16 loads are 16-byte aligned: LDS position a*1023+g <-> a*1024+g.
+constexpr int kPlane = 1024;
+constexpr int NPAD = 16 * kPlane;
 constexpr int kGroups31 = N / 31;       // 528 radix-31 groups
 constexpr int kLeft = kGroups31 - kThreads;  // 16 groups done as direct dot products
 
@@ -187,14 +197,33 @@ __device__ __forceinline__ int in_index(int p) {  // Ruritanian input map n(p)
 }
 
 // ---- the three in-LDS passes (16, 3x11, 31) ----------------------------------
-__device__ __forceinline__ void pass16(float2* lds, int t) {
-  for (int g = t; g < M16; g += kThreads) {
-    float2 x[16];
+// Correlation-kernel first pass straight from HBM/L2: every thread owns the
+// two adjacent radix-16 groups g = 2t, 2t+1 and reads them as ONE 16-byte
+// buffer load per plane a (scalar plane offset a*8 KiB, 32-bit lane offset),
+// forms D = conj(X) * F, runs both DFT16s in registers and writes LDS once.
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load_mul_pass16(const float2* __restrict__ Xb,
+                                                const float2* __restrict__ Fc, float2* lds,
+                                                int t) {
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, 0, NPAD * 8, 0x00020000);
+  const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)Fc, 0, NPAD * 8, 0x00020000);
+  const int g0 = 2 * t;
+  const int voff = g0 * 8;
+  float2 x0[16], x1[16];
 #pragma unroll
-    for (int a = 0; a < 16; a++) x[a] = lds[a * M16 + g];
-    dft16(x);
+  for (int a = 0; a < 16; a++) {
+    const f4v u = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, a * kPlane * 8, 0));
+    const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
+    x0[a] = make_float2(u.x * f.x + u.y * f.y, u.x * f.y - u.y * f.x);
+    x1[a] = make_float2(u.z * f.z + u.w * f.w, u.z * f.w - u.w * f.z);
+  }
+  dft16(x0);
+  dft16(x1);
+  const bool two = g0 + 1 < M16;
 #pragma unroll
-    for (int a = 0; a < 16; a++) lds[a * M16 + g] = x[a];
+  for (int a = 0; a < 16; a++) {
+    lds[a * M16 + g0] = x0[a];
+    if (two) lds[a * M16 + g0 + 1] = x1[a];
   }
 }
 
@@ -242,56 +271,87 @@ __device__ __forceinline__ void init_tw31(float2* tw) {
 // natural output index of LDS position t*31 + d': k = (a E16 + b E3 + c E11 + d' E31) mod N
 __device__ __forceinline__ int out_base(int t) {
   const int a = t / 33, bc = t % 33, b = bc / 11, c = bc % 11;
-  return (int)(((long)a * E16 + (long)b * E3 + (long)c * E11) % N);
+  return (a * E16 + b * E3 + c * E11) % N;  // < 2^31: 32-bit modulo
 }
 
 // ---- forward spectra: wiped-off IF rows and code rows --------------------------
+// The forward transforms are latency-bound (82 rows for a GPS search), so each
+// row is split over many small workgroups with the prime-factor structure:
+//   K1: wipe-off + radix-16 pass, 4 workgroups x 256 groups per row -> HBM
+//       staging T[row][a'][1024]
+//   K2: the 16 independent 1023-point (3 x 11 x 31) sub-transforms of a row,
+//       one wavefront each, written straight to the correlation layout (sigma).
 // mode 0: IF row = (freq_id, block); x[n] = IF[block][n] * exp(i f ((n*2)*pi)*ts)
 // mode 1: code row c; x[n] = code[c][n]
-__global__ __launch_bounds__(kThreads) void acq_forward_kernel(
+constexpr int kFwd1Threads = 256;
+__global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
     const int8_t* __restrict__ src, int iq, int n_blocks, const double* __restrict__ freqs,
-    double ts, int mode, const int* __restrict__ sigma, float2* __restrict__ out) {
-  __shared__ float2 lds[N];
-  __shared__ float2 tw[32];
-  const int row = blockIdx.x;
-  const int t = threadIdx.x;
-  init_tw31(tw);
+    double ts, int mode, float2* __restrict__ stage) {
+  const int row = blockIdx.x >> 2;
+  const int g = (blockIdx.x & 3) * kFwd1Threads + threadIdx.x;
+  if (g >= M16) return;
+  float2 x[16];
   if (mode == 0) {
     const int fid = row / n_blocks, blk = row % n_blocks;
     const double f = freqs[fid];
     const int8_t* s = src + (long)blk * N * (iq ? 2 : 1);
-    for (int p = t; p < N; p += kThreads) {
-      const int n = in_index(p);
+#pragma unroll
+    for (int a = 0; a < 16; a++) {
+      const int n = in_index(a * M16 + g);
       const double I = iq ? (double)s[2 * n] : (double)s[n];
       const double Q = iq ? (double)s[2 * n + 1] : 0.0;
       // acquisition.sci:61-62, 107: phasePoints = (0:N-1)*2*%pi*ts; exp(i f pp)
       const double th = f * ((((double)n * 2.0) * M_PI) * ts);
       double sn, cs;
       sincos(th, &sn, &cs);
-      lds[p] = make_float2((float)(I * cs - Q * sn), (float)(I * sn + Q * cs));
+      x[a] = make_float2((float)(I * cs - Q * sn), (float)(I * sn + Q * cs));
     }
   } else {
     const int8_t* s = src + (long)row * N;
-    for (int p = t; p < N; p += kThreads) lds[p] = make_float2((float)s[in_index(p)], 0.f);
+#pragma unroll
+    for (int a = 0; a < 16; a++) x[a] = make_float2((float)s[in_index(a * M16 + g)], 0.f);
+  }
+  dft16(x);
+  float2* o = stage + (long)row * NPAD + g;
+#pragma unroll
+  for (int a = 0; a < 16; a++) o[a * kPlane] = x[a];
+}
+
+__global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restrict__ stage,
+                                                        const int* __restrict__ sigma,
+                                                        float2* __restrict__ out) {
+  __shared__ float2 sub[M16 + 1];
+  const int row = blockIdx.x >> 4, a = blockIdx.x & 15;
+  const int lane = threadIdx.x;
+  const float2* in = stage + (long)row * NPAD + a * kPlane;
+  for (int i = lane; i < M16; i += 64) sub[i] = in[i];
+  __syncthreads();
+  if (lane < 31) {  // 3 x 11 over (b, c) for fixed d = lane
+    float2 v[3][11];
+#pragma unroll
+    for (int b = 0; b < 3; b++)
+#pragma unroll
+      for (int c = 0; c < 11; c++) v[b][c] = sub[(b * 11 + c) * 31 + lane];
+#pragma unroll
+    for (int c = 0; c < 11; c++) dft3(v[0][c], v[1][c], v[2][c]);
+#pragma unroll
+    for (int b = 0; b < 3; b++) dftp<11>(v[b]);
+#pragma unroll
+    for (int b = 0; b < 3; b++)
+#pragma unroll
+      for (int c = 0; c < 11; c++) sub[(b * 11 + c) * 31 + lane] = v[b][c];
   }
   __syncthreads();
-  pass16(lds, t);
-  __syncthreads();
-  pass33(lds, t);
-  __syncthreads();
-  float2* o = out + (long)row * N;
-  float2 y = make_float2(0.f, 0.f);
-  const bool extra = t < kLeft * 31;
-  if (extra) y = dft31_single(lds, tw, t);
-  {
+  if (lane < 33) {  // radix 31 over d for fixed (b, c) = lane
     float2 x[31];
 #pragma unroll
-    for (int d = 0; d < 31; d++) x[d] = lds[t * 31 + d];
+    for (int d = 0; d < 31; d++) x[d] = sub[lane * 31 + d];
     dftp<31>(x);
+    float2* o = out + (long)row * NPAD;
+    const int p0 = a * M16 + lane * 31;
 #pragma unroll
-    for (int d = 0; d < 31; d++) o[sigma[t * 31 + d]] = x[d];
+    for (int d = 0; d < 31; d++) o[sigma[p0 + d]] = x[d];
   }
-  if (extra) o[sigma[kThreads * 31 + t]] = y;
 }
 
 // ---- block-level reductions ---------------------------------------------------
@@ -336,20 +396,29 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
   return v;
 }
 
-// ---- the hot kernel: one (group, bin) row per workgroup ------------------------
+// ---- the hot kernel ------------------------------------------------------------
+// One workgroup = one work unit: BEST_OF_BLOCKS -> unit = (row, block), the
+// statistics of that block go to stats[unit]; NONCOHERENT -> unit = row, |.|^2
+// summed over the blocks in registers, stats to stats[row * n_blocks].
+// (Row-sized units would leave the last of ~5 rounds of workgroups 1/8 full.)
 // Every thread owns radix-31 group t (positions t*31 .. t*31+30) and threads
 // t < 496 also own one output of the 16 leftover groups (position 512*31 + t).
 template <int MODE, bool DUMP>
 __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
     const float2* __restrict__ X, const float2* __restrict__ F, int n_blocks,
     const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins,
-    int spc, gnsscorr_acq_row* __restrict__ rows, float* __restrict__ dump_power,
-    int dump_block) {
+    int spc, gnsscorr_acq_row* __restrict__ stats, float* __restrict__ dump_power,
+    int dump_block, const int* __restrict__ order) {
   __shared__ float2 lds[N];
   __shared__ float2 tw[32];
   __shared__ PeakSlot s_pk[kThreads / 64];
   __shared__ float s_mx[kThreads / 64];
-  const int rowid = blockIdx.x;
+  constexpr bool kNonCoh = MODE == GNSSCORR_ACQ_NONCOHERENT;
+  ACQ_STAMP(12);
+  const int unit = order[blockIdx.x];
+  const int rowid = kNonCoh ? unit : unit / n_blocks;
+  const int blk0 = kNonCoh ? 0 : unit % n_blocks;
+  const int nblk = kNonCoh ? n_blocks : 1;
   const int g = rowid / n_bins, bin = rowid % n_bins;
   const int code = group_code[g];
   const int fid = group_freq[g * n_bins + bin];
@@ -358,30 +427,28 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
   const bool extra = t < kLeft * 31;
   const int kb = out_base(t);
   // natural index of the leftover output owned by this thread
-  const int kx = (int)(((long)out_base(kThreads + t / 31) + (long)(t % 31) * E31) % N);
+  const int kx = (out_base(kThreads + t / 31) + (t % 31) * E31) % N;
   init_tw31(tw);
 
-  constexpr bool kNonCoh = MODE == GNSSCORR_ACQ_NONCOHERENT;
   constexpr int kAcc = kNonCoh ? 32 : 1;
   float pacc[kAcc];
 #pragma unroll
   for (int d = 0; d < kAcc; d++) pacc[d] = 0.f;
   float best_pk = -1.f, best_sec = 0.f;
-  int best_k = 0, best_blk = 0;
+  int best_k = 0;
 
-  const float2* Fc = F + (long)code * N;
-  for (int blk = 0; blk < n_blocks; blk++) {
-    const float2* Xb = X + ((long)fid * n_blocks + blk) * N;
-    // D = conj(X) * F  (= conj(X * conj(F)), acquisition.sci:116)
-    for (int p = t; p < N; p += kThreads) {
-      const float2 x = Xb[p], f = Fc[p];
-      lds[p] = make_float2(x.x * f.x + x.y * f.y, x.x * f.y - x.y * f.x);
-    }
+  const float2* Fc = F + (long)code * NPAD;
+  for (int i = 0; i < nblk; i++) {
+    const int blk = blk0 + i;
+    const float2* Xb = X + ((long)fid * n_blocks + blk) * NPAD;
+    ACQ_STAMP(i * 6 + 0);
+    // D = conj(X) * F  (= conj(X * conj(F)), acquisition.sci:116), then radix-16
+    load_mul_pass16(Xb, Fc, lds, t);
     __syncthreads();
-    pass16(lds, t);
-    __syncthreads();
+    ACQ_STAMP(i * 6 + 1);
     pass33(lds, t);
     __syncthreads();
+    ACQ_STAMP(i * 6 + 2);
     float pw[32];  // pw[31] = this thread's leftover output (or -1)
     {
       const float2 y = extra ? dft31_single(lds, tw, t) : make_float2(0.f, 0.f);
@@ -393,6 +460,7 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
 #pragma unroll
       for (int d = 0; d < 31; d++) pw[d] = (x[d].x * x[d].x + x[d].y * x[d].y) * inv_n2;
     }
+    ACQ_STAMP(i * 6 + 3);
     if (DUMP && blk == dump_block) {
       int k = kb;
 #pragma unroll
@@ -407,85 +475,116 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
 #pragma unroll
       for (int d = 0; d < 32; d++) pacc[d % kAcc] += pw[d];
       __syncthreads();  // LDS is rewritten by the next block
-      if (blk + 1 < n_blocks) continue;
+      if (i + 1 < nblk) continue;
 #pragma unroll
       for (int d = 0; d < 31; d++) pw[d] = pacc[d % kAcc];
       pw[31] = extra ? pacc[31 % kAcc] : -1.f;
     }
-    // row maximum with the first (smallest natural index) occurrence
-    float v = pw[31];
-    int kk = extra ? kx : 0x7fffffff;
-    {
-      int k = kb;
+    // Row statistics.  Thread t's 31 strided outputs sit at natural indices
+    // kb + 528 d (mod N), so ANY window of < 528 samples holds at most one of
+    // them: a per-thread top-2 (max + fmed3) gives the largest value outside
+    // the +-spc window without a second pass.  The leftover output (kx) is
+    // handled on its own.  Within-thread exact ties keep the first slot
+    // (slot order, not natural order).
+    float m1 = -1.f, m2 = -1.f;
+    int d1 = 0;
 #pragma unroll
-      for (int d = 0; d < 31; d++) {
-        if (better(pw[d], k, v, kk)) { v = pw[d]; kk = k; }
-        k += E31;
-        if (k >= N) k -= N;
-      }
+    for (int d = 0; d < 31; d++) {
+      const float v = pw[d];
+      d1 = v > m1 ? d : d1;
+      m2 = __builtin_amdgcn_fmed3f(m2, m1, v);
+      m1 = fmaxf(m1, v);
     }
+    int k1 = kb + d1 * E31;
+    if (k1 >= N) k1 -= N;
+    float v = m1;
+    int kk = k1;
+    if (extra && better(pw[31], kx, v, kk)) { v = pw[31]; kk = kx; }
     block_argmax(v, kk, s_pk);
+    ACQ_STAMP(i * 6 + 4);
     // second peak outside the open window (argmax - spc, argmax + spc), circular
-    float sv = -1.f;
-    {
-      int k = kb;
-#pragma unroll
-      for (int d = 0; d < 32; d++) {
-        const int kd = d == 31 ? kx : k;
-        int dist = kd - kk;
-        if (dist < 0) dist += N;
-        if ((d < 31 || extra) && dist >= spc && dist <= N - spc) sv = fmaxf(sv, pw[d]);
-        k += E31;
-        if (k >= N) k -= N;
-      }
-    }
+    auto in_win = [&](int k) {
+      int dist = k - kk;
+      if (dist < 0) dist += N;
+      return dist < spc || dist > N - spc;
+    };
+    float sv = in_win(k1) ? m2 : m1;
+    if (extra && !in_win(kx)) sv = fmaxf(sv, pw[31]);
     sv = block_max(sv, s_mx);
-    // acquisition.sci:126-132: a later block replaces the kept one unless the
-    // kept block's max is strictly larger
-    if (blk == 0 || !(best_pk > v)) {
-      best_pk = v;
-      best_k = kk;
-      best_sec = sv;
-      best_blk = blk;
-    }
+    ACQ_STAMP(i * 6 + 5);
+    best_pk = v;
+    best_k = kk;
+    best_sec = sv;
   }
   if (t == 0) {
     gnsscorr_acq_row r;
     r.peak = best_pk;
     r.argmax = best_k;
     r.second = best_sec;
-    r.block = kNonCoh ? -1 : best_blk;
-    rows[rowid] = r;
+    r.block = kNonCoh ? -1 : blk0;
+    stats[(long)rowid * n_blocks + blk0] = r;
   }
+  ACQ_STAMP(13);
 }
 
-// acquisition.sci:141-186 per group: frequencyBinIndex = first row with the
-// largest max; codePhase = first column holding it; metric = peak / second.
-__global__ void acq_select_kernel(const gnsscorr_acq_row* __restrict__ rows, int n_groups,
-                                  int n_bins, const int* __restrict__ group_freq,
-                                  const double* __restrict__ freqs,
-                                  gnsscorr_acq_result* __restrict__ res) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n_groups) return;
-  const gnsscorr_acq_row* r = rows + (long)g * n_bins;
-  float pk = r[0].peak;
-  int bin = 0;
-  for (int b = 1; b < n_bins; b++)
-    if (r[b].peak > pk) { pk = r[b].peak; bin = b; }
+// Per group (one wavefront, bins across lanes):
+//  combine   acquisition.sci:126-132 -- per bin keep block 1 only if its max
+//            is strictly larger than block 2's (generalised: a later block
+//            replaces the kept one unless the kept max is strictly larger);
+//  select    acquisition.sci:141-186 -- frequencyBinIndex = first row with the
+//            largest max, codePhase = first column holding it, metric =
+//            peak / second.
+__device__ __forceinline__ gnsscorr_acq_row combine_blocks(const gnsscorr_acq_row* st,
+                                                          int n_blocks, int mode) {
+  gnsscorr_acq_row r = st[0];
+  if (mode != GNSSCORR_ACQ_NONCOHERENT)
+    for (int k = 1; k < n_blocks; k++)
+      if (!(r.peak > st[k].peak)) r = st[k];
+  return r;
+}
+
+__global__ __launch_bounds__(64) void acq_select_kernel(
+    const gnsscorr_acq_row* __restrict__ stats, int n_groups, int n_bins, int n_blocks, int mode,
+    const int* __restrict__ group_freq, const double* __restrict__ freqs,
+    gnsscorr_acq_row* __restrict__ rows, gnsscorr_acq_result* __restrict__ res) {
+  const int g = blockIdx.x;
+  const int lane = threadIdx.x;
+  const gnsscorr_acq_row* st = stats + (long)g * n_bins * n_blocks;
+  float pk = -1.f;
+  int bin = 0x7fffffff;
+  for (int b = lane; b < n_bins; b += 64) {
+    const gnsscorr_acq_row r = combine_blocks(st + (long)b * n_blocks, n_blocks, mode);
+    rows[(long)g * n_bins + b] = r;
+    if (r.peak > pk) { pk = r.peak; bin = b; }
+  }
+  if (!res) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(pk, o, 64);
+    const int b2 = __shfl_xor(bin, o, 64);
+    if (v2 > pk || (v2 == pk && b2 < bin)) { pk = v2; bin = b2; }
+  }
   int cp = 0x7fffffff;
-  for (int b = 0; b < n_bins; b++)
-    if (r[b].peak == pk && r[b].argmax < cp) cp = r[b].argmax;
-  gnsscorr_acq_result o;
-  o.peak = pk;
-  o.second = r[bin].second;
-  o.metric = pk / r[bin].second;
-  o.bin = bin;
-  o.code_phase = cp + 1;
-  // 1 if an exact tie put the global first column in another row than the
-  // winning row's own argmax (second peak then centred on the row's argmax)
-  o.pad = cp != r[bin].argmax;
-  o.carr_freq = freqs[group_freq[(long)g * n_bins + bin]];
-  res[g] = o;
+  for (int b = lane; b < n_bins; b += 64) {
+    const gnsscorr_acq_row r = combine_blocks(st + (long)b * n_blocks, n_blocks, mode);
+    if (r.peak == pk) cp = min(cp, r.argmax);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cp = min(cp, __shfl_xor(cp, o, 64));
+  if (lane == 0) {
+    const gnsscorr_acq_row rb = combine_blocks(st + (long)bin * n_blocks, n_blocks, mode);
+    gnsscorr_acq_result o;
+    o.peak = pk;
+    o.second = rb.second;
+    o.metric = pk / rb.second;
+    o.bin = bin;
+    o.code_phase = cp + 1;
+    // 1 if an exact tie put the global first column in another row than the
+    // winning row's own argmax (second peak then centred on the row's argmax)
+    o.pad = cp != rb.argmax;
+    o.carr_freq = freqs[group_freq[(long)g * n_bins + bin]];
+    res[g] = o;
+  }
 }
 
 // ---- host-side index tables ---------------------------------------------------
@@ -511,6 +610,14 @@ struct gnsscorr_acq_ctx {
   float2* d_X = nullptr;     // IF spectra, permuted, [max_freqs*max_blocks][N]
   int n_codes = 0;
   int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra
+  int* d_order = nullptr;               // workgroup -> work-unit permutation (XCD tiles)
+  int order_groups = 0, order_bins = 0, order_units = 0;
+  size_t cap_order = 0;
+  float2* d_stage = nullptr;            // forward-FFT staging rows
+  size_t cap_stage = 0;
+  gnsscorr_acq_row* d_stats = nullptr;  // per (row, block) statistics
+  size_t cap_stats = 0;
+  int stat_groups = 0, stat_bins = 0, stat_blocks = 0, stat_mode = 0;
   // host-API staging
   int8_t* d_if = nullptr;
   double* d_freqs = nullptr;
@@ -521,6 +628,9 @@ struct gnsscorr_acq_ctx {
   float* d_dump = nullptr;
   size_t cap_rows = 0, cap_res = 0, cap_gcode = 0, cap_gfreq = 0;
 };
+
+static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
+                          const double* d_freqs, int mode, int n_rows, float2* dst);
 
 static int grow(void** p, size_t* cap, size_t need, size_t elem) {
   if (need <= *cap) return GNSSCORR_OK;
@@ -569,8 +679,10 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
   };
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_sigma, sizeof(int) * N) != hipSuccess ||
-      hipMalloc(&c->d_F, sizeof(float2) * N * (size_t)cfg->max_codes) != hipSuccess ||
-      hipMalloc(&c->d_X, sizeof(float2) * N * (size_t)cfg->max_freqs * cfg->max_blocks) != hipSuccess ||
+      hipMalloc(&c->d_F, sizeof(float2) * NPAD * (size_t)cfg->max_codes) != hipSuccess ||
+      hipMalloc(&c->d_X, sizeof(float2) * NPAD * (size_t)cfg->max_freqs * cfg->max_blocks) != hipSuccess ||
+      hipMemset(c->d_F, 0, sizeof(float2) * NPAD * (size_t)cfg->max_codes) != hipSuccess ||
+      hipMemset(c->d_X, 0, sizeof(float2) * NPAD * (size_t)cfg->max_freqs * cfg->max_blocks) != hipSuccess ||
       hipMalloc(&c->d_if, (size_t)N * 2 * cfg->max_blocks) != hipSuccess ||
       hipMalloc(&c->d_freqs, sizeof(double) * cfg->max_freqs) != hipSuccess) {
     gnsscorr_set_error("gnsscorr_acq_create: device allocation failed");
@@ -581,7 +693,10 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
   int* inv_in = (int*)malloc(sizeof(int) * N);
   int* sigma = (int*)malloc(sizeof(int) * N);
   for (int p = 0; p < N; p++) inv_in[host_in_index(p)] = p;
-  for (int p = 0; p < N; p++) sigma[p] = inv_in[host_out_index(p)];
+  for (int p = 0; p < N; p++) {
+    const int q = inv_in[host_out_index(p)];          // LDS position in the correlation kernel
+    sigma[p] = (q / M16) * kPlane + q % M16;          // padded HBM index
+  }
   hipError_t e = hipMemcpy(c->d_sigma, sigma, sizeof(int) * N, hipMemcpyHostToDevice);
   free(inv_in);
   free(sigma);
@@ -597,8 +712,8 @@ extern "C" int gnsscorr_acq_destroy(gnsscorr_acq_ctx* c) {
   if (!c) return GNSSCORR_OK;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_sigma, c->d_F, c->d_X, c->d_if, c->d_freqs, c->d_gcode,
-                  c->d_gfreq, c->d_rows, c->d_res, c->d_dump};
+  void* bufs[] = {c->d_sigma, c->d_F, c->d_X, c->d_if, c->d_freqs, c->d_gcode, c->d_gfreq,
+                  c->d_rows, c->d_res, c->d_dump, c->d_order, c->d_stage, c->d_stats};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -616,12 +731,71 @@ extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const in
   int8_t* d = nullptr;
   HIP_TRY(hipMalloc(&d, (size_t)n_codes * N));
   HIP_TRY(hipMemcpyAsync(d, h_codes, (size_t)n_codes * N, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(acq_forward_kernel, dim3(n_codes), dim3(kThreads), 0, c->stream, d, 0, 1,
-                     (const double*)nullptr, 0.0, 1, c->d_sigma, c->d_F);
-  HIP_TRY(hipGetLastError());
+  int rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F);
+  if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipFree(d));
   c->n_codes = n_codes;
+  return GNSSCORR_OK;
+}
+
+// XCD-aware workgroup order.  Workgroups are dealt round-robin over the 8
+// XCDs (blockIdx % 8 share an L2; MI355X_MICROARCH.md "Workgroup dispatch").
+// Rows are cut into tiles of 4 bins x 8 groups (= the 32 CUs of one XCD), so
+// the workgroups an XCD runs concurrently read 4 IF-spectrum rows and 8 code
+// spectra (~2 MB) from its 4 MB L2 instead of 32 distinct pairs.  Placement
+// only changes speed, never results.
+static void build_tile_order(int n_groups, int n_bins, int units_per_row, int* perm) {
+  const int R = n_groups * n_bins * units_per_row;
+  constexpr int TB = 4, TG = 8, NX = 8;
+  int* seq = (int*)malloc(sizeof(int) * R);
+  int k = 0;
+  for (int g0 = 0; g0 < n_groups; g0 += TG)
+    for (int b0 = 0; b0 < n_bins; b0 += TB)
+      for (int u = 0; u < units_per_row; u++)
+        for (int bi = b0; bi < b0 + TB && bi < n_bins; bi++)
+          for (int gi = g0; gi < g0 + TG && gi < n_groups; gi++)
+            seq[k++] = (gi * n_bins + bi) * units_per_row + u;
+  int start[NX + 1];
+  start[0] = 0;
+  for (int x = 0; x < NX; x++) start[x + 1] = start[x] + (R - x + NX - 1) / NX;
+  for (int b = 0; b < R; b++) perm[b] = seq[start[b % NX] + b / NX];
+  free(seq);
+}
+
+static int ensure_order(gnsscorr_acq_ctx* c, int n_groups, int n_bins, int units_per_row) {
+  if (c->d_order && c->order_groups == n_groups && c->order_bins == n_bins &&
+      c->order_units == units_per_row)
+    return GNSSCORR_OK;
+  const int R = n_groups * n_bins * units_per_row;
+  int* perm = (int*)malloc(sizeof(int) * R);
+  build_tile_order(n_groups, n_bins, units_per_row, perm);
+  int rc = grow((void**)&c->d_order, &c->cap_order, R, sizeof(int));
+  if (rc) { free(perm); return rc; }
+  hipError_t e = hipMemcpyAsync(c->d_order, perm, sizeof(int) * R, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  free(perm);
+  if (e != hipSuccess) {
+    gnsscorr_set_error("ensure_order: %s", hipGetErrorString(e));
+    return GNSSCORR_EDEVICE;
+  }
+  c->order_groups = n_groups;
+  c->order_bins = n_bins;
+  c->order_units = units_per_row;
+  return GNSSCORR_OK;
+}
+
+// forward transform of n_rows rows into dst (padded correlation layout)
+static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
+                          const double* d_freqs, int mode, int n_rows, float2* dst) {
+  int rc = grow((void**)&c->d_stage, &c->cap_stage, (size_t)n_rows * NPAD, sizeof(float2));
+  if (rc) return rc;
+  hipLaunchKernelGGL(acq_fwd16_kernel, dim3(n_rows * 4), dim3(kFwd1Threads), 0, c->stream, src, iq,
+                     n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, mode, c->d_stage);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(acq_fwd1023_kernel, dim3(n_rows * 16), dim3(64), 0, c->stream, c->d_stage,
+                     c->d_sigma, dst);
+  HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
 
@@ -640,9 +814,8 @@ static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n
                           int n_freqs, const double* d_freqs) {
   int rc = check_search(c, n_blocks, n_freqs, GNSSCORR_ACQ_BEST_OF_BLOCKS);
   if (rc) return rc;
-  hipLaunchKernelGGL(acq_forward_kernel, dim3(n_freqs * n_blocks), dim3(kThreads), 0, c->stream,
-                     d_if, iq, n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, 0, c->d_sigma, c->d_X);
-  HIP_TRY(hipGetLastError());
+  rc = forward_launch(c, d_if, iq, n_blocks, d_freqs, 0, n_freqs * n_blocks, c->d_X);
+  if (rc) return rc;
   c->spec_blocks = n_blocks;
   c->spec_freqs = n_freqs;
   return GNSSCORR_OK;
@@ -659,10 +832,17 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
                        "blocks %d vs spectra %d)", n_groups, n_bins, spc, n_blocks, c->spec_blocks);
     return GNSSCORR_EINVAL;
   }
-#define ACQ_CORR_LAUNCH(M, D)                                                                  \
-  hipLaunchKernelGGL((acq_corr_kernel<M, D>), dim3(n_groups * n_bins), dim3(kThreads), 0,       \
-                     c->stream, c->d_X, c->d_F, n_blocks, d_gcode, d_gfreq, n_bins, spc, d_rows, \
-                     d_dump, dump_block)
+  const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;  // work units per row
+  rc = ensure_order(c, n_groups, n_bins, upr);
+  if (rc) return rc;
+  rc = grow((void**)&c->d_stats, &c->cap_stats, (size_t)n_groups * n_bins * n_blocks,
+            sizeof(gnsscorr_acq_row));
+  if (rc) return rc;
+  const int n_units = n_groups * n_bins * upr;
+#define ACQ_CORR_LAUNCH(M, D)                                                                \
+  hipLaunchKernelGGL((acq_corr_kernel<M, D>), dim3(n_units), dim3(kThreads), 0, c->stream,    \
+                     c->d_X, c->d_F, n_blocks, d_gcode, d_gfreq, n_bins, spc, c->d_stats,      \
+                     d_dump, dump_block, c->d_order)
   if (d_dump)
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
   else if (mode == GNSSCORR_ACQ_NONCOHERENT)
@@ -671,9 +851,17 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, false);
 #undef ACQ_CORR_LAUNCH
   HIP_TRY(hipGetLastError());
-  if (d_res) {
-    hipLaunchKernelGGL(acq_select_kernel, dim3((n_groups + 63) / 64), dim3(64), 0, c->stream,
-                       d_rows, n_groups, n_bins, d_gfreq, d_freqs, d_res);
+  c->stat_groups = n_groups;
+  c->stat_bins = n_bins;
+  c->stat_blocks = n_blocks;
+  c->stat_mode = mode;
+  if (d_rows || d_res) {
+    if (!d_rows || (d_res && !d_freqs)) {
+      gnsscorr_set_error("gnsscorr_acq_correlate: d_res needs d_rows and d_freqs");
+      return GNSSCORR_EINVAL;
+    }
+    hipLaunchKernelGGL(acq_select_kernel, dim3(n_groups), dim3(64), 0, c->stream, c->d_stats,
+                       n_groups, n_bins, n_blocks, mode, d_gfreq, d_freqs, d_rows, d_res);
     HIP_TRY(hipGetLastError());
   }
   return GNSSCORR_OK;
@@ -705,7 +893,7 @@ extern "C" int gnsscorr_acq_correlate_dev(gnsscorr_acq_ctx* c, int n_blocks, int
                                           const int32_t* d_group_code,
                                           const int32_t* d_group_freq, int spc,
                                           gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res) {
-  if (!c || !d_group_code || !d_group_freq || !d_rows || (d_res && !d_freqs)) {
+  if (!c || !d_group_code || !d_group_freq || (d_res && (!d_freqs || !d_rows))) {
     gnsscorr_set_error("gnsscorr_acq_correlate_dev: null argument");
     return GNSSCORR_EINVAL;
   }
@@ -716,14 +904,18 @@ extern "C" int gnsscorr_acq_correlate_dev(gnsscorr_acq_ctx* c, int n_blocks, int
 
 extern "C" int gnsscorr_acq_select_dev(gnsscorr_acq_ctx* c, int n_groups, int n_bins,
                                        const double* d_freqs, const int32_t* d_group_freq,
-                                       const gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res) {
-  if (!c || !d_freqs || !d_group_freq || !d_rows || !d_res || n_groups < 1 || n_bins < 1) {
-    gnsscorr_set_error("gnsscorr_acq_select_dev: bad arguments");
+                                       gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res) {
+  if (!c || !d_freqs || !d_group_freq || !d_rows || n_groups != c->stat_groups ||
+      n_bins != c->stat_bins || n_groups < 1) {
+    gnsscorr_set_error("gnsscorr_acq_select_dev: bad arguments (shape must match the last "
+                       "correlate call: %d groups x %d bins)", c ? c->stat_groups : 0,
+                       c ? c->stat_bins : 0);
     return GNSSCORR_EINVAL;
   }
   HIP_TRY(hipSetDevice(c->cfg.device));
-  hipLaunchKernelGGL(acq_select_kernel, dim3((n_groups + 63) / 64), dim3(64), 0, c->stream, d_rows,
-                     n_groups, n_bins, d_group_freq, d_freqs, d_res);
+  hipLaunchKernelGGL(acq_select_kernel, dim3(n_groups), dim3(64), 0, c->stream, c->d_stats,
+                     n_groups, n_bins, c->stat_blocks, c->stat_mode, d_group_freq, d_freqs, d_rows,
+                     d_res);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }

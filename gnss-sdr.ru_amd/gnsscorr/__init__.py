@@ -391,9 +391,9 @@ class AcqCtx:
                "gnsscorr_acq_spectra_dev")
 
     def correlate_dev(self, n_blocks, d_freqs, n_groups, n_bins, d_group_code, d_group_freq,
-                      d_rows, d_res=None, spc=16, mode=ACQ_BEST_OF_BLOCKS):
+                      d_rows=None, d_res=None, spc=16, mode=ACQ_BEST_OF_BLOCKS):
         _check(lib().gnsscorr_acq_correlate_dev(self.h, n_blocks, mode, d_freqs, n_groups, n_bins,
-                                                d_group_code, d_group_freq, spc, d_rows,
+                                                d_group_code, d_group_freq, spc, d_rows or None,
                                                 d_res or None), "gnsscorr_acq_correlate_dev")
 
     def select_dev(self, n_groups, n_bins, d_freqs, d_group_freq, d_rows, d_res):

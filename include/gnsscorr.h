@@ -202,8 +202,10 @@ int gnsscorr_acq_search_dev(gnsscorr_acq_ctx *ctx, const int8_t *d_if, int iq, i
 /* The two stages of gnsscorr_acq_search_dev, for re-correlating resident
  * spectra with another code set or timing the stages separately:
  *  spectra:   wipe-off + FFT of every (freq, block), kept in the context
- *  correlate: conj-multiply + IFFT + |.|^2 + peak search of every group row
- *             (d_res may be NULL: rows only, no per-group selection). */
+ *  correlate: conj-multiply + IFFT + |.|^2 + peak search of every group row;
+ *             with d_rows the rows are combined over blocks (and with d_res
+ *             the per-group selection runs too); with both NULL the per-block
+ *             statistics stay in the context for gnsscorr_acq_select_dev(). */
 int gnsscorr_acq_spectra_dev(gnsscorr_acq_ctx *ctx, const int8_t *d_if, int iq, int n_blocks,
                              int n_freqs, const double *d_freqs);
 int gnsscorr_acq_correlate_dev(gnsscorr_acq_ctx *ctx, int n_blocks, int mode,
@@ -211,9 +213,11 @@ int gnsscorr_acq_correlate_dev(gnsscorr_acq_ctx *ctx, int n_blocks, int mode,
                                const int32_t *d_group_code, const int32_t *d_group_freq, int spc,
                                gnsscorr_acq_row *d_rows, gnsscorr_acq_result *d_res);
 
-/* Per-group selection (acquisition.sci:141-186) over rows already computed. */
+/* Block combine (acquisition.sci:126-132) + per-group selection (:141-186)
+ * over the statistics of the last correlate call; writes d_rows (and d_res
+ * when not NULL). */
 int gnsscorr_acq_select_dev(gnsscorr_acq_ctx *ctx, int n_groups, int n_bins, const double *d_freqs,
-                            const int32_t *d_group_freq, const gnsscorr_acq_row *d_rows,
+                            const int32_t *d_group_freq, gnsscorr_acq_row *d_rows,
                             gnsscorr_acq_result *d_res);
 
 /* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples floats. */
