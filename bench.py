@@ -81,7 +81,7 @@ def acq_setup(dev, rank):
     rng = np.random.default_rng(100 + rank)
     planted = rng.choice(np.arange(1, 33), 8, replace=False)
     sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
-                 doppler=float(rng.uniform(-5000, 5000)), cn0=46.0, data_bits=1) for p in planted]
+                 doppler=float(rng.uniform(-5000, 5000)), cn0=49.0, data_bits=1) for p in planted]
     IF = gc.ifgen(N_BLK * N, sigs, fs=FS, seed=0x5EED0002 + rank)
     codes = np.stack([gc.sample_code(gc.ca_code(p), 1.023e6, FS, N) for p in range(1, 33)])
     freqs = 2.42e6 - 10000.0 + 500.0 * np.arange(N_BINS)           # acquisition.sci:101-104
@@ -198,11 +198,18 @@ def cpu_baseline_track(budget_s=8.0):
     n_inst, if_calls = threads, 32
     IF = np.random.default_rng(1).choice(np.array([-3, -1, 1, 3], np.int8),
                                          size=n_inst * if_calls * TRACK_NS * 2)
-    calls, t0 = 50, time.perf_counter()
-    o.L.osgo_bench(n_inst, TRACK_CH, IF.ctypes.data, TRACK_NS, calls, if_calls, 31750430,
-                   6710886, threads)
-    probe = time.perf_counter() - t0
-    calls = max(50, int(calls * budget_s / max(probe, 1e-3)))
+    # size the sample: grow the call count until a run takes >= budget/4, then
+    # scale to the budget (the first calls also pay thread start + page faults)
+    calls = 50
+    while True:
+        t0 = time.perf_counter()
+        o.L.osgo_bench(n_inst, TRACK_CH, IF.ctypes.data, TRACK_NS, calls, if_calls, 31750430,
+                       6710886, threads)
+        probe = time.perf_counter() - t0
+        if probe >= budget_s / 4 or calls >= 1 << 20:
+            break
+        calls *= 4
+    calls = max(calls, int(calls * budget_s / max(probe, 1e-3)))
     t0 = time.perf_counter()
     work = o.L.osgo_bench(n_inst, TRACK_CH, IF.ctypes.data, TRACK_NS, calls, if_calls, 31750430,
                           6710886, threads)

@@ -148,6 +148,11 @@ __device__ __forceinline__ void corr_sample(int I, int Q, uint32_t& phase, uint3
   }
 }
 
+__device__ __forceinline__ int xcd_channel(int b, int G) {
+  const int q = G >> 3, r = G & 7, x = b & 7, slot = b >> 3;
+  return x * q + (x < r ? x : r) + slot;
+}
+
 template <bool IQ>
 __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
     const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp,
@@ -155,7 +160,11 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
     gnsscorr_track_result* __restrict__ res, int32_t* __restrict__ all_dumps, int max_dumps,
     const uint32_t* __restrict__ pk, int64_t tic_count) {
   __shared__ int32_t s_sum[kMaxEpochs][6];
-  const int chn = blockIdx.x;
+  // XCD-aware order: workgroup b runs on XCD b % 8, so give every XCD a
+  // contiguous channel range -- the channels of one receiver (consecutive
+  // channels sharing an IF stream) then hit the same 4 MiB L2 and the stream
+  // is fetched from HBM once instead of once per XCD.
+  const int chn = xcd_channel(blockIdx.x, gridDim.x);
   const gnsscorr_nco_cmd cmd = cmds[chn];
   gnsscorr_chan_state st = state[chn];
   if (cmd.epoch_load >= 0) {  // epoch set, correlator.c:177-182

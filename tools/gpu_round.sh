@@ -1,0 +1,29 @@
+# One GPU session: parity tests, bench, kernel-trace stats, PMC passes.
+# usage (via gpurun): bash tools/gpu_round.sh <tag>
+# Every GPU step has its own time limit; the first failure ends the script.
+set -eu
+TAG=${1:-r1}
+O=gpurun_out/$TAG
+mkdir -p $O/pmc
+export TMPDIR=/tmp
+echo "== pytest -m gpu"
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1
+tail -3 $O/pytest.log
+echo "== bench"
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
+cat $O/bench.json
+echo "== rocprofv3 kernel-trace stats"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+  python3 bench.py --no-cpu-baseline > $O/prof.log 2>&1
+echo "== pmc"
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+i=0
+for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
+         "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" \
+         "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc/p$i -o run -- $B > $O/pmc/p$i.log 2>&1
+  echo "pmc pass $i ok"
+done
+python tools/pmc_summary.py $O/pmc $O/pmc_summary.json
+echo "== done"
