@@ -43,6 +43,9 @@ PEAK_FP32_TFLOPS = 157.3                       # MI355X_MICROARCH.md (vector == 
 PEAK_HBM_GBS = 8000.0
 PEAK_INT_TOPS = 78.6                           # 256 CU x 128 lanes x 2.4 GHz, 32-bit VALU
 TRACK_RX, TRACK_CH, TRACK_NS = 256, 12, 16368
+SGT_RX, SGT_FS = 256, 16.0e6                   # GLONASS records: initSettings.sci fs = 16 MHz
+SGT_DP_PER_SAMPLE = 27                         # fp64 ops/sample of sgt_track_kernel
+PEAK_FP64_TFLOPS = 78.6                        # MI355X FP64 vector (AMD spec; not in the guide)
 TRACK_OPS_PER_SAMPLE = 20                      # SURVEY 8d integer-op model
 METRIC = "1ms E/P/L correlations/sec + acquisition cells/sec @16.368Msps; 1/2/4/8 GPU"
 
@@ -170,6 +173,70 @@ def run_track(dist, dev, steps, warmup):
     return dict(dt=dt, kern_ms=kern_ms, channels=C, dumps_ok=dumps_ok)
 
 
+def run_sgt(dist, dev, steps, warmup):
+    """BASELINE config 4: GLONASS L1OF 14 FDMA channels, tracking.sci float loop on the GPU.
+    Throughput: SGT_RX records x 14 FCH; latency: one 14-channel receiver."""
+    K = steps + warmup + 2
+    ns = int(SGT_FS * K / 1000)
+    stride = 2 * ns
+    d_if = gc.DevBuf(SGT_RX * stride, dev)
+    d_if.fill_if2(0x5EED0004 + dist.rank)
+    ctx = gc.SgtCtx(1, device=dev, samplingFreq=SGT_FS)
+    rng = np.random.default_rng(44 + dist.rank)
+    fch = np.tile(np.arange(-7, 7), SGT_RX)
+    C = len(fch)
+    ch = ctx.init_chans(fch, rng.integers(1, 16000, C), 1e6 + 0.5625e6 * fch +
+                        rng.uniform(-3000, 3000, C), streams=np.repeat(np.arange(SGT_RX), 14))
+    d_ch = gc.DevBuf.from_array(ch, dev)
+    d_ep = gc.DevBuf(C * max(steps, warmup) * gc.SGT_EPOCH.itemsize, dev)
+    ctx.track_dev(d_if.ptr, stride, ns, C, d_ch.ptr, warmup, d_ep.ptr)
+    ctx.sync()
+    e0, e1 = gc.Event(dev), gc.Event(dev)
+    dist.barrier()
+    gc.dev_synchronize(dev)
+    t0 = time.perf_counter()
+    e0.record(ctx.stream)
+    ctx.track_dev(d_if.ptr, stride, ns, C, d_ch.ptr, steps, d_ep.ptr)
+    e1.record(ctx.stream)
+    ctx.sync()
+    t1 = time.perf_counter()
+    dist.barrier()
+    dt = dist.max(t1 - t0)
+    kern_ms = dist.max(e0.elapsed_ms(e1))
+    ep = d_ep.download(gc.SGT_EPOCH, C * steps).reshape(C, steps)
+    ok = bool((ep["status"] == 0).all() and (np.abs(ep["blksize"] - 16000) < 20).all())
+    # config 4 as stated: one 14-channel receiver, epochs back to back
+    ch14 = ctx.init_chans(np.arange(-7, 7), rng.integers(1, 16000, 14),
+                          1e6 + 0.5625e6 * np.arange(-7, 7))
+    d14 = gc.DevBuf.from_array(ch14, dev)
+    ctx.track_dev(d_if.ptr, stride, ns, 14, d14.ptr, warmup, d_ep.ptr)
+    d14.upload(ch14)
+    ctx.sync()
+    e0.record(ctx.stream)
+    ctx.track_dev(d_if.ptr, stride, ns, 14, d14.ptr, steps, d_ep.ptr)
+    e1.record(ctx.stream)
+    ctx.sync()
+    lat_ms = e0.elapsed_ms(e1) / steps
+    return dict(dt=dt, kern_ms=kern_ms, channels=C, steps=steps, ok=ok, lat_ms=lat_ms)
+
+
+def cpu_baseline_sgt(budget_s=6.0):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sgt_oracle
+    s = sgt_oracle.settings(1, samplingFreq=SGT_FS)
+    n_ms = 40
+    IF = np.random.default_rng(3).choice(np.array([-3, -1, 1, 3], np.int8),
+                                         size=2 * int(SGT_FS * (n_ms + 2) / 1000))
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        for k in range(-7, 7):
+            n += len(sgt_oracle.track(IF, s, k, 100, 1e6 + 0.5625e6 * k, n_ms)["I_P"])
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="channel-ms/s", cores=1, kind="port",
+                sample=f"{n} channel-epochs of the fp64 numpy tracking.sci restatement "
+                       f"(oracle/sgt_oracle.py, 14 FCH x {n_ms} ms), {dt:.1f} s")
+
+
 def cpu_baseline_acq(meta, budget_s=12.0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import acq_oracle
@@ -244,6 +311,7 @@ def main():
 
     acq = run_acq(dist, dev, a.steps, a.warmup)
     trk = None if a.skip_track else run_track(dist, dev, max(a.steps, 20), a.warmup)
+    sgt = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup)
 
     if dist.rank == 0:
         W = dist.world
@@ -293,12 +361,37 @@ def main():
                              "kernel_ms_per_launch": trk["kern_ms"]},
                 "dumps_sane": trk["dumps_ok"],
             }
+        if sgt:
+            C = sgt["channels"]
+            k_s = sgt["kern_ms"] * 1e-3
+            dp = C * sgt["steps"] * SGT_FS / 1000 * SGT_DP_PER_SAMPLE
+            out["glonass_tracking"] = {
+                "metric": "1ms E/P/L correlations/sec (GLONASS L1OF float loop, tracking.sci)",
+                "value": C * sgt["steps"] * W / sgt["dt"], "unit": "channel-ms/s",
+                "steps": sgt["steps"], "channels_per_gpu": C,
+                "config": f"BASELINE config 4 scaled out: {SGT_RX} records x 14 FCH, 511-chip ST, "
+                          f"{SGT_FS / 1e6:g} Msps int8 IQ, fp64 NCOs + FLL/PLL/DLL on the GPU",
+                "config4_ms_per_epoch_14ch": sgt["lat_ms"],
+                "config4_realtime_factor": 1.0 / sgt["lat_ms"],
+                "realtime_channels_per_gpu": C * sgt["steps"] / sgt["kern_ms"],
+                "roofline": {"bound": "valu", "kernel": "sgt_track_kernel",
+                             "achieved": dp / k_s / 1e12, "peak": PEAK_FP64_TFLOPS,
+                             "unit": f"TFLOP/s (fp64, {SGT_DP_PER_SAMPLE} ops/sample model)",
+                             "frac": dp / k_s / 1e12 / PEAK_FP64_TFLOPS,
+                             "hbm_algorithmic_GBs": C * sgt["steps"] * SGT_FS / 1000 * 2 / 14
+                             / k_s / 1e9,
+                             "traffic": pmc_traffic("sgt_track_kernel"),
+                             "kernel_ms_per_launch": sgt["kern_ms"]},
+                "epochs_sane": sgt["ok"],
+            }
         if W == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_acq(acq["meta"])
             if trk:
                 tb = cpu_baseline_track()
                 if tb:
                     out["tracking"]["cpu_baseline"] = tb
+            if sgt:
+                out["glonass_tracking"]["cpu_baseline"] = cpu_baseline_sgt()
         print(json.dumps(out))
     dist.close()
 

@@ -1,0 +1,429 @@
+// sgt.hip -- SoftGNSS float tracking loop ("sgt") on gfx950.
+//
+// The Scilab receivers track one channel at a time over a recorded file
+// (GLONASS/L1/tracking.sci:150-400, GPS/L1/tracking.sci:124-360).  Here the
+// whole record lives in HBM and one workgroup runs one channel's loop for
+// many epochs without leaving the GPU:
+//
+//  epoch (uniform scalars, every thread computes the same fp64 values):
+//    step    = codeFreq / fs                             tracking.sci:248
+//    blksize = ceil((L - remCode) / step)                tracking.sci:250
+//  samples (k = tid + j*T, coalesced int8 I,Q loads):
+//    code index  ceil((remCode -/+ spc) + k*step)  -> padded [c(end) c c(1)]
+//                (:282-299, fp64 with contraction off: bit-exact indices)
+//    carrier     exp(i*((2*pi*f)*(k/fs) + remCarr)): one fp64 sincos per
+//                thread, then an fp64 rotation per T samples (:305-313)
+//    sums        I = code*imag(carr*raw), Q = code*real(carr*raw) (:316-326),
+//                code +-1 applied as an fp64 sign flip (table of sign masks)
+//  reduction: wavefront xor-shuffles, per-wave partials in LDS (double
+//    buffered by epoch parity -> one barrier per epoch), every thread adds the
+//    wave partials in the same order and runs the loop filters itself, so the
+//    state stays uniform without a broadcast.
+//  loop (closed_loop=1): FLL-assisted PLL + DLL, tracking.sci:329-375.
+//
+// Roofline: fp64 VALU (~27 DP ops per sample); HBM is 2 B/sample.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "gnsscorr_internal.h"
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      gnsscorr_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                         __LINE__);                                                     \
+      return GNSSCORR_EDEVICE;                                                          \
+    }                                                                                   \
+  } while (0)
+
+namespace {
+
+constexpr int kMaxCode = 1023;
+constexpr int kPadLen = kMaxCode + 2;
+constexpr int kMaxWaves = 16;
+
+struct SgtParams {
+  int system, file_type, switch_iq, code_length;
+  double fs, code_basis, if_freq, l1_if_step, glo_zero, spc;
+  double tau1, tau2, k1, k2, k3, pdi_code;
+};
+
+__device__ __forceinline__ int xcd_channel(int b, int G) {
+  const int q = G >> 3, r = G & 7, x = b & 7, slot = b >> 3;
+  return x * q + (x < r ? x : r) + slot;
+}
+
+__device__ __forceinline__ double flip(double v, uint32_t signmask) {
+  // multiply by +-1 exactly: xor the sign bit of the high dword
+  int2 b = *reinterpret_cast<int2*>(&v);
+  b.y ^= (int)signmask;
+  return *reinterpret_cast<double*>(&b);
+}
+
+// indices are in [0, L+1] for every state the loop produces (remCode in
+// [0, step)); the clamp only keeps a corrupted state inside the LDS table
+__device__ __forceinline__ int clampi(int i, int hi) { return i < 0 ? 0 : (i > hi ? hi : i); }
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int FT, bool CLOSED>
+__global__ __launch_bounds__(1024) void sgt_track_kernel(
+    SgtParams p, const int8_t* __restrict__ ifbuf, int64_t stride, int64_t n_samples,
+    const uint32_t* __restrict__ codes, gnsscorr_sgt_chan* __restrict__ chans, int n_epochs,
+    gnsscorr_sgt_epoch* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ uint32_t s_code[kPadLen];
+  __shared__ double s_part[2][kMaxWaves][6];
+  const int ch = xcd_channel(blockIdx.x, gridDim.x);
+  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nw = T >> 6;
+  gnsscorr_sgt_chan c = chans[ch];
+  const int L = p.code_length;
+  const int row = p.system == 1 ? 0 : c.code_id;
+  for (int i = tid; i < L + 2; i += T) s_code[i] = codes[row * kPadLen + i];
+  __syncthreads();
+
+  const int8_t* base = ifbuf + (int64_t)c.stream * stride;
+  const double twopi = 2.0 * M_PI;
+  const double dL = (double)L;
+  int e = 0;
+  for (; e < n_epochs; e++) {
+    gnsscorr_sgt_epoch* rec = out + (int64_t)ch * n_epochs + e;
+    if (c.status != 0) {
+      if (tid == 0) { gnsscorr_sgt_epoch z = {}; z.status = 1; *rec = z; }
+      continue;
+    }
+    const double step = c.code_freq / p.fs;
+    const double blk_d = ceil((dL - c.rem_code) / step);
+    const int64_t blk = (int64_t)blk_d;
+    if (c.pos + blk > n_samples) {  // tracking.sci:273-277: not enough samples
+      c.status = 1;
+      if (tid == 0) { gnsscorr_sgt_epoch z = {}; z.status = 1; z.blksize = (int32_t)blk; *rec = z; }
+      continue;
+    }
+    const double aE = c.rem_code - p.spc, aL = c.rem_code + p.spc, aP = c.rem_code;
+    const double A = (c.carr_freq * 2.0) * M_PI;        // (carrFreq * 2.0 * %pi)
+    // carrier at the thread's first sample, rotation by T samples
+    // (sin/cos rather than sincos: its pointer outputs get promoted to 32 KB of LDS)
+    const double th0 = A * ((double)tid / p.fs) + c.rem_carr, thw = A * ((double)T / p.fs);
+    double sn = sin(th0), cs = cos(th0);
+    const double sw = sin(thw), cw = cos(thw);
+    double ie = 0, ip = 0, il = 0, qe = 0, qp = 0, ql = 0;
+    const int8_t* src = base + (FT == 2 ? 2 : 1) * c.pos;
+    for (int64_t k = tid; k < blk; k += T) {
+      const double t = (double)k * step;
+      const uint32_t mE = s_code[clampi((int)ceil(aE + t), L + 1)];
+      const uint32_t mP = s_code[clampi((int)ceil(aP + t), L + 1)];
+      const uint32_t mL = s_code[clampi((int)ceil(aL + t), L + 1)];
+      double re, im;
+      if (FT == 2) {
+        const char2 v = *reinterpret_cast<const char2*>(src + 2 * k);
+        re = (double)v.x;
+        im = (double)v.y;
+        if (p.switch_iq) { const double tmp = re; re = im; im = tmp; }
+      } else {
+        re = (double)src[k];
+        im = 0.0;
+      }
+      const double qb = cs * re - sn * im;   // real(carrsig .* rawSignal)
+      const double ib = cs * im + sn * re;   // imag(carrsig .* rawSignal)
+      ie += flip(ib, mE); ip += flip(ib, mP); il += flip(ib, mL);
+      qe += flip(qb, mE); qp += flip(qb, mP); ql += flip(qb, mL);
+      const double c2 = cs * cw - sn * sw;
+      sn = sn * cw + cs * sw;
+      cs = c2;
+    }
+    ie = wave_sum(ie); ip = wave_sum(ip); il = wave_sum(il);
+    qe = wave_sum(qe); qp = wave_sum(qp); ql = wave_sum(ql);
+    const int par = e & 1;
+    if (lane == 0) {
+      s_part[par][wave][0] = ie; s_part[par][wave][1] = ip; s_part[par][wave][2] = il;
+      s_part[par][wave][3] = qe; s_part[par][wave][4] = qp; s_part[par][wave][5] = ql;
+    }
+    __syncthreads();
+    double S[6] = {0, 0, 0, 0, 0, 0};
+    for (int w = 0; w < nw; w++)
+#pragma unroll
+      for (int j = 0; j < 6; j++) S[j] += s_part[par][w][j];
+    const double I_E = S[0], I_P = S[1], I_L = S[2], Q_E = S[3], Q_P = S[4], Q_L = S[5];
+
+    // carry-over (tracking.sci:301-313)
+    const double tlast = aP + (double)(blk - 1) * step;   // tcode(blksize) of the prompt range
+    c.rem_code = (tlast + step) - dL;
+    const double last = A * ((double)blk / p.fs) + c.rem_carr;
+    c.rem_carr = last - trunc(last / twopi) * twopi;
+    c.pos += blk;
+    double code_err = 0, carr_err = 0;
+    if (CLOSED) {
+      // FLL-assisted PLL (tracking.sci:329-353)
+      const double I2 = c.i1, Q2 = c.q1;
+      c.i1 = I_P; c.q1 = Q_P;
+      const double cross = c.i1 * Q2 - I2 * c.q1;
+      const double dot = fabs(c.i1 * I2 + c.q1 * Q2);
+      const double freq_err = atan2(cross, dot) / M_PI;
+      carr_err = atan(Q_P / I_P) / (2.0 * M_PI);
+      const double carr_nco = c.old_carr_nco + p.k1 * carr_err - p.k2 * c.old_carr_error -
+                              p.k3 * freq_err;
+      c.old_carr_nco = carr_nco;
+      c.old_carr_error = carr_err;
+      c.carr_freq = c.carr_freq_basis + carr_nco;
+      // DLL (tracking.sci:355-374)
+      const double aEm = sqrt(I_E * I_E + Q_E * Q_E), aLm = sqrt(I_L * I_L + Q_L * Q_L);
+      code_err = (aEm - aLm) / (aEm + aLm);
+      const double code_nco = c.old_code_nco + (p.tau2 / p.tau1) * (code_err - c.old_code_error) +
+                              code_err * (p.pdi_code / p.tau1);
+      c.old_code_nco = code_nco;
+      c.old_code_error = code_err;
+      if (p.system == 1) {
+        const double fch = (double)c.code_id;
+        c.code_freq = p.code_basis - code_nco +
+                      (c.carr_freq - (p.if_freq + p.l1_if_step * fch)) /
+                          ((p.glo_zero + fch * p.l1_if_step) / p.code_basis);
+      } else {
+        c.code_freq = p.code_basis - code_nco + ((c.carr_freq - p.if_freq) / 1540);
+      }
+    }
+    c.n_epochs++;
+    if (tid == 0) {
+      gnsscorr_sgt_epoch r;
+      r.i_e = I_E; r.i_p = I_P; r.i_l = I_L; r.q_e = Q_E; r.q_p = Q_P; r.q_l = Q_L;
+      r.carr_freq = c.carr_freq;
+      r.code_freq = c.code_freq;
+      r.absolute_sample = (double)c.pos - c.rem_code * (p.fs / 1000) / dL;
+      r.dll_discr = code_err;
+      r.dll_discr_filt = c.old_code_nco;
+      r.pll_discr = carr_err;
+      r.pll_discr_filt = c.old_carr_nco;
+      r.blksize = (int32_t)blk;
+      r.status = 0;
+      *rec = r;
+    }
+  }
+  if (tid == 0) chans[ch] = c;
+}
+
+}  // namespace
+
+// ============================================================================
+// host side
+// ============================================================================
+struct gnsscorr_sgt_ctx {
+  gnsscorr_sgt_cfg cfg;
+  SgtParams p;
+  hipStream_t stream = nullptr;
+  uint32_t* d_codes = nullptr;
+  gnsscorr_sgt_chan* d_chan = nullptr;
+  gnsscorr_sgt_epoch* d_ep = nullptr;
+  size_t chan_cap = 0, ep_cap = 0;
+};
+
+extern "C" void gnsscorr_sgt_loop_coefs(const gnsscorr_sgt_cfg* cfg, double* tau1, double* tau2,
+                                        double* k1, double* k2, double* k3) {
+  // calcLoopCoef.sci:39-43 (k = 1.0)
+  const double z = cfg->dll_damping;
+  const double wn = cfg->dll_noise_bw * 8 * z / (4 * (z * z) + 1);
+  *tau1 = 1.0 / (wn * wn);
+  *tau2 = 2.0 * z / wn;
+  // calcFLLPLLLoopCoef.sci:36-38 (T = PDIcarr = 0.001)
+  const double T = 0.001, b = cfg->pll_noise_bw / 0.53;
+  *k1 = T * (b * b) + 1.414 * b;
+  *k2 = 1.414 * b;
+  *k3 = T * (cfg->fll_noise_bw / 0.25);
+}
+
+static int check_cfg(const gnsscorr_sgt_cfg* cfg) {
+  if (!cfg || (cfg->system != 0 && cfg->system != 1) ||
+      (cfg->file_type != 1 && cfg->file_type != 2) || cfg->samp_rate <= 0 ||
+      cfg->code_freq_basis <= 0 || cfg->dll_spacing < 0 || cfg->dll_spacing >= 1 ||
+      cfg->code_length != (cfg->system == 1 ? 511 : 1023)) {
+    gnsscorr_set_error("sgt: bad config (system 0/1, file_type 1/2, code_length 1023/511, "
+                       "0<=dll_spacing<1)");
+    return GNSSCORR_EINVAL;
+  }
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sgt_init_chan(const gnsscorr_sgt_cfg* cfg, int code_id, int stream,
+                                      int64_t skip, int64_t code_phase_1b, double acq_freq,
+                                      gnsscorr_sgt_chan* o) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!o || code_phase_1b < 1 || stream < 0 || skip < 0 ||
+      (cfg->system == 0 && (code_id < 1 || code_id > 32)) ||
+      (cfg->system == 1 && (code_id < -7 || code_id > 6))) {
+    gnsscorr_set_error("gnsscorr_sgt_init_chan: bad channel (PRN 1..32 / FCH -7..6, "
+                       "code_phase >= 1)");
+    return GNSSCORR_EINVAL;
+  }
+  memset(o, 0, sizeof *o);
+  o->code_id = code_id;
+  o->stream = stream;
+  o->pos = skip + code_phase_1b - 1;   // mseek, tracking.sci:163-168
+  o->code_freq = cfg->code_freq_basis;
+  o->carr_freq = o->carr_freq_basis = acq_freq;
+  o->i1 = o->q1 = 0.001;               // tracking.sci:201
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sgt_destroy(gnsscorr_sgt_ctx* c) {
+  if (!c) return GNSSCORR_OK;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_codes);
+  (void)hipFree(c->d_chan);
+  (void)hipFree(c->d_ep);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sgt_create(gnsscorr_sgt_ctx** out, const gnsscorr_sgt_cfg* cfg) {
+  if (!out) return GNSSCORR_EINVAL;
+  *out = nullptr;
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    gnsscorr_set_error("gnsscorr_sgt_create: no HIP device");
+    return GNSSCORR_ENODEV;
+  }
+  if (cfg->device < 0 || cfg->device >= ndev) {
+    gnsscorr_set_error("gnsscorr_sgt_create: device %d out of range", cfg->device);
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(cfg->device));
+  auto* c = new gnsscorr_sgt_ctx();
+  c->cfg = *cfg;
+  SgtParams& p = c->p;
+  p.system = cfg->system;
+  p.file_type = cfg->file_type;
+  p.switch_iq = cfg->system == 1 ? cfg->switch_iq : 0;
+  p.code_length = cfg->code_length;
+  p.fs = cfg->samp_rate;
+  p.code_basis = cfg->code_freq_basis;
+  p.if_freq = cfg->if_freq;
+  p.l1_if_step = cfg->l1_if_step;
+  p.glo_zero = cfg->glonass_zero_channel;
+  p.spc = cfg->dll_spacing;
+  p.pdi_code = 0.001;
+  gnsscorr_sgt_loop_coefs(cfg, &p.tau1, &p.tau2, &p.k1, &p.k2, &p.k3);
+  // padded code rows [c(end) c c(1)] as fp64 sign masks (tracking.sci:171-174)
+  const int rows = cfg->system == 1 ? 1 : 33;
+  uint32_t* h = (uint32_t*)calloc((size_t)rows * kPadLen, sizeof(uint32_t));
+  int8_t chips[kMaxCode];
+  const int L = cfg->code_length;
+  for (int r = 0; r < rows; r++) {
+    if (cfg->system == 1) gnsscorr_st_code(chips);
+    else if (r == 0) continue;
+    else gnsscorr_ca_code(r, chips);
+    uint32_t* row = h + (size_t)r * kPadLen;
+    auto m = [](int8_t v) { return v < 0 ? 0x80000000u : 0u; };
+    row[0] = m(chips[L - 1]);
+    for (int i = 0; i < L; i++) row[1 + i] = m(chips[i]);
+    row[L + 1] = m(chips[0]);
+  }
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->d_codes, sizeof(uint32_t) * rows * kPadLen);
+  if (e == hipSuccess)
+    e = hipMemcpy(c->d_codes, h, sizeof(uint32_t) * rows * kPadLen, hipMemcpyHostToDevice);
+  free(h);
+  if (e != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_sgt_create: %s", hipGetErrorString(e));
+    gnsscorr_sgt_destroy(c);
+    return GNSSCORR_EDEVICE;
+  }
+  *out = c;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx* c, const int8_t* d_if, int64_t stride,
+                                      int64_t n_samples, int n_ch, gnsscorr_sgt_chan* d_chan,
+                                      int n_epochs, int closed_loop, gnsscorr_sgt_epoch* d_ep) {
+  if (!c || !d_if || !d_chan || !d_ep || n_ch < 1 || n_epochs < 1 || n_samples < 0 ||
+      stride < 0) {
+    gnsscorr_set_error("gnsscorr_sgt_track_dev: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  if (c->cfg.file_type == 2 && ((uintptr_t)d_if & 1)) {
+    gnsscorr_set_error("gnsscorr_sgt_track_dev: IQ record must be 2-byte aligned");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  // small channel counts: wide workgroups (latency); many channels: 256 threads
+  const int T = n_ch >= 512 ? 256 : (n_ch >= 128 ? 512 : 1024);
+  dim3 grid(n_ch), block(T);
+  if (c->cfg.file_type == 2) {
+    if (closed_loop)
+      hipLaunchKernelGGL((sgt_track_kernel<2, true>), grid, block, 0, c->stream, c->p, d_if,
+                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
+    else
+      hipLaunchKernelGGL((sgt_track_kernel<2, false>), grid, block, 0, c->stream, c->p, d_if,
+                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
+  } else {
+    if (closed_loop)
+      hipLaunchKernelGGL((sgt_track_kernel<1, true>), grid, block, 0, c->stream, c->p, d_if,
+                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
+    else
+      hipLaunchKernelGGL((sgt_track_kernel<1, false>), grid, block, 0, c->stream, c->p, d_if,
+                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
+  }
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sgt_track(gnsscorr_sgt_ctx* c, const int8_t* d_if, int64_t stride,
+                                  int64_t n_samples, int n_ch, gnsscorr_sgt_chan* h_chan,
+                                  int n_epochs, int closed_loop, gnsscorr_sgt_epoch* h_ep) {
+  if (!c || !h_chan || !h_ep || n_ch < 1 || n_epochs < 1) {
+    gnsscorr_set_error("gnsscorr_sgt_track: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  for (int i = 0; i < n_ch; i++) {
+    const int id = h_chan[i].code_id;
+    if (c->cfg.system == 0 ? (id < 1 || id > 32) : (id < -7 || id > 6)) {
+      gnsscorr_set_error("gnsscorr_sgt_track: channel %d: bad PRN/FCH %d", i, id);
+      return GNSSCORR_EINVAL;
+    }
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  const size_t nc = (size_t)n_ch, ne = nc * (size_t)n_epochs;
+  if (nc > c->chan_cap) {
+    (void)hipFree(c->d_chan);
+    c->d_chan = nullptr;
+    HIP_TRY(hipMalloc(&c->d_chan, nc * sizeof(gnsscorr_sgt_chan)));
+    c->chan_cap = nc;
+  }
+  if (ne > c->ep_cap) {
+    (void)hipFree(c->d_ep);
+    c->d_ep = nullptr;
+    HIP_TRY(hipMalloc(&c->d_ep, ne * sizeof(gnsscorr_sgt_epoch)));
+    c->ep_cap = ne;
+  }
+  HIP_TRY(hipMemcpyAsync(c->d_chan, h_chan, nc * sizeof(gnsscorr_sgt_chan),
+                         hipMemcpyHostToDevice, c->stream));
+  int rc = gnsscorr_sgt_track_dev(c, d_if, stride, n_samples, n_ch, c->d_chan, n_epochs,
+                                  closed_loop, c->d_ep);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(h_chan, c->d_chan, nc * sizeof(gnsscorr_sgt_chan),
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(h_ep, c->d_ep, ne * sizeof(gnsscorr_sgt_epoch), hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sgt_sync(gnsscorr_sgt_ctx* c) {
+  if (!c) return GNSSCORR_EINVAL;
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" void* gnsscorr_sgt_stream(gnsscorr_sgt_ctx* c) { return c ? (void*)c->stream : nullptr; }

@@ -41,6 +41,19 @@ SIG = np.dtype([("system", "<i4"), ("prn", "<i4"), ("fch", "<i4"), ("data_bits",
 assert NCO_CMD.itemsize == 24 and CHAN_STATE.itemsize == 56 and TRACK_RESULT.itemsize == 64
 assert ACQ_ROW.itemsize == 16 and ACQ_RESULT.itemsize == 32 and SIG.itemsize == 48
 
+SGT_CHAN = np.dtype([("code_id", "<i4"), ("stream", "<i4"), ("status", "<i4"),
+                     ("n_epochs", "<i4"), ("pos", "<i8"), ("pad", "<i8"),
+                     ("rem_code", "<f8"), ("rem_carr", "<f8"), ("code_freq", "<f8"),
+                     ("carr_freq", "<f8"), ("carr_freq_basis", "<f8"), ("old_code_nco", "<f8"),
+                     ("old_code_error", "<f8"), ("old_carr_nco", "<f8"),
+                     ("old_carr_error", "<f8"), ("i1", "<f8"), ("q1", "<f8"), ("pad2", "<f8")])
+SGT_EPOCH = np.dtype([("I_E", "<f8"), ("I_P", "<f8"), ("I_L", "<f8"), ("Q_E", "<f8"),
+                      ("Q_P", "<f8"), ("Q_L", "<f8"), ("carrFreq", "<f8"), ("codeFreq", "<f8"),
+                      ("absoluteSample", "<f8"), ("dllDiscr", "<f8"), ("dllDiscrFilt", "<f8"),
+                      ("pllDiscr", "<f8"), ("pllDiscrFilt", "<f8"), ("blksize", "<i4"),
+                      ("status", "<i4")])
+assert SGT_CHAN.itemsize == 128 and SGT_EPOCH.itemsize == 112
+
 ACQ_BEST_OF_BLOCKS = 0
 ACQ_NONCOHERENT = 1
 
@@ -55,6 +68,16 @@ class AcqCfg(C.Structure):
                 ("max_freqs", C.c_int), ("max_blocks", C.c_int), ("max_codes", C.c_int)]
 
 
+class SgtCfg(C.Structure):
+    _fields_ = [("system", C.c_int32), ("file_type", C.c_int32), ("switch_iq", C.c_int32),
+                ("code_length", C.c_int32), ("device", C.c_int32), ("max_channels", C.c_int32),
+                ("samp_rate", C.c_double), ("code_freq_basis", C.c_double),
+                ("if_freq", C.c_double), ("l1_if_step", C.c_double),
+                ("glonass_zero_channel", C.c_double), ("dll_spacing", C.c_double),
+                ("dll_noise_bw", C.c_double), ("dll_damping", C.c_double),
+                ("pll_noise_bw", C.c_double), ("fll_noise_bw", C.c_double)]
+
+
 # every symbol include/gnsscorr.h + include/gnsscorr_osg.h declare
 EXPORTED_FUNCTIONS = [
     "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
@@ -66,6 +89,9 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
     "gnsscorr_acq_spectra_dev", "gnsscorr_acq_correlate_dev", "gnsscorr_acq_select_dev",
     "gnsscorr_acq_sync", "gnsscorr_acq_stream",
+    "gnsscorr_sgt_loop_coefs", "gnsscorr_sgt_init_chan", "gnsscorr_sgt_create",
+    "gnsscorr_sgt_destroy", "gnsscorr_sgt_track_dev", "gnsscorr_sgt_track", "gnsscorr_sgt_sync",
+    "gnsscorr_sgt_stream",
     "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
     "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
     "gnsscorr_event_elapsed_ms", "gnsscorr_event_destroy", "gnsscorr_dev_fill_if2",
@@ -118,6 +144,14 @@ def lib() -> C.CDLL:
         "gnsscorr_acq_select_dev": (I, [P, I, I, P, P, P, P]),
         "gnsscorr_acq_sync": (I, [P]),
         "gnsscorr_acq_stream": (P, [P]),
+        "gnsscorr_sgt_loop_coefs": (None, [C.POINTER(SgtCfg)] + [C.POINTER(D)] * 5),
+        "gnsscorr_sgt_init_chan": (I, [C.POINTER(SgtCfg), I, I, I64, I64, D, P]),
+        "gnsscorr_sgt_create": (I, [C.POINTER(P), C.POINTER(SgtCfg)]),
+        "gnsscorr_sgt_destroy": (I, [P]),
+        "gnsscorr_sgt_track_dev": (I, [P, P, I64, I64, I, P, I, I, P]),
+        "gnsscorr_sgt_track": (I, [P, P, I64, I64, I, P, I, I, P]),
+        "gnsscorr_sgt_sync": (I, [P]),
+        "gnsscorr_sgt_stream": (P, [P]),
         "gnsscorr_dev_alloc": (I, [I, C.c_size_t, C.POINTER(P)]),
         "gnsscorr_dev_free": (I, [I, P]),
         "gnsscorr_memcpy_htod": (I, [I, P, P, C.c_size_t]),
@@ -413,6 +447,83 @@ class AcqCtx:
     @property
     def stream(self) -> int:
         return lib().gnsscorr_acq_stream(self.h)
+
+
+# ---------------------------------------------------------------- SoftGNSS float tracking
+def sgt_cfg(system: int, device: int = 0, **kw) -> SgtCfg:
+    """initSettings.sci defaults (GLONASS/L1:41-107, GPS/L1:41-95); keyword overrides
+    use the Scilab names (samplingFreq, IF, dllCorrelatorSpacing, fileType, ...)."""
+    glo = system == 1
+    d = dict(samplingFreq=16e6, codeFreqBasis=0.511e6 if glo else 1.023e6,
+             codeLength=511 if glo else 1023, IF=1e6 if glo else 2.42e6,
+             L1_IF_step=0.5625e6 if glo else 0.0, GLONASS_zero_channel=1602e6 if glo else 0.0,
+             dllCorrelatorSpacing=0.05 if glo else 0.2, dllNoiseBandwidth=0.5 if glo else 0.1,
+             dllDampingRatio=0.7, pllNoiseBandwidth=25.0, fllNoiseBandwidth=250.0, fileType=2,
+             switchIQ=0)
+    unknown = set(kw) - set(d) - {"system"}
+    if unknown:
+        raise ValueError(f"unknown settings {sorted(unknown)}")
+    d.update(kw)
+    return SgtCfg(system, d["fileType"], d["switchIQ"], d["codeLength"], device, 0,
+                  d["samplingFreq"], d["codeFreqBasis"], d["IF"], d["L1_IF_step"],
+                  d["GLONASS_zero_channel"], d["dllCorrelatorSpacing"], d["dllNoiseBandwidth"],
+                  d["dllDampingRatio"], d["pllNoiseBandwidth"], d["fllNoiseBandwidth"])
+
+
+class SgtCtx:
+    """SoftGNSS float tracking (tracking.sci) for many channels over HBM-resident records."""
+
+    def __init__(self, system: int, device: int = 0, **settings):
+        self.cfg = sgt_cfg(system, device, **settings)
+        h = C.c_void_p()
+        _check(lib().gnsscorr_sgt_create(C.byref(h), C.byref(self.cfg)), "gnsscorr_sgt_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gnsscorr_sgt_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def loop_coefs(self):
+        v = [C.c_double() for _ in range(5)]
+        lib().gnsscorr_sgt_loop_coefs(C.byref(self.cfg), *[C.byref(x) for x in v])
+        return tuple(x.value for x in v)     # tau1code, tau2code, k1, k2, k3
+
+    def init_chans(self, code_ids, code_phases_1b, acq_freqs, streams=None, skip=0):
+        n = len(code_ids)
+        out = np.zeros(n, SGT_CHAN)
+        streams = np.zeros(n, np.int64) if streams is None else np.asarray(streams)
+        for i in range(n):
+            _check(lib().gnsscorr_sgt_init_chan(C.byref(self.cfg), int(code_ids[i]),
+                                                int(streams[i]), int(skip),
+                                                int(code_phases_1b[i]), float(acq_freqs[i]),
+                                                out[i:i + 1].ctypes.data),
+                   "gnsscorr_sgt_init_chan")
+        return out
+
+    def track(self, d_if, stride, n_samples, chans, n_epochs, closed_loop=True):
+        """Host channel array in/out; returns epochs [n_ch, n_epochs]."""
+        assert chans.dtype == SGT_CHAN and chans.flags.c_contiguous
+        ep = np.zeros((len(chans), n_epochs), SGT_EPOCH)
+        _check(lib().gnsscorr_sgt_track(self.h, d_if, stride, n_samples, len(chans),
+                                        _ptr(chans), n_epochs, int(closed_loop), _ptr(ep)),
+               "gnsscorr_sgt_track")
+        return ep
+
+    def track_dev(self, d_if, stride, n_samples, n_ch, d_chan, n_epochs, d_epochs,
+                  closed_loop=True):
+        _check(lib().gnsscorr_sgt_track_dev(self.h, d_if, stride, n_samples, n_ch, d_chan,
+                                            n_epochs, int(closed_loop), d_epochs),
+               "gnsscorr_sgt_track_dev")
+
+    def sync(self):
+        _check(lib().gnsscorr_sgt_sync(self.h), "gnsscorr_sgt_sync")
+
+    @property
+    def stream(self) -> int:
+        return lib().gnsscorr_sgt_stream(self.h)
 
 
 # ---------------------------------------------------------------- legacy OSG view

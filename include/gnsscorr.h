@@ -227,6 +227,83 @@ int gnsscorr_acq_sync(gnsscorr_acq_ctx *ctx);
 void *gnsscorr_acq_stream(gnsscorr_acq_ctx *ctx);
 
 /* ======================================================================
+ * SoftGNSS float tracking ("sgt"): the Scilab receivers' per-channel loop
+ *   GLONASS POSTPROCESSING_SCILAB_RECEIVERS/GLONASS/L1/tracking.sci:150-400
+ *   GPS     POSTPROCESSING_SCILAB_RECEIVERS/GPS/L1/tracking.sci:124-360
+ * One epoch = one code period: blksize = ceil((L - remCode)/step) samples,
+ * E/P/L replica indices ceil(remCode -/+ spc + k*step) (fp64, bit-exact),
+ * carrier exp(i*(2*pi*f*t + remCarr)) (fp64), six fp64 sums
+ * I = sum(code*imag(carr*raw)), Q = sum(code*real(carr*raw)), then (closed
+ * loop) the FLL-assisted PLL and the DLL of tracking.sci:329-375 on the GPU.
+ * The IF record(s) stay resident in HBM; each channel reads from its own
+ * position (the reference's per-channel mseek, tracking.sci:163-168).
+ * ==================================================================== */
+typedef struct gnsscorr_sgt_ctx gnsscorr_sgt_ctx;
+
+typedef struct {          /* initSettings.sci fields used by tracking.sci     */
+  int32_t system;         /* 0 = GPS L1 C/A (C/A code per PRN), 1 = GLONASS L1OF (ST) */
+  int32_t file_type;      /* settings.fileType: 1 = int8 real, 2 = int8 interleaved I,Q */
+  int32_t switch_iq;      /* settings.switchIQ (GLONASS only, tracking.sci:263-267) */
+  int32_t code_length;    /* settings.codeLength: 1023 / 511                   */
+  int32_t device;
+  int32_t max_channels;
+  double  samp_rate;      /* settings.samplingFreq                             */
+  double  code_freq_basis;/* settings.codeFreqBasis                            */
+  double  if_freq;        /* settings.IF                                       */
+  double  l1_if_step;     /* settings.L1_IF_step (GLONASS)                      */
+  double  glonass_zero_channel; /* settings.GLONASS_zero_channel               */
+  double  dll_spacing;    /* settings.dllCorrelatorSpacing [chips]             */
+  double  dll_noise_bw, dll_damping;   /* calcLoopCoef(dllNoiseBandwidth, dllDampingRatio, 1) */
+  double  pll_noise_bw, fll_noise_bw;  /* calcFLLPLLLoopCoef(pll, fll, PDIcarr=0.001) */
+} gnsscorr_sgt_cfg;
+
+typedef struct {          /* one tracking channel (tracking.sci:159-201 + loop state) */
+  int32_t code_id;        /* GPS PRN 1..32, or GLONASS FCH -7..6                */
+  int32_t stream;         /* which IF record (stride given per call)           */
+  int32_t status;         /* 0 tracking, 1 out of data (tracking.sci:273-277)  */
+  int32_t n_epochs;       /* epochs processed so far                           */
+  int64_t pos;            /* next sample (complex or real) of the record       */
+  int64_t pad;
+  double  rem_code, rem_carr, code_freq, carr_freq, carr_freq_basis;
+  double  old_code_nco, old_code_error, old_carr_nco, old_carr_error, i1, q1;
+  double  pad2;
+} gnsscorr_sgt_chan;      /* 128 bytes */
+
+typedef struct {          /* trackResults(ch).* for one epoch (tracking.sci:387-398) */
+  double  i_e, i_p, i_l, q_e, q_p, q_l;
+  double  carr_freq, code_freq, absolute_sample;
+  double  dll_discr, dll_discr_filt, pll_discr, pll_discr_filt;
+  int32_t blksize;
+  int32_t status;         /* 0 ok; 1 = this epoch was not processed (out of data) */
+} gnsscorr_sgt_epoch;     /* 112 bytes */
+
+/* Loop coefficients exactly as calcLoopCoef.sci:39-43 / calcFLLPLLLoopCoef.sci:36-38. */
+void gnsscorr_sgt_loop_coefs(const gnsscorr_sgt_cfg *cfg, double *tau1code, double *tau2code,
+                             double *k1, double *k2, double *k3);
+/* Channel initialisation from an acquisition result (tracking.sci:159-201):
+ * pos = skip_samples + code_phase_1b - 1, codeFreq = basis, carrFreq = acquiredFreq. */
+int gnsscorr_sgt_init_chan(const gnsscorr_sgt_cfg *cfg, int code_id, int stream,
+                           int64_t skip_samples, int64_t code_phase_1b, double acquired_freq,
+                           gnsscorr_sgt_chan *out);
+int gnsscorr_sgt_create(gnsscorr_sgt_ctx **out, const gnsscorr_sgt_cfg *cfg);
+int gnsscorr_sgt_destroy(gnsscorr_sgt_ctx *ctx);
+/* Run n_epochs epochs of n_ch channels (state in d_chan, updated in place).
+ * d_if: the records, stream s at d_if + s*stream_stride bytes, each
+ * n_samples samples long.  closed_loop=1: the loop filters of tracking.sci
+ * update codeFreq/carrFreq after every epoch; 0: correlator only, frequencies
+ * held (a host-side loop updates them between calls).  d_epochs[ch*n_epochs+e]
+ * receives the per-epoch record.  Asynchronous on the context's stream. */
+int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx *ctx, const int8_t *d_if, int64_t stream_stride,
+                           int64_t n_samples, int n_ch, gnsscorr_sgt_chan *d_chan,
+                           int n_epochs, int closed_loop, gnsscorr_sgt_epoch *d_epochs);
+/* Same with host channel state / results (synchronous). */
+int gnsscorr_sgt_track(gnsscorr_sgt_ctx *ctx, const int8_t *d_if, int64_t stream_stride,
+                       int64_t n_samples, int n_ch, gnsscorr_sgt_chan *h_chan, int n_epochs,
+                       int closed_loop, gnsscorr_sgt_epoch *h_epochs);
+int gnsscorr_sgt_sync(gnsscorr_sgt_ctx *ctx);
+void *gnsscorr_sgt_stream(gnsscorr_sgt_ctx *ctx);
+
+/* ======================================================================
  * Device buffers / events (so hosts need no other GPU runtime)
  * ==================================================================== */
 int gnsscorr_dev_alloc(int device, size_t bytes, void **d_ptr);
