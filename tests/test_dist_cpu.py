@@ -1,0 +1,75 @@
+"""CPU, multi-process: the N>1 control path with gloo (world_size 2).
+
+* bench.Dist: barrier + max-over-ranks timing (the bench contract);
+* full-sky sharding (gnsscorr/fullsky.py): every rank takes a disjoint group
+  set, the per-group results are gathered (all_gather_object over gloo) and
+  merged on rank 0 in group order -- the only exchange config 5 needs.
+No GPU: each rank fabricates its shard's results.
+"""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "gnss-sdr.ru_amd")]
+    import bench
+    from gnsscorr.fullsky import GROUPS, merge, shard
+    d = bench.Dist()
+    d.barrier()
+    m = d.max(float(rank + 1) * 1.5)
+    mine = shard(len(GROUPS), world, rank)
+    part = [(i, GROUPS[i][0], GROUPS[i][1], float(i) * 10 + rank) for i in mine]
+    allp = d.gather(part)
+    if rank == 0:
+        merged = merge(allp)
+        q.put(("ok", m, [r[0] for r in merged], [r[3] for r in merged]))
+    d.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_barrier_max_and_fullsky_gather(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        tag, m, idx, vals = q.get(timeout=120)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert tag == "ok"
+    assert m == 1.5 * world
+    assert idx == list(range(46))
+    assert vals == [i * 10.0 + i % world for i in range(46)]
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_shard_is_a_partition():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gnss-sdr.ru_amd"))
+    from gnsscorr.fullsky import shard
+    for world in (1, 2, 3, 4, 8):
+        parts = [shard(46, world, r) for r in range(world)]
+        flat = sorted(i for p in parts for i in p)
+        assert flat == list(range(46))
+        assert max(map(len, parts)) - min(map(len, parts)) <= 1
+    with pytest.raises(ValueError):
+        shard(46, 2, 2)
