@@ -22,6 +22,8 @@ extern "C" {
 void gnsscorr_osg_table_image(int8_t *img);
 void gnsscorr_osg_packed_table(uint32_t *pk);
 void gnsscorr_set_error(const char *fmt, ...);
+/* GPS-SDR tables (sdr_host.c): packed (i, q) int16 pairs, N = 2048 */
+void gnsscorr_sdr_twiddles(int16_t *w, int16_t *iw);
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,8 @@ SGT_EPOCH = np.dtype([("I_E", "<f8"), ("I_P", "<f8"), ("I_L", "<f8"), ("Q_E", "<
                       ("pllDiscr", "<f8"), ("pllDiscrFilt", "<f8"), ("blksize", "<i4"),
                       ("status", "<i4")])
 assert SGT_CHAN.itemsize == 128 and SGT_EPOCH.itemsize == 112
+SDR_RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
+                       ("magnitude", "<u4"), ("success", "<i4"), ("row", "<i4")])
 
 ACQ_BEST_OF_BLOCKS = 0
 ACQ_NONCOHERENT = 1
@@ -78,6 +80,10 @@ class SgtCfg(C.Structure):
                 ("pll_noise_bw", C.c_double), ("fll_noise_bw", C.c_double)]
 
 
+class SdrAcqCfg(C.Structure):
+    _fields_ = [("fif", C.c_double), ("device", C.c_int32), ("saturate", C.c_int32)]
+
+
 # every symbol include/gnsscorr.h + include/gnsscorr_osg.h declare
 EXPORTED_FUNCTIONS = [
     "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
@@ -92,6 +98,9 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sgt_loop_coefs", "gnsscorr_sgt_init_chan", "gnsscorr_sgt_create",
     "gnsscorr_sgt_destroy", "gnsscorr_sgt_track_dev", "gnsscorr_sgt_track", "gnsscorr_sgt_sync",
     "gnsscorr_sgt_stream",
+    "gnsscorr_sdr_prn_codes", "gnsscorr_sdr_sine_gen", "gnsscorr_sdr_acq_create",
+    "gnsscorr_sdr_acq_destroy", "gnsscorr_sdr_acq_strong", "gnsscorr_sdr_acq_strong_dev",
+    "gnsscorr_sdr_acq_sync", "gnsscorr_sdr_acq_stream",
     "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
     "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
     "gnsscorr_event_elapsed_ms", "gnsscorr_event_destroy", "gnsscorr_dev_fill_if2",
@@ -152,6 +161,14 @@ def lib() -> C.CDLL:
         "gnsscorr_sgt_track": (I, [P, P, I64, I64, I, P, I, I, P]),
         "gnsscorr_sgt_sync": (I, [P]),
         "gnsscorr_sgt_stream": (P, [P]),
+        "gnsscorr_sdr_prn_codes": (I, [P]),
+        "gnsscorr_sdr_sine_gen": (None, [P, D, D, I]),
+        "gnsscorr_sdr_acq_create": (I, [C.POINTER(P), C.POINTER(SdrAcqCfg)]),
+        "gnsscorr_sdr_acq_destroy": (I, [P]),
+        "gnsscorr_sdr_acq_strong": (I, [P, P, I, I, P, I, I, P]),
+        "gnsscorr_sdr_acq_strong_dev": (I, [P, P, I, I, P, I, I, P]),
+        "gnsscorr_sdr_acq_sync": (I, [P]),
+        "gnsscorr_sdr_acq_stream": (P, [P]),
         "gnsscorr_dev_alloc": (I, [I, C.c_size_t, C.POINTER(P)]),
         "gnsscorr_dev_free": (I, [I, P]),
         "gnsscorr_memcpy_htod": (I, [I, P, P, C.c_size_t]),
@@ -524,6 +541,59 @@ class SgtCtx:
     @property
     def stream(self) -> int:
         return lib().gnsscorr_sgt_stream(self.h)
+
+
+# ---------------------------------------------------------------- GPS-SDR integer acquisition
+def sdr_prn_codes() -> np.ndarray:
+    """PRN_Codes (51, 2048, 2) int16 as gen_fft_codes.m builds them."""
+    out = np.zeros((51, 2048, 2), np.int16)
+    _check(lib().gnsscorr_sdr_prn_codes(_ptr(out)), "gnsscorr_sdr_prn_codes")
+    return out
+
+
+def sdr_sine_gen(f: float, n: int = 2048, fs: float = 2048000.0) -> np.ndarray:
+    out = np.zeros((n, 2), np.int16)
+    lib().gnsscorr_sdr_sine_gen(_ptr(out), f, fs, n)
+    return out
+
+
+class SdrAcqCtx:
+    """GPS-SDR strong (1 ms, int16 FFT) acquisition, bit-exact with the reference."""
+
+    def __init__(self, fif: float = 38400.0, device: int = 0, saturate: bool = False):
+        h = C.c_void_p()
+        _check(lib().gnsscorr_sdr_acq_create(C.byref(h), C.byref(SdrAcqCfg(fif, device,
+                                                                             int(saturate)))),
+               "gnsscorr_sdr_acq_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gnsscorr_sdr_acq_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def strong(self, buffers, svs, doppmin=-15000, doppmax=15000) -> np.ndarray:
+        """buffers: (n_rec, 2048, 2) or (2048, 2) int16; returns SDR_RESULT [n_rec, n_sv]."""
+        b = np.ascontiguousarray(buffers, np.int16).reshape(-1, 2048, 2)
+        svs = np.ascontiguousarray(svs, np.int32)
+        res = np.zeros((b.shape[0], len(svs)), SDR_RESULT)
+        _check(lib().gnsscorr_sdr_acq_strong(self.h, _ptr(b), b.shape[0], len(svs), _ptr(svs),
+                                             doppmin, doppmax, _ptr(res)),
+               "gnsscorr_sdr_acq_strong")
+        return res
+
+    def strong_dev(self, d_buff, n_rec, n_sv, d_svs, d_res, doppmin=-15000, doppmax=15000):
+        _check(lib().gnsscorr_sdr_acq_strong_dev(self.h, d_buff, n_rec, n_sv, d_svs, doppmin,
+                                                 doppmax, d_res), "gnsscorr_sdr_acq_strong_dev")
+
+    def sync(self):
+        _check(lib().gnsscorr_sdr_acq_sync(self.h), "gnsscorr_sdr_acq_sync")
+
+    @property
+    def stream(self) -> int:
+        return lib().gnsscorr_sdr_acq_stream(self.h)
 
 
 # ---------------------------------------------------------------- legacy OSG view

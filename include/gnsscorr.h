@@ -304,6 +304,54 @@ int gnsscorr_sgt_sync(gnsscorr_sgt_ctx *ctx);
 void *gnsscorr_sgt_stream(gnsscorr_sgt_ctx *ctx);
 
 /* ======================================================================
+ * GPS-SDR integer strong acquisition ("sdr"), bit-exact with the real-time
+ * receiver's int16 path (REALTIME_RECEIVERS/GPS/GPS_SDR_REAL_TIME_GPS_RECEIVER):
+ *   Acquisition::doPrepIF    objects/acquisition.cpp:191-236 (1 ms buffer)
+ *   Acquisition::doAcqStrong objects/acquisition.cpp:244-301
+ * Input: CPX buffers of 2048 int16 (I, Q) pairs = 1 ms at 2.048 Msps
+ * (defines.h:150-151), IF fif (signaldef.h:34: 38.4 kHz).  Per sv (0-based
+ * index into PRN_Codes, MAX_SV = 32): 4 sub-bins (0/250/500/750 Hz) x 1 kHz
+ * circular spectrum shifts lcv in [doppmin/1000, doppmax/1000), int16 FFTs
+ * with the reference's Q14 twiddles, rank scaling and wrap points.
+ * ==================================================================== */
+typedef struct gnsscorr_sdr_acq_ctx gnsscorr_sdr_acq_ctx;
+
+typedef struct {
+  double  fif;            /* IF [Hz]: the wipe-offs are sine_gen(-fif - 250*j) */
+  int32_t device;
+  int32_t saturate;       /* 1: sse_cmulsc packssdw saturation (production);
+                             0: x86_cmulsc int16 wrap (the -DNO_SIMD build)   */
+} gnsscorr_sdr_acq_cfg;
+
+typedef struct {          /* Acq_Command_S result fields (structs.h:130-164) */
+  int32_t  sv;
+  int32_t  code_phase;    /* 2048 - argmax                                   */
+  int32_t  doppler;       /* lcv*1000 + lcv2*250                             */
+  uint32_t magnitude;     /* I^2 + Q^2 of the peak (int32 arithmetic)        */
+  int32_t  success;       /* magnitude > THRESH_STRONG (= 0, config.h:72)    */
+  int32_t  row;           /* winning row (lcv - doppmin/1000)*4 + lcv2       */
+} gnsscorr_sdr_acq_result;
+
+/* PRN_Codes (accessories/prn_codes.h, generated by gen_fft_codes.m): 51 PRNs x
+ * 2048 (re, im) int16 = conj(FFT(resampled code)) scaled to 9 bits. */
+int gnsscorr_sdr_prn_codes(int16_t *h_out);
+/* sine_gen (accessories/misc.cpp:95-115): n (i, q) int16 pairs. */
+void gnsscorr_sdr_sine_gen(int16_t *h_out, double f, double fs, int n);
+int gnsscorr_sdr_acq_create(gnsscorr_sdr_acq_ctx **out, const gnsscorr_sdr_acq_cfg *cfg);
+int gnsscorr_sdr_acq_destroy(gnsscorr_sdr_acq_ctx *ctx);
+/* n_rec buffers (each 2048 CPX) x n_sv svs -> h_res[rec*n_sv + s].  Requires
+ * -100 <= doppmin/1000 < doppmax/1000 <= 101 (the reference's +-100-bin row
+ * padding, acquisition.cpp:229-233) and 0 <= sv < 32. */
+int gnsscorr_sdr_acq_strong(gnsscorr_sdr_acq_ctx *ctx, const int16_t *h_buff, int n_rec, int n_sv,
+                            const int32_t *h_svs, int doppmin, int doppmax,
+                            gnsscorr_sdr_acq_result *h_res);
+int gnsscorr_sdr_acq_strong_dev(gnsscorr_sdr_acq_ctx *ctx, const int16_t *d_buff, int n_rec,
+                                int n_sv, const int32_t *d_svs, int doppmin, int doppmax,
+                                gnsscorr_sdr_acq_result *d_res);
+int gnsscorr_sdr_acq_sync(gnsscorr_sdr_acq_ctx *ctx);
+void *gnsscorr_sdr_acq_stream(gnsscorr_sdr_acq_ctx *ctx);
+
+/* ======================================================================
  * Device buffers / events (so hosts need no other GPU runtime)
  * ==================================================================== */
 int gnsscorr_dev_alloc(int device, size_t bytes, void **d_ptr);

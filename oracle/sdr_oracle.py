@@ -1,0 +1,190 @@
+"""oracle/sdr_oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes views of
+  * OracleSDR: our C restatement of the GPS-SDR int16 strong acquisition
+    (oracle/sdr_acq.c, built into liboracle.so), and
+  * RefSDR: the reference primitives compiled from their own sources with
+    -DNO_SIMD (oracle/_ref/libsdr_ref.so; only where /root/reference exists),
+plus a deterministic input generator for the 2.048 Msps CPX buffer the
+acquisition consumes (SDR/includes/defines.h:150-151, IF 38.4 kHz signaldef.h:34).
+Only tests/, smoke() and bench.py's cpu_baseline use this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libsdr_ref.so")
+N = 2048
+FS = 2048000.0
+IF_SDR = 38400.0
+RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
+                   ("magnitude", "<u4"), ("success", "<i4"), ("row", "<i4")])
+R1 = np.zeros(16, np.int32)
+R2 = np.array([0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 1, 1, 1, 1, 1], np.int32)
+
+
+def _p(a):
+    return a.ctypes.data
+
+
+def have_ref() -> bool:
+    return os.path.exists(REF_SO)
+
+
+class OracleSDR:
+    def __init__(self):
+        L = C.CDLL(ORACLE_SO)
+        P, I, D = C.c_void_p, C.c_int, C.c_double
+        L.sdro_sine_gen.argtypes = [P, D, D, I]
+        L.sdro_twiddles.argtypes = [I, P, P]
+        L.sdro_fft.argtypes = [P, I, P, P]
+        L.sdro_cmulsc.argtypes = [P, P, P, I, I, I]
+        L.sdro_cmag_max.argtypes = [P, I, P, P]
+        L.sdro_prep_if.argtypes = [P, D, I, P]
+        L.sdro_acq_strong.argtypes = [P, P, I, I, I, I]
+        L.sdro_acq_strong.restype = _Res
+        L.sdro_prn_codes.argtypes = [P]
+        self.L = L
+
+    def sine_gen(self, f, n=N, fs=FS):
+        out = np.zeros((n, 2), np.int16)
+        self.L.sdro_sine_gen(_p(out), f, fs, n)
+        return out
+
+    def fft(self, x, inverse=False, scale=None):
+        x = np.ascontiguousarray(x, np.int16).copy()
+        n = x.shape[0]
+        w = np.zeros((n // 2, 4), np.int16)
+        iw = np.zeros((n // 2, 4), np.int16)
+        self.L.sdro_twiddles(n, _p(w), _p(iw))
+        sc = np.ascontiguousarray(R1 if scale is None else scale, np.int32)
+        self.L.sdro_fft(_p(x), n, _p(iw if inverse else w), _p(sc))
+        return x
+
+    def cmulsc(self, a, b, shift, saturate=False):
+        a = np.ascontiguousarray(a, np.int16)
+        b = np.ascontiguousarray(b, np.int16)
+        c = np.zeros_like(a)
+        self.L.sdro_cmulsc(_p(a), _p(b), _p(c), a.shape[0], shift, int(saturate))
+        return c
+
+    def cmag_max(self, a):
+        a = np.ascontiguousarray(a, np.int16)
+        i, m = C.c_int32(), C.c_int32()
+        self.L.sdro_cmag_max(_p(a), a.shape[0], C.byref(i), C.byref(m))
+        return i.value, m.value
+
+    def prep_if(self, buff, fif=IF_SDR, saturate=False):
+        buff = np.ascontiguousarray(buff, np.int16)
+        rows = np.zeros((4, N, 2), np.int16)
+        self.L.sdro_prep_if(_p(buff), fif, int(saturate), _p(rows))
+        return rows
+
+    def acq_strong(self, buff, codes, svs, doppmin=-15000, doppmax=15000, fif=IF_SDR,
+                   saturate=False):
+        rows = self.prep_if(buff, fif, saturate)
+        out = np.zeros(len(svs), RESULT)
+        for k, sv in enumerate(svs):
+            r = self.L.sdro_acq_strong(_p(rows), _p(np.ascontiguousarray(codes[sv])), int(sv),
+                                       doppmin, doppmax, int(saturate))
+            out[k] = (r.sv, r.code_phase, r.doppler, r.magnitude, r.success, r.row)
+        return out
+
+    def prn_codes(self):
+        out = np.zeros((51, N, 2), np.int16)
+        self.L.sdro_prn_codes(_p(out))
+        return out
+
+
+class _Res(C.Structure):
+    _fields_ = [("sv", C.c_int32), ("code_phase", C.c_int32), ("doppler", C.c_int32),
+                ("magnitude", C.c_uint32), ("success", C.c_int32), ("row", C.c_int32)]
+
+
+class RefSDR:
+    def __init__(self):
+        L = C.CDLL(REF_SO)
+        P, I, D = C.c_void_p, C.c_int, C.c_double
+        L.ref_sdr_sine_gen.argtypes = [P, D, D, I]
+        L.ref_sdr_fft.argtypes = [P, I, P, I]
+        L.ref_sdr_cmulsc.argtypes = [P, P, P, I, I]
+        L.ref_sdr_cmag_max.argtypes = [P, I, P, P]
+        L.ref_sdr_prn_codes.restype = C.POINTER(C.c_int16)
+        L.ref_sdr_acq_strong.argtypes = [P, D, I, I, I, P]
+        self.L = L
+
+    def sine_gen(self, f, n=N, fs=FS):
+        out = np.zeros((n, 2), np.int16)
+        self.L.ref_sdr_sine_gen(_p(out), f, fs, n)
+        return out
+
+    def fft(self, x, inverse=False, scale=None):
+        x = np.ascontiguousarray(x, np.int16).copy()
+        sc = np.ascontiguousarray(R1 if scale is None else scale, np.int32)
+        self.L.ref_sdr_fft(_p(x), x.shape[0], _p(sc), int(inverse))
+        return x
+
+    def cmulsc(self, a, b, shift):
+        a = np.ascontiguousarray(a, np.int16).copy()
+        b = np.ascontiguousarray(b, np.int16).copy()
+        c = np.zeros_like(a)
+        self.L.ref_sdr_cmulsc(_p(a), _p(b), _p(c), a.shape[0], shift)
+        return c
+
+    def cmag_max(self, a):
+        a = np.ascontiguousarray(a, np.int16).copy()
+        i, m = C.c_int32(), C.c_int32()
+        self.L.ref_sdr_cmag_max(_p(a), a.shape[0], C.byref(i), C.byref(m))
+        return i.value, m.value
+
+    def prn_codes(self):
+        p = self.L.ref_sdr_prn_codes()
+        return np.ctypeslib.as_array(p, shape=(51 * N * 2,)).copy().reshape(51, N, 2)
+
+    def acq_strong(self, buff, svs, doppmin=-15000, doppmax=15000, fif=IF_SDR):
+        buff = np.ascontiguousarray(buff, np.int16)
+        out = np.zeros(len(svs), RESULT)
+        o = np.zeros(6, np.int32)
+        for k, sv in enumerate(svs):
+            self.L.ref_sdr_acq_strong(_p(buff), fif, int(sv), doppmin, doppmax, _p(o))
+            out[k] = tuple(int(v) for v in o)
+        return out
+
+
+def ca_chips(prn: int) -> np.ndarray:
+    """+-1 C/A chips, code_gen (SDR/accessories/misc.cpp:28-87) form."""
+    g1 = np.zeros(1023, np.int8)
+    g2 = np.zeros(1023, np.int8)
+    r1 = [1] * 10
+    r2 = [1] * 10
+    for k in range(1023):
+        g1[k], g2[k] = r1[0], r2[0]
+        f1 = r1[7] ^ r1[0]
+        f2 = (r2[8] + r2[7] + r2[4] + r2[2] + r2[1] + r2[0]) & 1
+        r1 = r1[1:] + [f1]
+        r2 = r2[1:] + [f2]
+    delays = [5, 6, 7, 8, 17, 18, 139, 140, 141, 251, 252, 254, 255, 256, 257, 258, 469, 470,
+              471, 472, 473, 474, 509, 512, 513, 514, 515, 516, 859, 860, 861, 862]
+    d = 1023 - delays[prn - 1]
+    return 2 * (g1 ^ g2[(np.arange(1023) + d) % 1023]).astype(np.int16) - 1
+
+
+def make_buffer(sigs, n=N, seed=1, amp_noise=2.0, fif=IF_SDR):
+    """CPX int16 buffer [n, 2] at 2.048 Msps: planted C/A signals at +(fif+doppler),
+    complex Gaussian noise, rounded to small integers (AGC-like levels)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / FS
+    z = amp_noise * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+    for s in sigs:
+        chips = ca_chips(s["prn"])
+        cp = (s["code_phase"] + t * 1.023e6 * (1 + s["doppler"] / 1575.42e6)) % 1023
+        z += s["amp"] * chips[cp.astype(np.int64)] * np.exp(2j * np.pi * (fif + s["doppler"]) * t)
+    out = np.zeros((n, 2), np.int16)
+    out[:, 0] = np.clip(np.round(z.real), -127, 127)
+    out[:, 1] = np.clip(np.round(z.imag), -127, 127)
+    return out

@@ -1,0 +1,55 @@
+"""Generate tests/golden/sdr_*.npz from the REFERENCE GPS-SDR primitives.
+
+oracle/_ref/libsdr_ref.so is the reference's simd/x86.cpp, objects/fft.cpp and
+accessories/misc.cpp compiled with -DNO_SIMD from /root/reference (make -C
+oracle ref), plus PRN_Codes from accessories/prn_codes.h.  Stored:
+  sdr_prn_codes.npz   the PRN_Codes table (51 x 2048 x (re, im) int16)
+  sdr_acq.npz         input buffers (2048 CPX each, deterministic) and the
+                      reference doPrepIF + doAcqStrong results for sv 0..31
+  sdr_fft.npz         int16 FFT known answers (forward / inverse, rank masks,
+                      incl. inputs large enough to exercise the int16 wrap)
+Usage:  python tests/golden/make_sdr_golden.py
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import sdr_oracle as S  # noqa: E402
+
+SCENES = [  # (seed, amp_noise, signals)
+    (1, 2.0, [dict(prn=5, code_phase=300.0, doppler=2250.0, amp=1.0),
+              dict(prn=17, code_phase=800.3, doppler=-4100.0, amp=0.8)]),
+    (2, 4.0, [dict(prn=1, code_phase=10.5, doppler=-12300.0, amp=1.5),
+              dict(prn=32, code_phase=1000.0, doppler=7777.0, amp=1.2),
+              dict(prn=12, code_phase=511.0, doppler=0.0, amp=1.0)]),
+    (3, 40.0, [dict(prn=24, code_phase=77.0, doppler=14000.0, amp=30.0)]),   # large levels
+]
+
+
+def main():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    ref = S.RefSDR()
+    out = os.path.dirname(os.path.abspath(__file__))
+    np.savez_compressed(os.path.join(out, "sdr_prn_codes.npz"), prn_codes=ref.prn_codes())
+    bufs = np.stack([S.make_buffer(sig, seed=seed, amp_noise=a) for seed, a, sig in SCENES])
+    svs = np.arange(32)
+    res = np.stack([ref.acq_strong(b, svs) for b in bufs])
+    res_narrow = np.stack([ref.acq_strong(b, svs, -3000, 5000) for b in bufs])
+    np.savez_compressed(os.path.join(out, "sdr_acq.npz"), buffers=bufs, svs=svs, res=res,
+                        res_narrow=res_narrow, fif=np.array(S.IF_SDR))
+    rng = np.random.default_rng(11)
+    xs = np.stack([rng.integers(-a, a + 1, (2048, 2)) for a in (3, 300, 20000)]).astype(np.int16)
+    fwd = np.stack([ref.fft(x, False, S.R1) for x in xs])
+    inv = np.stack([ref.fft(x, True, S.R2) for x in xs])
+    np.savez_compressed(os.path.join(out, "sdr_fft.npz"), x=xs, fwd_r1=fwd, inv_r2=inv)
+    for k, r in enumerate(res):
+        print("scene", k, [(int(v["sv"]) + 1, int(v["code_phase"]), int(v["doppler"]),
+                            int(v["magnitude"])) for v in r if v["magnitude"] > 0][:3])
+
+
+if __name__ == "__main__":
+    main()

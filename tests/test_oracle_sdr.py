@@ -1,0 +1,88 @@
+"""CPU: the GPS-SDR int16 acquisition oracle (oracle/sdr_acq.c) pinned against
+the reference primitives compiled from their own sources (-DNO_SIMD,
+oracle/_ref/libsdr_ref.so) and against the committed fixtures
+(tests/golden/sdr_*.npz, made by tests/golden/make_sdr_golden.py), plus the
+product's host tables (PRN_Codes, sine_gen) against the same fixtures.
+
+Reference: REALTIME_RECEIVERS/GPS/GPS_SDR_REAL_TIME_GPS_RECEIVER objects/fft.cpp,
+simd/x86.cpp, accessories/misc.cpp, accessories/gen_fft_codes.m,
+objects/acquisition.cpp:191-301.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import sdr_oracle as S
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+need_ref = pytest.mark.skipif(not S.have_ref(), reason="reference build (oracle/_ref) absent")
+
+
+@pytest.fixture(scope="module")
+def o(oracle):
+    return S.OracleSDR()
+
+
+def test_prn_codes_golden(o, gc):
+    g = np.load(os.path.join(GOLD, "sdr_prn_codes.npz"))["prn_codes"]
+    assert g.shape == (51, 2048, 2)
+    assert (o.prn_codes() == g).all()            # oracle restatement of gen_fft_codes.m
+    assert (gc.sdr_prn_codes() == g).all()       # the product's table
+    # 9-bit scaling: the largest magnitude over all 51 codes is 512
+    assert np.abs(g.astype(np.float64)).max() <= 512
+
+
+def test_fft_golden(o):
+    f = np.load(os.path.join(GOLD, "sdr_fft.npz"))
+    for x, fw, iv in zip(f["x"], f["fwd_r1"], f["inv_r2"]):
+        assert (o.fft(x, False, S.R1) == fw).all()
+        assert (o.fft(x, True, S.R2) == iv).all()
+
+
+def test_acq_strong_golden(o):
+    f = np.load(os.path.join(GOLD, "sdr_acq.npz"))
+    codes = np.load(os.path.join(GOLD, "sdr_prn_codes.npz"))["prn_codes"]
+    for b, res, nar in zip(f["buffers"], f["res"], f["res_narrow"]):
+        got = o.acq_strong(b, codes, f["svs"], fif=float(f["fif"]))
+        assert (got == res).all()
+        got = o.acq_strong(b, codes, f["svs"], -3000, 5000, fif=float(f["fif"]))
+        assert (got == nar).all()
+
+
+def test_planted_signals_found(o):
+    f = np.load(os.path.join(GOLD, "sdr_acq.npz"))
+    r = f["res"][0]
+    # scene 0: PRN 5 at 300 chips / +2250 Hz -> code_phase 2048 - 2*(1023-300)... as sampled
+    assert r[4]["doppler"] == 2250 and abs(r[4]["code_phase"] - 600) <= 1
+    assert r[4]["magnitude"] > 5 * np.median(r["magnitude"])
+
+
+@need_ref
+def test_oracle_matches_reference_build(o):
+    ref = S.RefSDR()
+    for f in (-38400.0, -38650.0, -38900.0, -39150.0, 1000.5, 0.0):
+        assert (o.sine_gen(f) == ref.sine_gen(f)).all()
+    rng = np.random.default_rng(5)
+    for amp in (3, 1000, 32767):
+        x = rng.integers(-amp, amp + 1, (2048, 2)).astype(np.int16)
+        y = rng.integers(-amp, amp + 1, (2048, 2)).astype(np.int16)
+        for inv in (False, True):
+            for sc in (S.R1, S.R2, np.ones(16, np.int32)):
+                assert (o.fft(x, inv, sc) == ref.fft(x, inv, sc)).all()
+        for sh in (10, 14):
+            assert (o.cmulsc(x, y, sh) == ref.cmulsc(x, y, sh)).all()
+        assert o.cmag_max(x) == ref.cmag_max(x)
+    assert (o.prn_codes() == ref.prn_codes()).all()
+    buf = S.make_buffer([dict(prn=9, code_phase=123.0, doppler=-6400.0, amp=1.0)], seed=77)
+    svs = [8, 0, 20]
+    assert (o.acq_strong(buf, ref.prn_codes(), svs) == ref.acq_strong(buf, svs)).all()
+
+
+def test_saturating_cmulsc_differs_only_on_overflow(o):
+    x = np.array([[32767, 32767], [-32768, 5], [100, -100]], np.int16)
+    y = np.array([[32767, -32767], [-32768, 0], [3, 4]], np.int16)
+    w, s = o.cmulsc(x, y, 1), o.cmulsc(x, y, 1, saturate=True)
+    assert (w[2] == s[2]).all()
+    assert s[0, 0] == 32767 or s[0, 1] in (32767, -32768)
+    assert not (w[:2] == s[:2]).all()
