@@ -113,3 +113,25 @@ int gnsscorr_sdr_prn_codes(int16_t *out)
   free(im);
   return GNSSCORR_OK;
 }
+
+/* code_gen (SDR/accessories/misc.cpp:28-87): 0/1 chips of the 0-based G2-delay
+ * index sv (G1 xor G2 delayed by 1023 - delay[sv]). */
+void gnsscorr_sdr_code_gen(int sv, uint8_t *chips)
+{
+  static const short g2d[51] = {5, 6, 7, 8, 17, 18, 139, 140, 141, 251, 252, 254, 255, 256, 257,
+                                258, 469, 470, 471, 472, 473, 474, 509, 512, 513, 514, 515, 516,
+                                859, 860, 861, 862, 145, 175, 52, 21, 237, 235, 886, 657, 634,
+                                762, 355, 1012, 176, 603, 130, 359, 595, 68, 386};
+  uint8_t g1[1023], g2[1023];
+  unsigned s1 = 0x3FF, s2 = 0x3FF;
+  for (int k = 0; k < 1023; k++) {
+    g1[k] = s1 & 1u;
+    g2[k] = s2 & 1u;
+    const unsigned f1 = ((s1 >> 7) ^ s1) & 1u;
+    const unsigned f2 = ((s2 >> 8) ^ (s2 >> 7) ^ (s2 >> 4) ^ (s2 >> 2) ^ (s2 >> 1) ^ s2) & 1u;
+    s1 = (s1 >> 1) | (f1 << 9);
+    s2 = (s2 >> 1) | (f2 << 9);
+  }
+  const int d = 1023 - g2d[sv];
+  for (int k = 0; k < 1023; k++) chips[k] = g1[k] ^ g2[(k + d) % 1023];
+}

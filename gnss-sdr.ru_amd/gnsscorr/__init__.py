@@ -53,6 +53,19 @@ SGT_EPOCH = np.dtype([("I_E", "<f8"), ("I_P", "<f8"), ("I_L", "<f8"), ("Q_E", "<
                       ("pllDiscr", "<f8"), ("pllDiscrFilt", "<f8"), ("blksize", "<i4"),
                       ("status", "<i4")])
 assert SGT_CHAN.itemsize == 128 and SGT_EPOCH.itemsize == 112
+SDR_CHAN = np.dtype([("code_phase", "<f8"), ("carrier_phase", "<f8"),
+                     ("carrier_phase_prev", "<f8"), ("code_phase_mod", "<f8"),
+                     ("carrier_phase_mod", "<f8"), ("code_nco", "<f8"), ("carrier_nco", "<f8"),
+                     ("chan", "<u4"), ("sv", "<u4"), ("navigate", "<u4"), ("active", "<u4"),
+                     ("count", "<u4"), ("scount", "<u4"), ("epoch_1ms", "<u4"),
+                     ("epoch_20ms", "<u4"), ("z_count", "<u4"), ("rollover", "<u4"),
+                     ("cbin", "<u4", (3,)), ("sbin", "<u4"), ("coff", "<i4", (3,)),
+                     ("soff", "<i4")])
+SDR_CORR = np.dtype([("i", "<i4", (3,)), ("q", "<i4", (3,))])
+SDR_JOB = np.dtype([("packet", "<i4"), ("data_off", "<i4"), ("samps", "<i4"), ("sv", "<i4"),
+                    ("sbin", "<i4"), ("soff", "<i4"), ("cbin", "<i4", (3,)),
+                    ("coff", "<i4", (3,))])
+assert SDR_CHAN.itemsize == 128 and SDR_CORR.itemsize == 24 and SDR_JOB.itemsize == 48
 SDR_RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
                        ("magnitude", "<u4"), ("success", "<i4"), ("row", "<i4")])
 
@@ -80,6 +93,10 @@ class SgtCfg(C.Structure):
                 ("pll_noise_bw", C.c_double), ("fll_noise_bw", C.c_double)]
 
 
+class SdrCorrCfg(C.Structure):
+    _fields_ = [("device", C.c_int32), ("saturate", C.c_int32)]
+
+
 class SdrAcqCfg(C.Structure):
     _fields_ = [("fif", C.c_double), ("device", C.c_int32), ("saturate", C.c_int32)]
 
@@ -101,6 +118,9 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sdr_prn_codes", "gnsscorr_sdr_sine_gen", "gnsscorr_sdr_acq_create",
     "gnsscorr_sdr_acq_destroy", "gnsscorr_sdr_acq_strong", "gnsscorr_sdr_acq_strong_dev",
     "gnsscorr_sdr_acq_sync", "gnsscorr_sdr_acq_stream",
+    "gnsscorr_sdr_corr_create", "gnsscorr_sdr_corr_destroy", "gnsscorr_sdr_init_chan",
+    "gnsscorr_sdr_accum_dev", "gnsscorr_sdr_correlate", "gnsscorr_sdr_corr_sync",
+    "gnsscorr_sdr_corr_stream",
     "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
     "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
     "gnsscorr_event_elapsed_ms", "gnsscorr_event_destroy", "gnsscorr_dev_fill_if2",
@@ -169,6 +189,13 @@ def lib() -> C.CDLL:
         "gnsscorr_sdr_acq_strong_dev": (I, [P, P, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_sync": (I, [P]),
         "gnsscorr_sdr_acq_stream": (P, [P]),
+        "gnsscorr_sdr_corr_create": (I, [C.POINTER(P), C.POINTER(SdrCorrCfg)]),
+        "gnsscorr_sdr_corr_destroy": (I, [P]),
+        "gnsscorr_sdr_init_chan": (I, [P, I, I, I, D]),
+        "gnsscorr_sdr_accum_dev": (I, [P, P, I, P, P]),
+        "gnsscorr_sdr_correlate": (I, [P, P, I, I, P, P, P, P, P]),
+        "gnsscorr_sdr_corr_sync": (I, [P]),
+        "gnsscorr_sdr_corr_stream": (P, [P]),
         "gnsscorr_dev_alloc": (I, [I, C.c_size_t, C.POINTER(P)]),
         "gnsscorr_dev_free": (I, [I, P]),
         "gnsscorr_memcpy_htod": (I, [I, P, P, C.c_size_t]),
@@ -594,6 +621,55 @@ class SdrAcqCtx:
     @property
     def stream(self) -> int:
         return lib().gnsscorr_sdr_acq_stream(self.h)
+
+
+class SdrCorrCtx:
+    """GPS-SDR tracking correlator (Correlator class): batched Accum on the GPU,
+    Correlate schedule + UpdateState/DumpAccum on the host, channel loop by callback."""
+
+    def __init__(self, device: int = 0, saturate: bool = False):
+        h = C.c_void_p()
+        _check(lib().gnsscorr_sdr_corr_create(C.byref(h), C.byref(SdrCorrCfg(device,
+                                                                               int(saturate)))),
+               "gnsscorr_sdr_corr_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gnsscorr_sdr_corr_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    @staticmethod
+    def init_chan(sv, acq_code_phase, acq_doppler, packets_since_acq=0.0) -> np.ndarray:
+        out = np.zeros(1, SDR_CHAN)
+        _check(lib().gnsscorr_sdr_init_chan(_ptr(out), int(sv), int(acq_code_phase),
+                                            int(acq_doppler), float(packets_since_acq)),
+               "gnsscorr_sdr_init_chan")
+        return out[0]
+
+    def accum_dev(self, d_packets, n_jobs, d_jobs, d_out):
+        _check(lib().gnsscorr_sdr_accum_dev(self.h, d_packets, n_jobs, d_jobs, d_out),
+               "gnsscorr_sdr_accum_dev")
+
+    def correlate(self, packets, states, corr, cb, user=None, rx=None):
+        """packets: (n, 2048, 2) int16; states SDR_CHAN[n_ch], corr SDR_CORR[n_ch] in place;
+        cb: a C function pointer (int) of gnsscorr_sdr_dump_fn type; user: pointer or None."""
+        pk = np.ascontiguousarray(packets, np.int16).reshape(-1, 2048, 2)
+        assert states.dtype == SDR_CHAN and corr.dtype == SDR_CORR
+        rxa = None if rx is None else np.ascontiguousarray(rx, np.int32)
+        _check(lib().gnsscorr_sdr_correlate(self.h, _ptr(pk), pk.shape[0], len(states),
+                                            None if rxa is None else _ptr(rxa), _ptr(states),
+                                            _ptr(corr), cb, user),
+               "gnsscorr_sdr_correlate")
+
+    def sync(self):
+        _check(lib().gnsscorr_sdr_corr_sync(self.h), "gnsscorr_sdr_corr_sync")
+
+    @property
+    def stream(self) -> int:
+        return lib().gnsscorr_sdr_corr_stream(self.h)
 
 
 # ---------------------------------------------------------------- legacy OSG view

@@ -352,6 +352,74 @@ int gnsscorr_sdr_acq_sync(gnsscorr_sdr_acq_ctx *ctx);
 void *gnsscorr_sdr_acq_stream(gnsscorr_sdr_acq_ctx *ctx);
 
 /* ======================================================================
+ * GPS-SDR tracking correlator ("sdr corr"), bit-exact with the real-time
+ * receiver's Correlator class (objects/correlator.cpp):
+ *   Correlator::Accum       :425-448  wipe-off (cmulsc >>14) + E/P/L prn_accum_new
+ *                            -> batched on the GPU (gnsscorr_sdr_accum_dev)
+ *   Correlator::Correlate   :160-237  the per-packet rollover / dump schedule
+ *   UpdateState / DumpAccum :369-525  fp64 NCO state, correlation rotation
+ *   InitCorrelator          :610-676
+ * Pre-sampled tables as in the constructor/SamplePRN (:63-98, :562-590):
+ * 3001 carrier rows (-IF - 10 Hz*k, |k| <= 1500) x 4096 CPX and 32 SVs x 101
+ * fractional-chip code rows x 4096 samples, resident in HBM.  The channel
+ * DLL/PLL (Channel::Accum) stays host code: a callback per dump.
+ * ==================================================================== */
+typedef struct gnsscorr_sdr_corr_ctx gnsscorr_sdr_corr_ctx;
+
+typedef struct {
+  int32_t device;
+  int32_t saturate;        /* 1: sse_cmulsc saturation; 0: x86_cmulsc wrap */
+} gnsscorr_sdr_corr_cfg;
+
+typedef struct {           /* Correlator_State_S (sdr_structs.h:141-168); the row
+                              pointers pcode[3]/psine become (bin, offset) pairs */
+  double   code_phase, carrier_phase, carrier_phase_prev, code_phase_mod, carrier_phase_mod;
+  double   code_nco, carrier_nco;
+  uint32_t chan, sv, navigate, active, count, scount;
+  uint32_t epoch_1ms, epoch_20ms, z_count, rollover;
+  uint32_t cbin[3], sbin;
+  int32_t  coff[3], soff;
+} gnsscorr_sdr_chan;       /* 128 bytes */
+
+typedef struct { int32_t i[3], q[3]; } gnsscorr_sdr_corr;        /* Correlation_S: E, P, L */
+
+typedef struct {           /* NCO_Command_S (sdr_structs.h:112-125) */
+  double   carrier_nco, code_nco;
+  uint32_t kill, reset_1ms, reset_20ms, set_z_count, z_count, length, navigate, pad;
+} gnsscorr_sdr_feedback;
+
+/* Channel::Accum stand-in: called at every dump with the rotated correlations;
+ * fills the feedback (the struct is zeroed before the call). */
+typedef void (*gnsscorr_sdr_dump_fn)(void *user, int ch, const gnsscorr_sdr_chan *s,
+                                     const gnsscorr_sdr_corr *c, gnsscorr_sdr_feedback *f);
+
+typedef struct {           /* one Correlator::Accum call */
+  int32_t packet, data_off, samps;  /* samples [data_off, data_off+samps) of packet   */
+  int32_t sv, sbin, soff;           /* carrier row sbin from offset soff              */
+  int32_t cbin[3], coff[3];         /* E, P, L code rows of sv from offsets coff[]    */
+} gnsscorr_sdr_accum_job;  /* 48 bytes */
+
+int gnsscorr_sdr_corr_create(gnsscorr_sdr_corr_ctx **out, const gnsscorr_sdr_corr_cfg *cfg);
+int gnsscorr_sdr_corr_destroy(gnsscorr_sdr_corr_ctx *ctx);
+/* InitCorrelator from an acquisition result (sv 0-based, code_phase in samples,
+ * doppler Hz) and the packets elapsed since the acquisition's buffer. */
+int gnsscorr_sdr_init_chan(gnsscorr_sdr_chan *s, int sv, int acq_code_phase, int acq_doppler,
+                           double packets_since_acq);
+/* Batched Accum: d_packets = n x 2048 CPX on the device; d_out[j] = the E,P,L
+ * sums of job j (int32, wrapping).  Asynchronous on the context stream. */
+int gnsscorr_sdr_accum_dev(gnsscorr_sdr_corr_ctx *ctx, const int16_t *d_packets, int n_jobs,
+                           const gnsscorr_sdr_accum_job *d_jobs, gnsscorr_sdr_corr *d_out);
+/* Correlator::Correlate for one packet per receiver: h_packets = n_packets x
+ * 2048 CPX (host), channel c reads packet h_rx[c] (NULL: all packet 0).
+ * states/corr: n_ch entries updated in place; cb runs on the calling thread at
+ * every dump, in channel order within each of the (at most 3) segment phases. */
+int gnsscorr_sdr_correlate(gnsscorr_sdr_corr_ctx *ctx, const int16_t *h_packets, int n_packets,
+                           int n_ch, const int32_t *h_rx, gnsscorr_sdr_chan *states,
+                           gnsscorr_sdr_corr *corr, gnsscorr_sdr_dump_fn cb, void *user);
+int gnsscorr_sdr_corr_sync(gnsscorr_sdr_corr_ctx *ctx);
+void *gnsscorr_sdr_corr_stream(gnsscorr_sdr_corr_ctx *ctx);
+
+/* ======================================================================
  * Device buffers / events (so hosts need no other GPU runtime)
  * ==================================================================== */
 int gnsscorr_dev_alloc(int device, size_t bytes, void **d_ptr);

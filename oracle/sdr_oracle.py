@@ -90,8 +90,9 @@ class OracleSDR:
         rows = self.prep_if(buff, fif, saturate)
         out = np.zeros(len(svs), RESULT)
         for k, sv in enumerate(svs):
-            r = self.L.sdro_acq_strong(_p(rows), _p(np.ascontiguousarray(codes[sv])), int(sv),
-                                       doppmin, doppmax, int(saturate))
+            code = np.ascontiguousarray(codes[sv], np.int16)
+            r = self.L.sdro_acq_strong(_p(rows), _p(code), int(sv), doppmin, doppmax,
+                                       int(saturate))
             out[k] = (r.sv, r.code_phase, r.doppler, r.magnitude, r.success, r.row)
         return out
 
@@ -116,6 +117,8 @@ class RefSDR:
         L.ref_sdr_cmag_max.argtypes = [P, I, P, P]
         L.ref_sdr_prn_codes.restype = C.POINTER(C.c_int16)
         L.ref_sdr_acq_strong.argtypes = [P, D, I, I, I, P]
+        L.ref_sdr_code_gen.argtypes = [I, P]
+        L.ref_sdr_accum.argtypes = [P, P, P, P, P, I, P]
         self.L = L
 
     def sine_gen(self, f, n=N, fs=FS):
@@ -141,6 +144,19 @@ class RefSDR:
         i, m = C.c_int32(), C.c_int32()
         self.L.ref_sdr_cmag_max(_p(a), a.shape[0], C.byref(i), C.byref(m))
         return i.value, m.value
+
+    def code_gen(self, sv):
+        out = np.zeros(1023, np.int16)
+        self.L.ref_sdr_code_gen(sv, _p(out))
+        return out
+
+    def accum(self, data, sine, e, p, l, samps):
+        out = np.zeros(6, np.int32)
+        keep = [np.ascontiguousarray(data, np.int16).copy(),
+                np.ascontiguousarray(sine, np.int16).copy()] + \
+            [np.ascontiguousarray(x, np.int8) for x in (e, p, l)]   # alive during the call
+        self.L.ref_sdr_accum(*[_p(k) for k in keep], samps, _p(out))
+        return out
 
     def prn_codes(self):
         p = self.L.ref_sdr_prn_codes()
@@ -188,3 +204,63 @@ def make_buffer(sigs, n=N, seed=1, amp_noise=2.0, fif=IF_SDR):
     out[:, 0] = np.clip(np.round(z.real), -127, 127)
     out[:, 1] = np.clip(np.round(z.imag), -127, 127)
     return out
+
+
+# ---------------------------------------------------------------- tracking correlator
+CHAN = np.dtype([("code_phase", "<f8"), ("carrier_phase", "<f8"), ("carrier_phase_prev", "<f8"),
+                 ("code_phase_mod", "<f8"), ("carrier_phase_mod", "<f8"), ("code_nco", "<f8"),
+                 ("carrier_nco", "<f8"), ("chan", "<u4"), ("sv", "<u4"), ("navigate", "<u4"),
+                 ("active", "<u4"), ("count", "<u4"), ("scount", "<u4"), ("epoch_1ms", "<u4"),
+                 ("epoch_20ms", "<u4"), ("z_count", "<u4"), ("rollover", "<u4"),
+                 ("cbin", "<u4", (3,)), ("sbin", "<u4"), ("coff", "<i4", (3,)), ("soff", "<i4")])
+CORR = np.dtype([("i", "<i4", (3,)), ("q", "<i4", (3,))])
+ROW, SBINS, CBINS = 4096, 3001, 101
+
+
+class OracleSdrCorr:
+    """Scalar restatement of the GPS-SDR Correlator (oracle/sdr_corr.c)."""
+
+    def __init__(self, saturate=False):
+        L = C.CDLL(ORACLE_SO)
+        P, I, D = C.c_void_p, C.c_int, C.c_double
+        L.sdrc_tables.argtypes = [P, P]
+        L.sdrc_code_gen.argtypes = [I, P]
+        L.sdrc_accum.argtypes = [P, P, P, P, P, I, I, P]
+        L.sdrc_correlate.argtypes = [P, P, I, P, P, I, P, P]
+        L.sdrc_init_chan.argtypes = [P, I, I, I, D]
+        self.L = L
+        self.saturate = int(saturate)
+        self.carrier = np.zeros((SBINS, ROW, 2), np.int16)
+        self.code = np.zeros((32, CBINS, ROW), np.int8)
+        L.sdrc_tables(_p(self.carrier), _p(self.code))
+        self._t = (C.c_void_p * 2)(self.carrier.ctypes.data, self.code.ctypes.data)
+        self.test_loop = C.cast(L.sdrc_test_loop, C.c_void_p).value
+
+    def code_gen(self, sv):
+        out = np.zeros(1023, np.uint8)
+        self.L.sdrc_code_gen(sv, _p(out))
+        return out
+
+    def accum(self, data, job):
+        """One Accum job over flat tables (SDR_JOB-like dict/record); returns CORR record."""
+        c = np.zeros(1, CORR)
+        sv, sb, so = int(job["sv"]), int(job["sbin"]), int(job["soff"])
+        flat_car = self.carrier.reshape(-1, 2)
+        flat_code = self.code.reshape(-1)
+        sine = np.ascontiguousarray(flat_car[sb * ROW + so:])
+        codes = [np.ascontiguousarray(flat_code[(sv * CBINS + int(job["cbin"][k])) * ROW +
+                                                int(job["coff"][k]):]) for k in range(3)]
+        d = np.ascontiguousarray(data[int(job["data_off"]):])
+        self.L.sdrc_accum(_p(d), _p(sine), _p(codes[0]), _p(codes[1]), _p(codes[2]),
+                          int(job["samps"]), self.saturate, _p(c))
+        return c[0]
+
+    def init_chan(self, sv, cp, dop, since=0.0):
+        s = np.zeros(1, CHAN)
+        self.L.sdrc_init_chan(_p(s), sv, cp, dop, since)
+        return s[0]
+
+    def correlate(self, packet, states, corr, cb=None, user=None):
+        packet = np.ascontiguousarray(packet, np.int16)
+        self.L.sdrc_correlate(C.byref(self._t), _p(packet), len(states), _p(states), _p(corr),
+                              self.saturate, cb if cb is not None else self.test_loop, user)

@@ -35,6 +35,41 @@ void ref_sdr_cmag_max(CPX* a, int n, int32* index, int32* mag)
 
 const int16* ref_sdr_prn_codes(void) { return PRN_Codes; }
 
+// code_gen (accessories/misc.cpp:28-87): out[k] = chip (0/1) of sv
+void ref_sdr_code_gen(int sv, int16* out)
+{
+  CPX tmp[1023];
+  code_gen(tmp, sv);
+  for (int k = 0; k < 1023; k++) out[k] = tmp[k].i;
+}
+
+// Correlator::Accum (correlator.cpp:425-448) over the x86 primitives: wipe-off
+// then prn_accum_new.  codes: +-1 per sample for E, P, L; out: E.i E.q P.i P.q L.i L.q
+void ref_sdr_accum(CPX* data, CPX* sine, const int8_t* e, const int8_t* p, const int8_t* l,
+                   int samps, int32* out)
+{
+  CPX* scratch = new CPX[samps > 0 ? samps : 1];
+  MIX* m[3];
+  const int8_t* src[3] = {e, p, l};
+  for (int j = 0; j < 3; j++) {
+    m[j] = new MIX[samps > 0 ? samps : 1];
+    for (int k = 0; k < samps; k++) {
+      const short v = src[j][k] > 0 ? 0x0001 : (short)0xffff;   // SamplePRN mapping
+      m[j][k].i = m[j][k].ni = v;
+      m[j][k].q = m[j][k].nq = 0;
+    }
+  }
+  x86_cmulsc(data, sine, scratch, samps, 14);
+  CPX_ACCUM epl[3];
+  x86_prn_accum_new(scratch, m[0], m[1], m[2], samps, epl);
+  for (int j = 0; j < 3; j++) {
+    out[2 * j] = epl[j].i;
+    out[2 * j + 1] = epl[j].q;
+    delete[] m[j];
+  }
+  delete[] scratch;
+}
+
 // out: sv, code_phase, doppler, magnitude, success, row
 void ref_sdr_acq_strong(const CPX* buff, double fif, int sv, int doppmin, int doppmax, int32* out)
 {

@@ -8,6 +8,10 @@ oracle ref), plus PRN_Codes from accessories/prn_codes.h.  Stored:
                       reference doPrepIF + doAcqStrong results for sv 0..31
   sdr_fft.npz         int16 FFT known answers (forward / inverse, rank masks,
                       incl. inputs large enough to exercise the int16 wrap)
+  sdr_corr.npz        tracking correlator: SHA-256 of the 3001 x 4096 carrier
+                      wipe-off table built with the reference sine_gen, the
+                      code_gen chips of sv 0..31, and Correlator::Accum known
+                      answers (x86_cmulsc + x86_prn_accum_new) on random jobs
 Usage:  python tests/golden/make_sdr_golden.py
 """
 import os
@@ -46,6 +50,26 @@ def main():
     fwd = np.stack([ref.fft(x, False, S.R1) for x in xs])
     inv = np.stack([ref.fft(x, True, S.R2) for x in xs])
     np.savez_compressed(os.path.join(out, "sdr_fft.npz"), x=xs, fwd_r1=fwd, inv_r2=inv)
+    # tracking correlator
+    import hashlib
+    car = np.stack([ref.sine_gen(np.float32(-38400.0) - np.float32(k) * np.float32(10.0), n=4096)
+                    for k in range(-1500, 1501)])
+    chips = np.stack([ref.code_gen(sv) for sv in range(32)]).astype(np.uint8)
+    o = S.OracleSdrCorr()
+    jobs, data, exp = [], [], []
+    for it in range(48):
+        amp = (3, 300, 32767)[it % 3]
+        d = rng.integers(-amp, amp + 1, (2048, 2)).astype(np.int16)
+        sb, so, n = int(rng.integers(0, 3001)), int(rng.integers(0, 2048)), int(rng.integers(0, 2049))
+        sv, cb, co = int(rng.integers(0, 32)), rng.integers(0, 101, 3), rng.integers(0, 2048, 3)
+        codes = [o.code[sv, cb[k], co[k]:co[k] + n] for k in range(3)]
+        exp.append(ref.accum(d, car[sb, so:so + n], codes[0], codes[1], codes[2], n))
+        jobs.append([0, 0, n, sv, sb, so, *cb, *co])
+        data.append(d)
+    np.savez_compressed(os.path.join(out, "sdr_corr.npz"),
+                        carrier_sha256=np.array(hashlib.sha256(car.tobytes()).hexdigest()),
+                        chips=chips, jobs=np.array(jobs, np.int32), data=np.stack(data),
+                        expected=np.stack(exp))
     for k, r in enumerate(res):
         print("scene", k, [(int(v["sv"]) + 1, int(v["code_phase"]), int(v["doppler"]),
                             int(v["magnitude"])) for v in r if v["magnitude"] > 0][:3])

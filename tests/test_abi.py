@@ -17,6 +17,8 @@ def _declared():
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", txt, flags=re.M):
             name = m.group(1)
+            if m.group(0).startswith("typedef"):
+                continue                 # function-pointer typedefs are types, not symbols
             if name not in ("defined",):
                 funcs.add(name)
         for m in re.finditer(r"^extern\s+(?:int|double|long)\s+([^;(]+);", txt, flags=re.M):
