@@ -9,6 +9,9 @@ export TMPDIR=/tmp
 echo "== pytest -m gpu"
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1
 tail -3 $O/pytest.log
+echo "== smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -1 $O/smoke.log
 echo "== bench"
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 cat $O/bench.json
