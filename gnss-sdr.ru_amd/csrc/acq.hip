@@ -202,20 +202,52 @@ __device__ __forceinline__ int in_index(int p) {  // Ruritanian input map n(p)
 // buffer load per plane a (scalar plane offset a*8 KiB, 32-bit lane offset),
 // forms D = conj(X) * F, runs both DFT16s in registers and writes LDS once.
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Frequency bins on the fs/N grid share one spectrum: X_f[k] = X_f0[k - m]
+// for f = f0 + m*fs/N (exact circular shift).  In prime-factor coordinates a
+// shift by m subtracts (15m mod 16, 2m mod 3, 4m mod 11, m mod 31) from the
+// (a, b, c, d) of every position, so the X read below is still one plane per
+// a and an (almost always) contiguous pair of groups.
+struct Shift { int a, b, c, d; };
+
+__device__ __forceinline__ int shift_group(int g, const Shift& s) {
+  const int d = g % 31, bc = g / 31, c = bc % 11, b = bc / 11;
+  int b2 = b - s.b, c2 = c - s.c, d2 = d - s.d;
+  b2 += b2 < 0 ? 3 : 0;
+  c2 += c2 < 0 ? 11 : 0;
+  d2 += d2 < 0 ? 31 : 0;
+  return (b2 * 11 + c2) * 31 + d2;
+}
+
 __device__ __forceinline__ void load_mul_pass16(const float2* __restrict__ Xb,
                                                 const float2* __restrict__ Fc, float2* lds,
-                                                int t) {
+                                                int t, const Shift& sh) {
   const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, 0, NPAD * 8, 0x00020000);
   const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)Fc, 0, NPAD * 8, 0x00020000);
   const int g0 = 2 * t;
   const int voff = g0 * 8;
   float2 x0[16], x1[16];
+  if (sh.a == 0 && sh.b == 0 && sh.c == 0 && sh.d == 0) {   // uniform branch
 #pragma unroll
-  for (int a = 0; a < 16; a++) {
-    const f4v u = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, a * kPlane * 8, 0));
-    const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
-    x0[a] = make_float2(u.x * f.x + u.y * f.y, u.x * f.y - u.y * f.x);
-    x1[a] = make_float2(u.z * f.z + u.w * f.w, u.z * f.w - u.w * f.z);
+    for (int a = 0; a < 16; a++) {
+      const f4v u = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, a * kPlane * 8, 0));
+      const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
+      x0[a] = make_float2(u.x * f.x + u.y * f.y, u.x * f.y - u.y * f.x);
+      x1[a] = make_float2(u.z * f.z + u.w * f.w, u.z * f.w - u.w * f.z);
+    }
+  } else {
+    const int v0 = shift_group(g0 < M16 ? g0 : 0, sh) * 8;
+    const int v1 = shift_group(g0 + 1 < M16 ? g0 + 1 : 0, sh) * 8;
+#pragma unroll
+    for (int a = 0; a < 16; a++) {
+      const int pa = ((a - sh.a) & 15) * kPlane * 8;
+      const f2v u0 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v0, pa, 0));
+      const f2v u1 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v1, pa, 0));
+      const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
+      x0[a] = make_float2(u0.x * f.x + u0.y * f.y, u0.x * f.y - u0.y * f.x);
+      x1[a] = make_float2(u1.x * f.z + u1.y * f.w, u1.x * f.w - u1.y * f.z);
+    }
   }
   dft16(x0);
   dft16(x1);
@@ -286,14 +318,16 @@ __device__ __forceinline__ int out_base(int t) {
 constexpr int kFwd1Threads = 256;
 __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
     const int8_t* __restrict__ src, int iq, int n_blocks, const double* __restrict__ freqs,
-    double ts, int mode, float2* __restrict__ stage) {
+    double ts, int mode, float2* __restrict__ stage, const double* __restrict__ cfreqs,
+    const int* __restrict__ n_rows_dev) {
   const int row = blockIdx.x >> 2;
   const int g = (blockIdx.x & 3) * kFwd1Threads + threadIdx.x;
   if (g >= M16) return;
+  if (n_rows_dev && row >= *n_rows_dev * n_blocks) return;   // only the spectrum classes
   float2 x[16];
   if (mode == 0) {
-    const int fid = row / n_blocks, blk = row % n_blocks;
-    const double f = freqs[fid];
+    const int cls = row / n_blocks, blk = row % n_blocks;
+    const double f = cfreqs[cls];
     const int8_t* s = src + (long)blk * N * (iq ? 2 : 1);
 #pragma unroll
     for (int a = 0; a < 16; a++) {
@@ -319,9 +353,11 @@ __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
 
 __global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restrict__ stage,
                                                         const int* __restrict__ sigma,
-                                                        float2* __restrict__ out) {
+                                                        float2* __restrict__ out, int n_blocks,
+                                                        const int* __restrict__ n_rows_dev) {
   __shared__ float2 sub[M16 + 1];
   const int row = blockIdx.x >> 4, a = blockIdx.x & 15;
+  if (n_rows_dev && row >= *n_rows_dev * n_blocks) return;
   const int lane = threadIdx.x;
   const float2* in = stage + (long)row * NPAD + a * kPlane;
   for (int i = lane; i < M16; i += 64) sub[i] = in[i];
@@ -351,6 +387,58 @@ __global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restric
     const int p0 = a * M16 + lane * 31;
 #pragma unroll
     for (int d = 0; d < 31; d++) o[sigma[p0 + d]] = x[d];
+  }
+}
+
+// Spectrum classes: frequencies with the same residue r = f mod fs/N share one
+// forward spectrum, computed AT r; bin f = r + m*fs/N reads it circularly
+// shifted by m (exact identity: exp(i 2 pi m n / N) modulation).  The class
+// spectrum depends on r alone, so results do not depend on which other
+// frequencies are in the list (sharding / ordering invariant).
+// fmap[i] = {class, 15m mod 16, 2m mod 3, (4m mod 11) * 32 + m mod 31};
+// cfreq[class] = r.
+__device__ __forceinline__ double grid_residue(double f, double delta) {
+  double r = fmod(f, delta);
+  return r < 0 ? r + delta : r;
+}
+
+__global__ __launch_bounds__(1024) void acq_classify_kernel(const double* __restrict__ freqs,
+                                                            int n, double delta,
+                                                            int4* __restrict__ fmap,
+                                                            double* __restrict__ cfreq,
+                                                            int* __restrict__ n_classes) {
+  // pass 1: leader = first j with the same residue; shift m = (f - r) / delta
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double f = freqs[i], r = grid_residue(f, delta);
+    int l = i;
+    for (int j = 0; j < i; j++)
+      if (grid_residue(freqs[j], delta) == r) { l = j; break; }
+    const double q = rint((f - r) / delta);
+    fmap[i] = make_int4(l, fabs(q) < 1e8 ? (int)q : 0, 0, 0);
+  }
+  __syncthreads();
+  // pass 2: class id = number of leaders before the leader
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int4 v = fmap[i];
+    int cls = 0;
+    for (int k = 0; k < v.x; k++) cls += fmap[k].x == k;
+    int mN = v.y % N;
+    mN += mN < 0 ? N : 0;
+    fmap[i].z = cls;
+    fmap[i].w = mN;
+  }
+  if (threadIdx.x == 0) {
+    int cnt = 0;
+    for (int k = 0; k < n; k++) cnt += fmap[k].x == k;
+    *n_classes = cnt;
+  }
+  __syncthreads();
+  // pass 3: class frequencies and the packed shift coordinates
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int4 v = fmap[i];
+    if (v.x == i) cfreq[v.z] = grid_residue(freqs[i], delta);
+    const int mN = v.w;
+    fmap[i] = make_int4(v.z, (15 * mN) & 15, (2 * mN) % 3, ((4 * mN) % 11) * 32 + mN % 31);
   }
 }
 
@@ -408,7 +496,7 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
     const float2* __restrict__ X, const float2* __restrict__ F, int n_blocks,
     const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins,
     int spc, gnsscorr_acq_row* __restrict__ stats, float* __restrict__ dump_power,
-    int dump_block, const int* __restrict__ order) {
+    int dump_block, const int* __restrict__ order, const int4* __restrict__ fmap) {
   __shared__ float2 lds[N];
   __shared__ float2 tw[32];
   __shared__ PeakSlot s_pk[kThreads / 64];
@@ -422,6 +510,8 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
   const int g = rowid / n_bins, bin = rowid % n_bins;
   const int code = group_code[g];
   const int fid = group_freq[g * n_bins + bin];
+  const int4 fm = fmap[fid];
+  const Shift sh{fm.y, fm.z, fm.w >> 5, fm.w & 31};
   const int t = threadIdx.x;
   const float inv_n2 = 1.0f / ((float)N * (float)N);
   const bool extra = t < kLeft * 31;
@@ -440,10 +530,10 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
   const float2* Fc = F + (long)code * NPAD;
   for (int i = 0; i < nblk; i++) {
     const int blk = blk0 + i;
-    const float2* Xb = X + ((long)fid * n_blocks + blk) * NPAD;
+    const float2* Xb = X + ((long)fm.x * n_blocks + blk) * NPAD;
     ACQ_STAMP(i * 6 + 0);
     // D = conj(X) * F  (= conj(X * conj(F)), acquisition.sci:116), then radix-16
-    load_mul_pass16(Xb, Fc, lds, t);
+    load_mul_pass16(Xb, Fc, lds, t, sh);
     __syncthreads();
     ACQ_STAMP(i * 6 + 1);
     pass33(lds, t);
@@ -613,6 +703,9 @@ struct gnsscorr_acq_ctx {
   int* d_order = nullptr;               // workgroup -> work-unit permutation (XCD tiles)
   int order_groups = 0, order_bins = 0, order_units = 0;
   size_t cap_order = 0;
+  int4* d_fmap = nullptr;               // per frequency: spectrum class + shift coordinates
+  double* d_cfreq = nullptr;            // per class: the residue frequency whose spectrum is computed
+  int* d_nclass = nullptr;
   float2* d_stage = nullptr;            // forward-FFT staging rows
   size_t cap_stage = 0;
   gnsscorr_acq_row* d_stats = nullptr;  // per (row, block) statistics
@@ -630,7 +723,8 @@ struct gnsscorr_acq_ctx {
 };
 
 static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
-                          const double* d_freqs, int mode, int n_rows, float2* dst);
+                          const double* d_freqs, int mode, int n_rows, float2* dst,
+                          const double* d_cfreq, const int* d_nrows);
 
 static int grow(void** p, size_t* cap, size_t need, size_t elem) {
   if (need <= *cap) return GNSSCORR_OK;
@@ -684,7 +778,10 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
       hipMemset(c->d_F, 0, sizeof(float2) * NPAD * (size_t)cfg->max_codes) != hipSuccess ||
       hipMemset(c->d_X, 0, sizeof(float2) * NPAD * (size_t)cfg->max_freqs * cfg->max_blocks) != hipSuccess ||
       hipMalloc(&c->d_if, (size_t)N * 2 * cfg->max_blocks) != hipSuccess ||
-      hipMalloc(&c->d_freqs, sizeof(double) * cfg->max_freqs) != hipSuccess) {
+      hipMalloc(&c->d_freqs, sizeof(double) * cfg->max_freqs) != hipSuccess ||
+      hipMalloc(&c->d_fmap, sizeof(int4) * cfg->max_freqs) != hipSuccess ||
+      hipMalloc(&c->d_cfreq, sizeof(double) * cfg->max_freqs) != hipSuccess ||
+      hipMalloc(&c->d_nclass, sizeof(int)) != hipSuccess) {
     gnsscorr_set_error("gnsscorr_acq_create: device allocation failed");
     return fail(GNSSCORR_ENOMEM);
   }
@@ -713,7 +810,8 @@ extern "C" int gnsscorr_acq_destroy(gnsscorr_acq_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_sigma, c->d_F, c->d_X, c->d_if, c->d_freqs, c->d_gcode, c->d_gfreq,
-                  c->d_rows, c->d_res, c->d_dump, c->d_order, c->d_stage, c->d_stats};
+                  c->d_rows, c->d_res, c->d_dump, c->d_order, c->d_stage, c->d_stats,
+                  c->d_fmap, c->d_cfreq, c->d_nclass};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -731,7 +829,7 @@ extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const in
   int8_t* d = nullptr;
   HIP_TRY(hipMalloc(&d, (size_t)n_codes * N));
   HIP_TRY(hipMemcpyAsync(d, h_codes, (size_t)n_codes * N, hipMemcpyHostToDevice, c->stream));
-  int rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F);
+  int rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F, nullptr, nullptr);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipFree(d));
@@ -787,14 +885,16 @@ static int ensure_order(gnsscorr_acq_ctx* c, int n_groups, int n_bins, int units
 
 // forward transform of n_rows rows into dst (padded correlation layout)
 static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
-                          const double* d_freqs, int mode, int n_rows, float2* dst) {
+                          const double* d_freqs, int mode, int n_rows, float2* dst,
+                          const double* d_cfreq, const int* d_nrows) {
   int rc = grow((void**)&c->d_stage, &c->cap_stage, (size_t)n_rows * NPAD, sizeof(float2));
   if (rc) return rc;
   hipLaunchKernelGGL(acq_fwd16_kernel, dim3(n_rows * 4), dim3(kFwd1Threads), 0, c->stream, src, iq,
-                     n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, mode, c->d_stage);
+                     n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, mode, c->d_stage, d_cfreq,
+                     d_nrows);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(acq_fwd1023_kernel, dim3(n_rows * 16), dim3(64), 0, c->stream, c->d_stage,
-                     c->d_sigma, dst);
+                     c->d_sigma, dst, n_blocks, d_nrows);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
@@ -814,7 +914,12 @@ static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n
                           int n_freqs, const double* d_freqs) {
   int rc = check_search(c, n_blocks, n_freqs, GNSSCORR_ACQ_BEST_OF_BLOCKS);
   if (rc) return rc;
-  rc = forward_launch(c, d_if, iq, n_blocks, d_freqs, 0, n_freqs * n_blocks, c->d_X);
+  // spectrum classes on the fs/N grid (one forward FFT per class and block)
+  hipLaunchKernelGGL(acq_classify_kernel, dim3(1), dim3(1024), 0, c->stream, d_freqs, n_freqs,
+                     c->cfg.samp_rate / N, c->d_fmap, c->d_cfreq, c->d_nclass);
+  HIP_TRY(hipGetLastError());
+  rc = forward_launch(c, d_if, iq, n_blocks, d_freqs, 0, n_freqs * n_blocks, c->d_X, c->d_cfreq,
+                      c->d_nclass);
   if (rc) return rc;
   c->spec_blocks = n_blocks;
   c->spec_freqs = n_freqs;
@@ -842,7 +947,7 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
 #define ACQ_CORR_LAUNCH(M, D)                                                                \
   hipLaunchKernelGGL((acq_corr_kernel<M, D>), dim3(n_units), dim3(kThreads), 0, c->stream,    \
                      c->d_X, c->d_F, n_blocks, d_gcode, d_gfreq, n_bins, spc, c->d_stats,      \
-                     d_dump, dump_block, c->d_order)
+                     d_dump, dump_block, c->d_order, c->d_fmap)
   if (d_dump)
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
   else if (mode == GNSSCORR_ACQ_NONCOHERENT)
