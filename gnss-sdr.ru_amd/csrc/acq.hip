@@ -70,20 +70,34 @@ constexpr float kCos16[16] = {1.0f, 9.238795325e-01f, 7.071067812e-01f, 3.826834
 constexpr float kSin16[16] = {0.0f, 3.826834324e-01f, 7.071067812e-01f, 9.238795325e-01f, 1.0f, 9.238795325e-01f, 7.071067812e-01f, 3.826834324e-01f, 0.0f, -3.826834324e-01f, -7.071067812e-01f, -9.238795325e-01f, -1.0f, -9.238795325e-01f, -7.071067812e-01f, -3.826834324e-01f};
 constexpr float kSqrt3_2 = 8.660254038e-01f;
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// Complex values live in packed fp32 pairs (v2f): gfx950 executes v_pk_fma_f32 /
+// v_pk_add_f32 on both halves in one instruction, and re/im swaps and sign
+// flips fold into the op_sel / neg modifiers, so the DFTs below are written
+// with explicit swaps instead of scalar re/im arithmetic.
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f swp(v2f v) { return __builtin_shufflevector(v, v, 1, 0); }
+__device__ __forceinline__ v2f bc(float c) { return (v2f){c, c}; }
+// -i v = (v.y, -v.x)
+__device__ __forceinline__ v2f mul_mi(v2f v) { return swp(v) * (v2f){1.f, -1.f}; }
+// v * (c + i s) for constants c, s
+__device__ __forceinline__ v2f cmulc(v2f v, float c, float s) {
+  return v * bc(c) + swp(v) * (v2f){-s, s};
+}
+__device__ __forceinline__ v2f ld2(const float2& f) { return (v2f){f.x, f.y}; }
+__device__ __forceinline__ float2 st2(v2f v) { return make_float2(v.x, v.y); }
 
 // ---- small forward DFTs (W = exp(-2 pi i / P)) --------------------------------
-__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d) {
-  const float2 t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = csub(b, d);
-  a = cadd(t0, t2);
-  c = csub(t0, t2);
-  b = make_float2(t1.x + t3.y, t1.y - t3.x);  // t1 - i t3
-  d = make_float2(t1.x - t3.y, t1.y + t3.x);  // t1 + i t3
+__device__ __forceinline__ void dft4(v2f& a, v2f& b, v2f& c, v2f& d) {
+  const v2f t0 = a + c, t1 = a - c, t2 = b + d, t3 = b - d;
+  a = t0 + t2;
+  c = t0 - t2;
+  const v2f s3 = swp(t3);
+  b = __builtin_elementwise_fma(s3, (v2f){1.f, -1.f}, t1);   // t1 - i t3
+  d = __builtin_elementwise_fma(s3, (v2f){-1.f, 1.f}, t1);   // t1 + i t3
 }
 
 // In place: on return x[k] = X[k].
-__device__ __forceinline__ void dft16(float2 (&x)[16]) {
+__device__ __forceinline__ void dft16(v2f (&x)[16]) {
 #pragma unroll
   for (int n2 = 0; n2 < 4; n2++) dft4(x[n2], x[4 + n2], x[8 + n2], x[12 + n2]);
 #pragma unroll
@@ -91,14 +105,12 @@ __device__ __forceinline__ void dft16(float2 (&x)[16]) {
 #pragma unroll
     for (int n2 = 1; n2 < 4; n2++) {
       const int m = n2 * k1;
-      const float c = kCos16[m], s = -kSin16[m];
-      const float2 v = x[4 * k1 + n2];
-      x[4 * k1 + n2] = make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+      x[4 * k1 + n2] = cmulc(x[4 * k1 + n2], kCos16[m], -kSin16[m]);
     }
 #pragma unroll
   for (int k1 = 0; k1 < 4; k1++) dft4(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3]);
-  // X[k1 + 4 k2] sits in slot 4 k1 + k2: transpose the 4x4 block
-  float2 y[16];
+  // X[k1 + 4 k2] sits in slot 4 k1 + k2: transpose the 4x4 block (register renaming)
+  v2f y[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) y[i] = x[i];
 #pragma unroll
@@ -107,12 +119,13 @@ __device__ __forceinline__ void dft16(float2 (&x)[16]) {
     for (int k2 = 0; k2 < 4; k2++) x[k1 + 4 * k2] = y[4 * k1 + k2];
 }
 
-__device__ __forceinline__ void dft3(float2& x0, float2& x1, float2& x2) {
-  const float2 s = cadd(x1, x2), d = csub(x1, x2);
-  const float2 t = make_float2(x0.x - 0.5f * s.x, x0.y - 0.5f * s.y);
-  x0 = cadd(x0, s);
-  x1 = make_float2(t.x + kSqrt3_2 * d.y, t.y - kSqrt3_2 * d.x);
-  x2 = make_float2(t.x - kSqrt3_2 * d.y, t.y + kSqrt3_2 * d.x);
+__device__ __forceinline__ void dft3(v2f& x0, v2f& x1, v2f& x2) {
+  const v2f s = x1 + x2, d = x1 - x2;
+  const v2f t = x0 - bc(0.5f) * s;
+  x0 = x0 + s;
+  const v2f sd = swp(d);   // -/+ i sqrt(3)/2 (x1 - x2)
+  x1 = __builtin_elementwise_fma(sd, (v2f){kSqrt3_2, -kSqrt3_2}, t);
+  x2 = __builtin_elementwise_fma(sd, (v2f){-kSqrt3_2, kSqrt3_2}, t);
 }
 
 template <int P>
@@ -123,67 +136,31 @@ __device__ __forceinline__ float stab(int k) { return P == 11 ? kSin11[k] : kSin
 // Symmetric prime-length DFT: X_m = A_m - i B_m, X_{P-m} = A_m + i B_m with
 // A_m = x0 + sum_j cos(2 pi jm/P)(x_j + x_{P-j}), B_m = sum_j sin(..)(x_j - x_{P-j}).
 template <int P>
-__device__ __forceinline__ void dftp(float2 (&x)[P]) {
+__device__ __forceinline__ void dftp(v2f (&x)[P]) {
   constexpr int H = (P - 1) / 2;
-  float2 s[H + 1], d[H + 1];
+  v2f s[H + 1], d[H + 1];
 #pragma unroll
   for (int j = 1; j <= H; j++) {
-    s[j] = cadd(x[j], x[P - j]);
-    d[j] = csub(x[j], x[P - j]);
+    s[j] = x[j] + x[P - j];
+    d[j] = x[j] - x[P - j];
   }
-  const float2 x0 = x[0];
-  float2 X0 = x0;
+  const v2f x0 = x[0];
+  v2f X0 = x0;
 #pragma unroll
-  for (int j = 1; j <= H; j++) X0 = cadd(X0, s[j]);
+  for (int j = 1; j <= H; j++) X0 += s[j];
   x[0] = X0;
 #pragma unroll
   for (int m = 1; m <= H; m++) {
-    float ar = x0.x, ai = x0.y, br = 0.f, bi = 0.f;
+    v2f A = x0, B = (v2f){0.f, 0.f};
 #pragma unroll
     for (int j = 1; j <= H; j++) {
       const int q = (j * m) % P;
-      const float c = ctab<P>(q), sn = stab<P>(q);
-      ar = fmaf(c, s[j].x, ar);
-      ai = fmaf(c, s[j].y, ai);
-      br = fmaf(sn, d[j].x, br);
-      bi = fmaf(sn, d[j].y, bi);
+      A += bc(ctab<P>(q)) * s[j];
+      B += bc(stab<P>(q)) * d[j];
     }
-    x[m] = make_float2(ar + bi, ai - br);
-    x[P - m] = make_float2(ar - bi, ai + br);
-  }
-}
-
-// Same DFT, but only |X_m|^2 * scale is produced (final pass of the
-// correlation kernel): halves the live registers of the output side.
-template <int P>
-__device__ __forceinline__ void dftp_power(const float2 (&x)[P], float scale, float (&pw)[P]) {
-  constexpr int H = (P - 1) / 2;
-  float2 s[H + 1], d[H + 1];
-#pragma unroll
-  for (int j = 1; j <= H; j++) {
-    s[j] = cadd(x[j], x[P - j]);
-    d[j] = csub(x[j], x[P - j]);
-  }
-  const float2 x0 = x[0];
-  float2 X0 = x0;
-#pragma unroll
-  for (int j = 1; j <= H; j++) X0 = cadd(X0, s[j]);
-  pw[0] = (X0.x * X0.x + X0.y * X0.y) * scale;
-#pragma unroll
-  for (int m = 1; m <= H; m++) {
-    float ar = x0.x, ai = x0.y, br = 0.f, bi = 0.f;
-#pragma unroll
-    for (int j = 1; j <= H; j++) {
-      const int q = (j * m) % P;
-      const float c = ctab<P>(q), sn = stab<P>(q);
-      ar = fmaf(c, s[j].x, ar);
-      ai = fmaf(c, s[j].y, ai);
-      br = fmaf(sn, d[j].x, br);
-      bi = fmaf(sn, d[j].y, bi);
-    }
-    const float r1 = ar + bi, i1 = ai - br, r2 = ar - bi, i2 = ai + br;
-    pw[m] = (r1 * r1 + i1 * i1) * scale;
-    pw[P - m] = (r2 * r2 + i2 * i2) * scale;
+    const v2f sb = swp(B);
+    x[m] = __builtin_elementwise_fma(sb, (v2f){1.f, -1.f}, A);        // A - i B
+    x[P - m] = __builtin_elementwise_fma(sb, (v2f){-1.f, 1.f}, A);    // A + i B
   }
 }
 
@@ -227,14 +204,16 @@ __device__ __forceinline__ void load_mul_pass16(const float2* __restrict__ Xb,
   const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)Fc, 0, NPAD * 8, 0x00020000);
   const int g0 = 2 * t;
   const int voff = g0 * 8;
-  float2 x0[16], x1[16];
+  v2f x0[16], x1[16];
   if (sh.a == 0 && sh.b == 0 && sh.c == 0 && sh.d == 0) {   // uniform branch
 #pragma unroll
     for (int a = 0; a < 16; a++) {
       const f4v u = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, a * kPlane * 8, 0));
       const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
-      x0[a] = make_float2(u.x * f.x + u.y * f.y, u.x * f.y - u.y * f.x);
-      x1[a] = make_float2(u.z * f.z + u.w * f.w, u.z * f.w - u.w * f.z);
+      // conj(u) * f = u.re * f + u.im * (f.im, -f.re)
+      const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
+      x0[a] = bc(u.x) * f0 + bc(u.y) * mul_mi(f0);
+      x1[a] = bc(u.z) * f1 + bc(u.w) * mul_mi(f1);
     }
   } else {
     const int v0 = shift_group(g0 < M16 ? g0 : 0, sh) * 8;
@@ -245,8 +224,9 @@ __device__ __forceinline__ void load_mul_pass16(const float2* __restrict__ Xb,
       const f2v u0 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v0, pa, 0));
       const f2v u1 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v1, pa, 0));
       const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
-      x0[a] = make_float2(u0.x * f.x + u0.y * f.y, u0.x * f.y - u0.y * f.x);
-      x1[a] = make_float2(u1.x * f.z + u1.y * f.w, u1.x * f.w - u1.y * f.z);
+      const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
+      x0[a] = bc(u0.x) * f0 + bc(u0.y) * mul_mi(f0);
+      x1[a] = bc(u1.x) * f1 + bc(u1.y) * mul_mi(f1);
     }
   }
   dft16(x0);
@@ -254,8 +234,8 @@ __device__ __forceinline__ void load_mul_pass16(const float2* __restrict__ Xb,
   const bool two = g0 + 1 < M16;
 #pragma unroll
   for (int a = 0; a < 16; a++) {
-    lds[a * M16 + g0] = x0[a];
-    if (two) lds[a * M16 + g0 + 1] = x1[a];
+    lds[a * M16 + g0] = st2(x0[a]);
+    if (two) lds[a * M16 + g0 + 1] = st2(x1[a]);
   }
 }
 
@@ -263,11 +243,11 @@ __device__ __forceinline__ void pass33(float2* lds, int t) {
   if (t >= 16 * 31) return;
   const int a = t / 31, d = t % 31;
   float2* base = lds + a * M16 + d;
-  float2 v[3][11];
+  v2f v[3][11];
 #pragma unroll
   for (int b = 0; b < 3; b++)
 #pragma unroll
-    for (int c = 0; c < 11; c++) v[b][c] = base[(b * 11 + c) * 31];
+    for (int c = 0; c < 11; c++) v[b][c] = ld2(base[(b * 11 + c) * 31]);
 #pragma unroll
   for (int c = 0; c < 11; c++) dft3(v[0][c], v[1][c], v[2][c]);
 #pragma unroll
@@ -275,7 +255,7 @@ __device__ __forceinline__ void pass33(float2* lds, int t) {
 #pragma unroll
   for (int b = 0; b < 3; b++)
 #pragma unroll
-    for (int c = 0; c < 11; c++) base[(b * 11 + c) * 31] = v[b][c];
+    for (int c = 0; c < 11; c++) base[(b * 11 + c) * 31] = st2(v[b][c]);
 }
 
 // dim-31 pass, leftover groups 512..527: thread t < 496 computes output m of
@@ -324,7 +304,7 @@ __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
   const int g = (blockIdx.x & 3) * kFwd1Threads + threadIdx.x;
   if (g >= M16) return;
   if (n_rows_dev && row >= *n_rows_dev * n_blocks) return;   // only the spectrum classes
-  float2 x[16];
+  v2f x[16];
   if (mode == 0) {
     const int cls = row / n_blocks, blk = row % n_blocks;
     const double f = cfreqs[cls];
@@ -338,17 +318,17 @@ __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
       const double th = f * ((((double)n * 2.0) * M_PI) * ts);
       double sn, cs;
       sincos(th, &sn, &cs);
-      x[a] = make_float2((float)(I * cs - Q * sn), (float)(I * sn + Q * cs));
+      x[a] = (v2f){(float)(I * cs - Q * sn), (float)(I * sn + Q * cs)};
     }
   } else {
     const int8_t* s = src + (long)row * N;
 #pragma unroll
-    for (int a = 0; a < 16; a++) x[a] = make_float2((float)s[in_index(a * M16 + g)], 0.f);
+    for (int a = 0; a < 16; a++) x[a] = (v2f){(float)s[in_index(a * M16 + g)], 0.f};
   }
   dft16(x);
   float2* o = stage + (long)row * NPAD + g;
 #pragma unroll
-  for (int a = 0; a < 16; a++) o[a * kPlane] = x[a];
+  for (int a = 0; a < 16; a++) o[a * kPlane] = st2(x[a]);
 }
 
 __global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restrict__ stage,
@@ -363,11 +343,11 @@ __global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restric
   for (int i = lane; i < M16; i += 64) sub[i] = in[i];
   __syncthreads();
   if (lane < 31) {  // 3 x 11 over (b, c) for fixed d = lane
-    float2 v[3][11];
+    v2f v[3][11];
 #pragma unroll
     for (int b = 0; b < 3; b++)
 #pragma unroll
-      for (int c = 0; c < 11; c++) v[b][c] = sub[(b * 11 + c) * 31 + lane];
+      for (int c = 0; c < 11; c++) v[b][c] = ld2(sub[(b * 11 + c) * 31 + lane]);
 #pragma unroll
     for (int c = 0; c < 11; c++) dft3(v[0][c], v[1][c], v[2][c]);
 #pragma unroll
@@ -375,18 +355,18 @@ __global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restric
 #pragma unroll
     for (int b = 0; b < 3; b++)
 #pragma unroll
-      for (int c = 0; c < 11; c++) sub[(b * 11 + c) * 31 + lane] = v[b][c];
+      for (int c = 0; c < 11; c++) sub[(b * 11 + c) * 31 + lane] = st2(v[b][c]);
   }
   __syncthreads();
   if (lane < 33) {  // radix 31 over d for fixed (b, c) = lane
-    float2 x[31];
+    v2f x[31];
 #pragma unroll
-    for (int d = 0; d < 31; d++) x[d] = sub[lane * 31 + d];
+    for (int d = 0; d < 31; d++) x[d] = ld2(sub[lane * 31 + d]);
     dftp<31>(x);
     float2* o = out + (long)row * NPAD;
     const int p0 = a * M16 + lane * 31;
 #pragma unroll
-    for (int d = 0; d < 31; d++) o[sigma[p0 + d]] = x[d];
+    for (int d = 0; d < 31; d++) o[sigma[p0 + d]] = st2(x[d]);
   }
 }
 
@@ -543,9 +523,9 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
     {
       const float2 y = extra ? dft31_single(lds, tw, t) : make_float2(0.f, 0.f);
       pw[31] = extra ? (y.x * y.x + y.y * y.y) * inv_n2 : -1.f;
-      float2 x[31];
+      v2f x[31];
 #pragma unroll
-      for (int d = 0; d < 31; d++) x[d] = lds[t * 31 + d];
+      for (int d = 0; d < 31; d++) x[d] = ld2(lds[t * 31 + d]);
       dftp<31>(x);
 #pragma unroll
       for (int d = 0; d < 31; d++) pw[d] = (x[d].x * x[d].x + x[d].y * x[d].y) * inv_n2;
