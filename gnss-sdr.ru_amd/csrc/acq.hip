@@ -44,6 +44,11 @@
 
 // Diagnostic hook: tools/acq_stamps.hip defines ACQ_STAMP(i) to record
 // s_memtime at phase boundaries; in the library it compiles to nothing.
+// tools/acq_ablate.hip sets ACQ_SKIP to time the kernel with phases removed
+// (1: no 3x11 pass, 2: no radix-31 pass, 4: no row statistics); 0 in the library.
+#ifndef ACQ_SKIP
+#define ACQ_SKIP 0
+#endif
 #ifndef ACQ_STAMP
 #define ACQ_STAMP(i)
 #endif
@@ -516,11 +521,14 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
     load_mul_pass16(Xb, Fc, lds, t, sh);
     __syncthreads();
     ACQ_STAMP(i * 6 + 1);
-    pass33(lds, t);
+    if (!(ACQ_SKIP & 1)) pass33(lds, t);
     __syncthreads();
     ACQ_STAMP(i * 6 + 2);
     float pw[32];  // pw[31] = this thread's leftover output (or -1)
-    {
+    if (ACQ_SKIP & 2) {
+#pragma unroll
+      for (int d = 0; d < 32; d++) pw[d] = lds[(t * 31 + d) % N].x;
+    } else {
       const float2 y = extra ? dft31_single(lds, tw, t) : make_float2(0.f, 0.f);
       pw[31] = extra ? (y.x * y.x + y.y * y.y) * inv_n2 : -1.f;
       v2f x[31];
@@ -556,6 +564,10 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
     // the +-spc window without a second pass.  The leftover output (kx) is
     // handled on its own.  Within-thread exact ties keep the first slot
     // (slot order, not natural order).
+    if (ACQ_SKIP & 4) {   // diagnostic only: no statistics
+      best_pk = pw[0] + pw[30];
+      continue;
+    }
     float m1 = -1.f, m2 = -1.f;
     int d1 = 0;
 #pragma unroll
