@@ -49,6 +49,9 @@
 #ifndef ACQ_SKIP
 #define ACQ_SKIP 0
 #endif
+#ifndef ACQ_LOAD_AUX
+#define ACQ_LOAD_AUX 0   // cache-policy bits of the X / F row loads
+#endif
 #ifndef ACQ_STAMP
 #define ACQ_STAMP(i)
 #endif
@@ -213,8 +216,8 @@ __device__ __forceinline__ void load_mul_pass16(const float2* __restrict__ Xb,
   if (sh.a == 0 && sh.b == 0 && sh.c == 0 && sh.d == 0) {   // uniform branch
 #pragma unroll
     for (int a = 0; a < 16; a++) {
-      const f4v u = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, a * kPlane * 8, 0));
-      const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
+      const f4v u = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, a * kPlane * 8, ACQ_LOAD_AUX));
+      const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, ACQ_LOAD_AUX));
       // conj(u) * f = u.re * f + u.im * (f.im, -f.re)
       const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
       x0[a] = bc(u.x) * f0 + bc(u.y) * mul_mi(f0);
@@ -226,9 +229,9 @@ __device__ __forceinline__ void load_mul_pass16(const float2* __restrict__ Xb,
 #pragma unroll
     for (int a = 0; a < 16; a++) {
       const int pa = ((a - sh.a) & 15) * kPlane * 8;
-      const f2v u0 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v0, pa, 0));
-      const f2v u1 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v1, pa, 0));
-      const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, 0));
+      const f2v u0 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v0, pa, ACQ_LOAD_AUX));
+      const f2v u1 = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v1, pa, ACQ_LOAD_AUX));
+      const f4v f = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, a * kPlane * 8, ACQ_LOAD_AUX));
       const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
       x0[a] = bc(u0.x) * f0 + bc(u0.y) * mul_mi(f0);
       x1[a] = bc(u1.x) * f1 + bc(u1.y) * mul_mi(f1);
@@ -437,7 +440,9 @@ __device__ __forceinline__ bool better(float v1, int k1, float v0, int k0) {
   return v1 > v0 || (v1 == v0 && k1 < k0);
 }
 
-// max value, smallest natural index among equals; result broadcast to all threads
+// max value, smallest natural index among equals; result broadcast to all
+// threads.  One barrier: the scratch slots are next written after at least
+// one more barrier (the next block / unit), so no trailing barrier is needed.
 __device__ __forceinline__ void block_argmax(float& v, int& k, PeakSlot* scratch) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -453,19 +458,19 @@ __device__ __forceinline__ void block_argmax(float& v, int& k, PeakSlot* scratch
 #pragma unroll
   for (int i = 1; i < kThreads / 64; i++)
     if (better(scratch[i].v, scratch[i].k, v, k)) { v = scratch[i].v; k = scratch[i].k; }
-  __syncthreads();
 }
 
-__device__ __forceinline__ float block_max(float v, float* scratch) {
+// max over the workgroup, valid in thread 0 only (one barrier, as above)
+__device__ __forceinline__ float block_max0(float v, float* scratch) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) scratch[w] = v;
   __syncthreads();
-  v = scratch[0];
+  if (threadIdx.x == 0) {
 #pragma unroll
-  for (int i = 1; i < kThreads / 64; i++) v = fmaxf(v, scratch[i]);
-  __syncthreads();
+    for (int i = 1; i < kThreads / 64; i++) v = fmaxf(v, scratch[i]);
+  }
   return v;
 }
 
@@ -592,7 +597,7 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
     };
     float sv = in_win(k1) ? m2 : m1;
     if (extra && !in_win(kx)) sv = fmaxf(sv, pw[31]);
-    sv = block_max(sv, s_mx);
+    sv = block_max0(sv, s_mx);
     ACQ_STAMP(i * 6 + 5);
     best_pk = v;
     best_k = kk;
