@@ -55,6 +55,12 @@
 #ifndef ACQ_STAMP
 #define ACQ_STAMP(i)
 #endif
+#ifndef ACQ_LDGROUP         // pipelined kernel: planes per group of row loads
+#define ACQ_LDGROUP 8
+#endif
+#ifndef ACQ_PSTAMP          // pipelined kernel: (unit iteration, stamp id), tools/acq_pstamps.hip
+#define ACQ_PSTAMP(it, i)
+#endif
 
 namespace {
 
@@ -65,7 +71,10 @@ constexpr int E16 = 15345, E3 = 10912, E11 = 5952, E31 = 528;
 constexpr int kThreads = 512;           // 8 wavefronts -> up to 256 VGPRs each
 // Spectra rows in HBM are padded to 16 planes x 1024 complex (128 KiB) so the
 // radix-16 loads are 16-byte aligned: LDS position a*1023+g <-> a*1024+g.
-constexpr int kPlane = 1024;
+#ifndef ACQ_PLANE
+#define ACQ_PLANE 1024
+#endif
+constexpr int kPlane = ACQ_PLANE;
 constexpr int NPAD = 16 * kPlane;
 constexpr int kGroups31 = N / 31;       // 528 radix-31 groups
 constexpr int kLeft = kGroups31 - kThreads;  // 16 groups done as direct dot products
@@ -614,6 +623,508 @@ __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
   ACQ_STAMP(13);
 }
 
+// ---- the pipelined (persistent, two-role) correlation kernel -------------------
+// One workgroup per CU (the 128 KiB row fills the LDS), 1024 threads:
+//   waves 0-7  ("compute"): the in-LDS passes of unit u -- 3x11, radix-31 --
+//              and the row statistics;
+//   waves 8-15 ("stream"):  the HBM/L2 loads, conj(X)*F and radix-16 of unit
+//              u+G in registers while the compute waves work, the LDS write
+//              of that row once the compute waves hold their radix-31 inputs,
+//              and the 16 leftover radix-31 groups of unit u.
+// Per unit:  P1 [3x11 | loads+radix-16]  S1  P2 [radix-31 inputs -> regs |
+// leftover inputs -> side buffer]  S2  P3 [radix-31 + top-2 | row write +
+// leftover outputs]  S3 (argmax)  P4 [second peak]  S4.
+// Both roles keep their per-thread working set in the SAME register array r,
+// so the stream role's 32 loaded values and the compute role's 31-33 values
+// share VGPRs (the 1024-thread launch bound allows 128 per thread).
+constexpr int kPipeThreads = 1024;
+constexpr int kRole = 512;   // threads per role
+
+template <int O>
+__device__ __forceinline__ void dft16_r(v2f (&r)[33]) {
+  v2f x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = r[O + i];
+  dft16(x);
+#pragma unroll
+  for (int i = 0; i < 16; i++) r[O + i] = x[i];
+}
+
+// conj(X) * F for radix-16 groups g0 = 2 tl, g0 + 1 into r[0..15], r[16..31]
+__device__ __forceinline__ void load_mul_r(const float2* __restrict__ Xb,
+                                           const float2* __restrict__ Fc, int tl,
+                                           const Shift& sh, v2f (&r)[33]) {
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, 0, NPAD * 8, 0x00020000);
+  const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)Fc, 0, NPAD * 8, 0x00020000);
+  // g0 is made opaque so that its (b, c, d) decomposition is recomputed per
+  // unit instead of being hoisted out of the unit loop into live VGPRs
+  int g0 = 2 * tl;
+  asm volatile("" : "+v"(g0));
+  const int voff = g0 * 8;
+  // Planes in groups of kLdGroup: all loads of a group are issued before any
+  // of its products (sched_group_barrier pins the 16-18 VMEM reads first), so
+  // a unit costs 16 / kLdGroup L2 round trips instead of one per plane.
+  constexpr int kLdGroup = ACQ_LDGROUP;
+  if (sh.a == 0 && sh.b == 0 && sh.c == 0 && sh.d == 0) {   // uniform branch
+#pragma unroll
+    for (int a0 = 0; a0 < 16; a0 += kLdGroup) {
+      f4v U[kLdGroup], Fv[kLdGroup];
+#pragma unroll
+      for (int a = 0; a < kLdGroup; a++) {
+        U[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, (a0 + a) * kPlane * 8, 0));
+        Fv[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, (a0 + a) * kPlane * 8, 0));
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, 2 * kLdGroup, 0);
+#pragma unroll
+      for (int a = 0; a < kLdGroup; a++) {
+        const f4v u = U[a], f = Fv[a];
+        const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
+        r[a0 + a] = bc(u.x) * f0 + bc(u.y) * mul_mi(f0);
+        r[16 + a0 + a] = bc(u.z) * f1 + bc(u.w) * mul_mi(f1);
+      }
+    }
+  } else {
+    const int v0 = shift_group(g0 < M16 ? g0 : 0, sh) * 8;
+    const int v1 = shift_group(g0 + 1 < M16 ? g0 + 1 : 0, sh) * 8;
+#pragma unroll
+    for (int a0 = 0; a0 < 16; a0 += kLdGroup) {
+      f2v U0[kLdGroup], U1[kLdGroup];
+      f4v Fv[kLdGroup];
+#pragma unroll
+      for (int a = 0; a < kLdGroup; a++) {
+        const int pa = ((a0 + a - sh.a) & 15) * kPlane * 8;
+        U0[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v0, pa, 0));
+        U1[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v1, pa, 0));
+        Fv[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, (a0 + a) * kPlane * 8, 0));
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, 3 * kLdGroup, 0);
+#pragma unroll
+      for (int a = 0; a < kLdGroup; a++) {
+        const f4v f = Fv[a];
+        const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
+        r[a0 + a] = bc(U0[a].x) * f0 + bc(U0[a].y) * mul_mi(f0);
+        r[16 + a0 + a] = bc(U1[a].x) * f1 + bc(U1[a].y) * mul_mi(f1);
+      }
+    }
+  }
+  dft16_r<0>(r);
+  dft16_r<16>(r);
+  // pin the radix-16 results here (P1): without this the arithmetic is sunk
+  // past the barriers to its only use, the LDS write in P3
+#pragma unroll
+  for (int i = 0; i < 32; i++) asm volatile("" : "+v"(r[i]));
+}
+
+__device__ __forceinline__ void store16_r(float2* lds, int tl, const v2f (&r)[33]) {
+  int g0 = 2 * tl;
+  asm volatile("" : "+v"(g0));   // per-unit address arithmetic, not hoisted VGPRs
+  const bool two = g0 + 1 < M16;
+#pragma unroll
+  for (int a = 0; a < 16; a++) {
+    lds[a * M16 + g0] = st2(r[a]);
+    if (two) lds[a * M16 + g0 + 1] = st2(r[16 + a]);
+  }
+}
+
+// Threads t >= 496 compute a copy of task 0 and store nothing: r is then
+// redefined on every lane (a lane that kept its old r would keep it live
+// around the whole unit loop).
+__device__ __forceinline__ void pass33_r(float2* lds, int t, v2f (&r)[33]) {
+  const bool own = t < 16 * 31;
+  const int tt = own ? t : 0;
+  const int a = tt / 31, d = tt % 31;
+  float2* base = lds + a * M16 + d;
+#pragma unroll
+  for (int i = 0; i < 33; i++) r[i] = ld2(base[i * 31]);
+#pragma unroll
+  for (int c = 0; c < 11; c++) dft3(r[c], r[11 + c], r[22 + c]);
+#pragma unroll
+  for (int b = 0; b < 3; b++) {
+    v2f x[11];
+#pragma unroll
+    for (int c = 0; c < 11; c++) x[c] = r[b * 11 + c];
+    dftp<11>(x);
+#pragma unroll
+    for (int c = 0; c < 11; c++) r[b * 11 + c] = x[c];
+  }
+  if (own) {
+#pragma unroll
+    for (int i = 0; i < 33; i++) base[i * 31] = st2(r[i]);
+  }
+}
+
+// Radix-31 of r[0..30] reduced on the fly to this thread's top-2 powers
+// |X_d|^2 * scale: the sums/differences overwrite r in place and each output
+// pair is squared and folded into (m1, d1, m2) as soon as it exists, so no
+// outputs are held (VGPR budget of the 1024-thread kernel).  Slots are visited
+// in the order 0, 1, 30, 2, 29, ..., 15, 16; an exact tie keeps the earlier
+// visited slot.
+__device__ __forceinline__ void top2_push(float p, int d, float& m1, float& m2, int& d1) {
+  d1 = p > m1 ? d : d1;
+  m2 = __builtin_amdgcn_fmed3f(m2, m1, p);
+  m1 = fmaxf(m1, p);
+}
+
+__device__ __forceinline__ void dft31_top2(v2f (&r)[33], float scale, float& m1, float& m2,
+                                           int& d1) {
+  constexpr int P = 31, H = 15;
+  const v2f x0 = r[0];
+  v2f X0 = x0;
+#pragma unroll
+  for (int j = 1; j <= H; j++) {
+    const v2f s = r[j] + r[P - j], d = r[j] - r[P - j];
+    r[j] = s;
+    r[P - j] = d;
+    X0 += s;
+  }
+  m1 = (X0.x * X0.x + X0.y * X0.y) * scale;
+  m2 = -1.f;
+  d1 = 0;
+#pragma unroll
+  for (int m = 1; m <= H; m++) {
+    v2f A = x0, B = (v2f){0.f, 0.f};
+#pragma unroll
+    for (int j = 1; j <= H; j++) {
+      const int q = (j * m) % P;
+      A += bc(kCos31[q]) * r[j];
+      B += bc(kSin31[q]) * r[P - j];
+    }
+    const v2f sb = swp(B);
+    const v2f lo = __builtin_elementwise_fma(sb, (v2f){1.f, -1.f}, A);    // X_m = A - i B
+    const v2f hi = __builtin_elementwise_fma(sb, (v2f){-1.f, 1.f}, A);    // X_{P-m} = A + i B
+    top2_push((lo.x * lo.x + lo.y * lo.y) * scale, m, m1, m2, d1);
+    top2_push((hi.x * hi.x + hi.y * hi.y) * scale, P - m, m1, m2, d1);
+  }
+}
+
+// One output pair (m, 31 - m) -- or X_0 for m = 0 -- of leftover radix-31
+// group 512 + g, g = t / 16, m = t % 16, from the side copy of its inputs;
+// twiddles from tw16[m][j] = (cos, sin)(2 pi jm / 31), j = 1..15.  Returns the
+// pair's top-2 powers and the natural index of the larger.
+__device__ __forceinline__ void leftover_pair(const float2* side, const float2* tw16, int t,
+                                              float scale, float& m1, float& m2, int& k1) {
+  const int g = t >> 4, m = t & 15;
+  const float2* x = side + g * 31;
+  const v2f x0 = ld2(x[0]);
+  v2f A = x0, B = (v2f){0.f, 0.f};
+#pragma unroll
+  for (int j = 1; j <= 15; j++) {
+    const v2f a = ld2(x[j]), b = ld2(x[31 - j]);
+    const float2 w = tw16[m * 16 + j];
+    A += bc(w.x) * (a + b);
+    B += bc(w.y) * (a - b);
+  }
+  const v2f sb = swp(B);
+  const v2f lo = __builtin_elementwise_fma(sb, (v2f){1.f, -1.f}, A);    // X_m
+  const v2f hi = __builtin_elementwise_fma(sb, (v2f){-1.f, 1.f}, A);    // X_{31-m}
+  const float pl = (lo.x * lo.x + lo.y * lo.y) * scale;
+  const float ph = m ? (hi.x * hi.x + hi.y * hi.y) * scale : -1.f;
+  const int d1 = ph > pl ? 31 - m : m;
+  m1 = fmaxf(pl, ph);
+  m2 = fminf(pl, ph);
+  k1 = out_base(kThreads + g) + d1 * E31;
+  k1 = k1 >= N ? k1 - N : k1;
+  k1 = k1 >= N ? k1 - N : k1;
+}
+
+// Wave reductions with ds_swizzle (xor 1..16 within each 32-lane half, the
+// pattern is an immediate: no per-lane address VGPRs to keep live); the two
+// half-wave results go to separate scratch slots.
+template <int X>
+__device__ __forceinline__ float swz_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x1f | (X << 10)));
+}
+template <int X>
+__device__ __forceinline__ int swz_i(int v) {
+  return __builtin_amdgcn_ds_swizzle(v, 0x1f | (X << 10));
+}
+
+__device__ __forceinline__ void pick(float& v, int& k, float v2, int k2) {
+  if (better(v2, k2, v, k)) { v = v2; k = k2; }
+}
+
+// (v, k) argmax over the workgroup (value max, smallest natural index among
+// equals), broadcast to every thread: swizzle steps within 32-lane halves,
+// the two halves via readlane, one slot per wave, one barrier, then a
+// depth-4 tree over the NT/64 slots.
+template <int NT>
+__device__ __forceinline__ void block_argmax_n(float& v, int& k, PeakSlot* scratch) {
+  pick(v, k, swz_f<1>(v), swz_i<1>(k));
+  pick(v, k, swz_f<2>(v), swz_i<2>(k));
+  pick(v, k, swz_f<4>(v), swz_i<4>(k));
+  pick(v, k, swz_f<8>(v), swz_i<8>(k));
+  pick(v, k, swz_f<16>(v), swz_i<16>(k));
+  float va = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  int ka = __builtin_amdgcn_readlane(k, 0);
+  pick(va, ka, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32)),
+       __builtin_amdgcn_readlane(k, 32));
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = PeakSlot{va, ka};
+  __syncthreads();
+  constexpr int S = NT / 64;
+  float sv[S];
+  int sk[S];
+#pragma unroll
+  for (int i = 0; i < S; i++) { sv[i] = scratch[i].v; sk[i] = scratch[i].k; }
+#pragma unroll
+  for (int w = 1; w < S; w *= 2)
+#pragma unroll
+    for (int i = 0; i + w < S; i += 2 * w) pick(sv[i], sk[i], sv[i + w], sk[i + w]);
+  v = sv[0];
+  k = sk[0];
+}
+
+// max over the workgroup, valid in thread 0 only (one barrier)
+template <int NT>
+__device__ __forceinline__ float block_max0_n(float v, float* scratch) {
+  v = fmaxf(v, swz_f<1>(v));
+  v = fmaxf(v, swz_f<2>(v));
+  v = fmaxf(v, swz_f<4>(v));
+  v = fmaxf(v, swz_f<8>(v));
+  v = fmaxf(v, swz_f<16>(v));
+  const float h = fmaxf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0)),
+                        __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32)));
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    constexpr int S = NT / 64;
+    float m[S];
+#pragma unroll
+    for (int i = 0; i < S; i++) m[i] = scratch[i];
+#pragma unroll
+    for (int w = 1; w < S; w *= 2)
+#pragma unroll
+      for (int i = 0; i + w < S; i += 2 * w) m[i] = fmaxf(m[i], m[i + w]);
+    v = m[0];
+  }
+  return v;
+}
+
+struct UnitInfo {
+  int rowid, blk, code;
+  int4 fm;
+};
+
+__device__ __forceinline__ UnitInfo unit_info(int u, const int* __restrict__ order, int n_blocks,
+                                              int n_bins, const int* __restrict__ group_code,
+                                              const int* __restrict__ group_freq,
+                                              const int4* __restrict__ fmap) {
+  UnitInfo ui;
+  const int unit = order[u];
+  ui.rowid = unit / n_blocks;
+  ui.blk = unit % n_blocks;
+  const int g = ui.rowid / n_bins, bin = ui.rowid % n_bins;
+  ui.code = group_code[g];
+  ui.fm = fmap[group_freq[g * n_bins + bin]];
+  return ui;
+}
+
+// Per-unit statistics of the pipelined kernel, carried across the next
+// unit's barriers by the compute role.
+struct RowCand {
+  float m1, m2, l1, l2;   // own group top-2, leftover pair top-2
+  int k1, kl;             // natural indices of m1 / l1
+};
+
+// DPP lane exchanges (quad_perm 1032 / 2301, row_half_mirror, row_mirror):
+// four steps leave every lane of each 16-lane row holding the row result;
+// the four rows are combined through readlane.  Pure VALU, no LDS round trips.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ float rl_f(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+// wave-level (v, k) argmax -> one slot per wave
+__device__ __forceinline__ void wave_argmax_slot(float v, int k, PeakSlot* slots) {
+  pick(v, k, dpp_f<0xB1>(v), dpp_i<0xB1>(k));
+  pick(v, k, dpp_f<0x4E>(v), dpp_i<0x4E>(k));
+  pick(v, k, dpp_f<0x141>(v), dpp_i<0x141>(k));
+  pick(v, k, dpp_f<0x140>(v), dpp_i<0x140>(k));
+  float va = rl_f(v, 0);
+  int ka = __builtin_amdgcn_readlane(k, 0);
+  pick(va, ka, rl_f(v, 16), __builtin_amdgcn_readlane(k, 16));
+  pick(va, ka, rl_f(v, 32), __builtin_amdgcn_readlane(k, 32));
+  pick(va, ka, rl_f(v, 48), __builtin_amdgcn_readlane(k, 48));
+  if ((threadIdx.x & 63) == 0) slots[threadIdx.x >> 6] = PeakSlot{va, ka};
+}
+
+template <int S>
+__device__ __forceinline__ PeakSlot read_argmax(const PeakSlot* slots) {
+  float sv[S];
+  int sk[S];
+#pragma unroll
+  for (int i = 0; i < S; i++) { sv[i] = slots[i].v; sk[i] = slots[i].k; }
+#pragma unroll
+  for (int w = 1; w < S; w *= 2)
+#pragma unroll
+    for (int i = 0; i + w < S; i += 2 * w) pick(sv[i], sk[i], sv[i + w], sk[i + w]);
+  return PeakSlot{sv[0], sk[0]};
+}
+
+// second-peak candidate of this thread given the row argmax kk (open circular
+// window); each candidate set has at most one slot inside any window of < 528
+__device__ __forceinline__ float second_cand(const RowCand& c, int kk, int spc) {
+  auto in_win = [&](int k) {
+    int dist = k - kk;
+    if (dist < 0) dist += N;
+    return dist < spc || dist > N - spc;
+  };
+  return fmaxf(in_win(c.k1) ? c.m2 : c.m1, in_win(c.kl) ? c.l2 : c.l1);
+}
+
+__device__ __forceinline__ void wave_max_slot(float v, float* slots) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  const float h = fmaxf(fmaxf(rl_f(v, 0), rl_f(v, 16)), fmaxf(rl_f(v, 32), rl_f(v, 48)));
+  if ((threadIdx.x & 63) == 0) slots[threadIdx.x >> 6] = h;
+}
+
+template <int S>
+__device__ __forceinline__ float read_max(const float* slots) {
+  float m[S];
+#pragma unroll
+  for (int i = 0; i < S; i++) m[i] = slots[i];
+#pragma unroll
+  for (int w = 1; w < S; w *= 2)
+#pragma unroll
+    for (int i = 0; i + w < S; i += 2 * w) m[i] = fmaxf(m[i], m[i + w]);
+  return m[0];
+}
+
+__device__ __forceinline__ void write_stats(gnsscorr_acq_row* stats, const UnitInfo& uc,
+                                            int n_blocks, float peak, int argmax, float second) {
+  gnsscorr_acq_row o;
+  o.peak = peak;
+  o.argmax = argmax;
+  o.second = second;
+  o.block = uc.blk;
+  stats[(long)uc.rowid * n_blocks + uc.blk] = o;
+}
+
+// BEST_OF_BLOCKS statistics only (unit = (row, block)); launched with at most
+// one workgroup per CU, each looping over units u = blockIdx.x + k * gridDim.x.
+// Three barriers per unit:
+//   P1 [compute: argmax of the previous unit from its slots, its second-peak
+//       wave maxima, 3x11 pass | stream: loads + radix-16 of unit u+G]   S1
+//   P2 [compute: radix-31 inputs -> regs, leftover inputs -> side copy;
+//       thread 0: second peak + stats of the previous unit]              S2
+//   P3 [compute: radix-31 + top-2, leftover pair, wave argmax slots |
+//       stream: row write of unit u+G]                                   S3
+// so the row statistics ride on the next unit's barriers.
+__global__ __launch_bounds__(kPipeThreads) void acq_corr_pipe_kernel(
+    const float2* __restrict__ X, const float2* __restrict__ F, int n_blocks,
+    const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins,
+    int spc, gnsscorr_acq_row* __restrict__ stats, const int* __restrict__ order,
+    const int4* __restrict__ fmap, int n_units) {
+  constexpr int S = kRole / 64;   // statistics slots: one per compute wave
+  __shared__ float2 lds[N];
+  __shared__ float2 side[kLeft * 31];
+  __shared__ float2 tw16[16 * 16];
+  __shared__ PeakSlot s_pk[S];
+  __shared__ float s_mx[S];
+  const int t = threadIdx.x;
+  // wave-uniform role, made visibly uniform (SGPR) so that the buffer
+  // descriptors built inside role branches stay scalar
+  const bool stream = __builtin_amdgcn_readfirstlane(t >> 9) != 0;
+  const int tl = t & (kRole - 1);
+  const int G = gridDim.x;
+  const float inv_n2 = 1.0f / ((float)N * (float)N);
+  int u = blockIdx.x;
+  if (u >= n_units) return;
+  if (t < 256) {
+    const int m = t >> 4, j = t & 15, q = (j * m) % 31;
+    tw16[t] = make_float2(kCos31[q], kSin31[q]);
+  }
+  const int kb = out_base(tl);   // natural index of slot 0 of radix-31 group tl
+
+  v2f r[33];
+#pragma unroll
+  for (int i = 0; i < 33; i++) r[i] = (v2f){0.f, 0.f};
+  if (stream) {   // prologue: the first unit's radix-16 pass
+    const UnitInfo un = unit_info(u, order, n_blocks, n_bins, group_code, group_freq, fmap);
+    const Shift sh{un.fm.y, un.fm.z, un.fm.w >> 5, un.fm.w & 31};
+    load_mul_r(X + ((long)un.fm.x * n_blocks + un.blk) * NPAD, F + (long)un.code * NPAD, tl, sh, r);
+    store16_r(lds, tl, r);
+  }
+  __syncthreads();
+
+  RowCand prev{-1.f, -1.f, -1.f, -1.f, 0, 0};
+  PeakSlot pk{-1.f, 0};
+  int it = 0;
+  for (; u < n_units; u += G, it++) {
+    const int un_next = u + G;
+    const bool nxt = un_next < n_units;
+    ACQ_PSTAMP(it, 0);
+    // P1
+    if (!stream) {
+      if (it > 0) {   // previous unit: row argmax, then second-peak wave maxima
+        pk = read_argmax<S>(s_pk);
+        wave_max_slot(second_cand(prev, pk.k, spc), s_mx);
+      }
+      pass33_r(lds, tl, r);
+    } else if (nxt) {
+      const UnitInfo un = unit_info(un_next, order, n_blocks, n_bins, group_code, group_freq, fmap);
+      const Shift sh{un.fm.y, un.fm.z, un.fm.w >> 5, un.fm.w & 31};
+      load_mul_r(X + ((long)un.fm.x * n_blocks + un.blk) * NPAD, F + (long)un.code * NPAD, tl, sh, r);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 33; i++) r[i] = (v2f){0.f, 0.f};   // r is redefined on every path
+    }
+    ACQ_PSTAMP(it, 1);
+    __syncthreads();   // S1
+    ACQ_PSTAMP(it, 2);
+    // P2
+    if (!stream) {
+#pragma unroll
+      for (int d = 0; d < 31; d++) r[d] = ld2(lds[tl * 31 + d]);
+      if (tl < kLeft * 31) side[tl] = lds[kThreads * 31 + tl];   // leftover inputs
+      if (t == 0 && it > 0)
+        write_stats(stats, unit_info(u - G, order, n_blocks, n_bins, group_code, group_freq, fmap),
+                    n_blocks, pk.v, pk.k, read_max<S>(s_mx));
+    }
+    ACQ_PSTAMP(it, 3);
+    __syncthreads();   // S2: the row is free
+    ACQ_PSTAMP(it, 4);
+    // P3: compute role -- radix-31 group tl, then (tl < 256) one output pair of
+    // the 16 leftover groups from the side copy; stream role -- the row write
+    if (!stream) {
+      RowCand c{-1.f, -1.f, -1.f, -1.f, 0, 0};
+      int d1;
+      dft31_top2(r, inv_n2, c.m1, c.m2, d1);
+      c.k1 = kb + d1 * E31;
+      if (c.k1 >= N) c.k1 -= N;
+      if (tl < kLeft * 16) leftover_pair(side, tw16, tl, inv_n2, c.l1, c.l2, c.kl);
+      float v = c.m1;
+      int k = c.k1;
+      pick(v, k, c.l1, c.kl);
+      wave_argmax_slot(v, k, s_pk);
+      prev = c;
+    } else if (nxt) {
+      store16_r(lds, tl, r);
+    }
+    ACQ_PSTAMP(it, 5);
+    __syncthreads();   // S3: next row written, argmax slots complete
+    ACQ_PSTAMP(it, 6);
+  }
+  // epilogue: statistics of the last unit
+  if (!stream) {
+    pk = read_argmax<S>(s_pk);
+    wave_max_slot(second_cand(prev, pk.k, spc), s_mx);
+  }
+  __syncthreads();
+  if (t == 0)
+    write_stats(stats, unit_info(u - G, order, n_blocks, n_bins, group_code, group_freq, fmap),
+                n_blocks, pk.v, pk.k, read_max<S>(s_mx));
+}
+
 // Per group (one wavefront, bins across lanes):
 //  combine   acquisition.sci:126-132 -- per bin keep block 1 only if its max
 //            is strictly larger than block 2's (generalised: a later block
@@ -703,6 +1214,8 @@ struct gnsscorr_acq_ctx {
   int4* d_fmap = nullptr;               // per frequency: spectrum class + shift coordinates
   double* d_cfreq = nullptr;            // per class: the residue frequency whose spectrum is computed
   int* d_nclass = nullptr;
+  int n_cu = 256;                       // persistent grid of the pipelined kernel
+  int pipe = 1;                         // GNSSCORR_ACQ_PIPE=0: one-unit-per-workgroup kernel
   float2* d_stage = nullptr;            // forward-FFT staging rows
   size_t cap_stage = 0;
   gnsscorr_acq_row* d_stats = nullptr;  // per (row, block) statistics
@@ -764,6 +1277,10 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
   HIP_TRY(hipSetDevice(cfg->device));
   auto* c = new gnsscorr_acq_ctx();
   c->cfg = *cfg;
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device) !=
+          hipSuccess || c->n_cu < 1)
+    c->n_cu = 256;
+  if (const char* e = getenv("GNSSCORR_ACQ_PIPE")) c->pipe = atoi(e) != 0;
   auto fail = [&](int code) {
     gnsscorr_acq_destroy(c);
     return code;
@@ -949,6 +1466,10 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
   else if (mode == GNSSCORR_ACQ_NONCOHERENT)
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_NONCOHERENT, false);
+  else if (c->pipe)
+    hipLaunchKernelGGL(acq_corr_pipe_kernel, dim3(n_units < c->n_cu ? n_units : c->n_cu),
+                       dim3(kPipeThreads), 0, c->stream, c->d_X, c->d_F, n_blocks, d_gcode,
+                       d_gfreq, n_bins, spc, c->d_stats, c->d_order, c->d_fmap, n_units);
   else
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, false);
 #undef ACQ_CORR_LAUNCH

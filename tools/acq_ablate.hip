@@ -50,15 +50,25 @@ int main() {
     float best = 1e9f;
     for (int it = 0; it < 12; it++) {
       (void)hipEventRecord(e0, 0);
+#ifdef PIPE
+      hipLaunchKernelGGL(acq_corr_pipe_kernel, dim3(256), dim3(kPipeThreads), 0, 0, dX, dF, NB, dgc,
+                         dgf, B, 16, drows, dord, dfm, R * NB);
+#else
       hipLaunchKernelGGL((acq_corr_kernel<0, false>), dim3(R * NB), dim3(kThreads), 0, 0, dX, dF,
                          NB, dgc, dgf, B, 16, drows, (float*)nullptr, -1, dord, dfm);
+#endif
       (void)hipEventRecord(e1, 0);
       (void)hipEventSynchronize(e1);
       float ms = 0;
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (it >= 2 && ms < best) best = ms;
     }
-    printf("ACQ_SKIP=%d %s: %.1f us\n", ACQ_SKIP, shifted ? "shifted" : "aligned", best * 1e3);
+#ifdef PIPE
+    const char* kern = "pipe";
+#else
+    const char* kern = "old";
+#endif
+    printf("%s plane=%d ACQ_SKIP=%d %s: %.1f us\n", kern, kPlane, ACQ_SKIP, shifted ? "shifted" : "aligned", best * 1e3);
   }
   return 0;
 }
