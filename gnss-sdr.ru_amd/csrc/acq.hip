@@ -650,61 +650,49 @@ __device__ __forceinline__ void dft16_r(v2f (&r)[33]) {
   for (int i = 0; i < 16; i++) r[O + i] = x[i];
 }
 
-// conj(X) * F for radix-16 groups g0 = 2 tl, g0 + 1 into r[0..15], r[16..31]
+// conj(X) * F for radix-16 groups g0 = tl and g1 = tl + 512 into r[0..15],
+// r[16..31] (8-byte loads: consecutive lanes read consecutive columns, and the
+// LDS writes of store16_r are bank-conflict free).  g1 = 1023 (tl = 511) is the
+// zero pad column of the HBM rows; it is loaded but never stored.
 __device__ __forceinline__ void load_mul_r(const float2* __restrict__ Xb,
                                            const float2* __restrict__ Fc, int tl,
                                            const Shift& sh, v2f (&r)[33]) {
   const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, 0, NPAD * 8, 0x00020000);
   const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)Fc, 0, NPAD * 8, 0x00020000);
-  // g0 is made opaque so that its (b, c, d) decomposition is recomputed per
-  // unit instead of being hoisted out of the unit loop into live VGPRs
-  int g0 = 2 * tl;
+  // tl is made opaque so that the (b, c, d) decomposition of its groups is
+  // recomputed per unit instead of being hoisted out of the unit loop
+  int g0 = tl;
   asm volatile("" : "+v"(g0));
-  const int voff = g0 * 8;
+  const int f0off = g0 * 8, f1off = (g0 + kRole) * 8;
   // Planes in groups of kLdGroup: all loads of a group are issued before any
-  // of its products (sched_group_barrier pins the 16-18 VMEM reads first), so
-  // a unit costs 16 / kLdGroup L2 round trips instead of one per plane.
+  // of its products (sched_group_barrier pins the VMEM reads first), so a
+  // unit costs 16 / kLdGroup L2 round trips instead of one per plane.
   constexpr int kLdGroup = ACQ_LDGROUP;
-  if (sh.a == 0 && sh.b == 0 && sh.c == 0 && sh.d == 0) {   // uniform branch
+  int x0off = f0off, x1off = f1off;
+  int pa_shift = 0;
+  if (!(sh.a == 0 && sh.b == 0 && sh.c == 0 && sh.d == 0)) {   // uniform branch
+    x0off = shift_group(g0, sh) * 8;
+    x1off = shift_group(g0 + kRole < M16 ? g0 + kRole : 0, sh) * 8;
+    pa_shift = sh.a;
+  }
 #pragma unroll
-    for (int a0 = 0; a0 < 16; a0 += kLdGroup) {
-      f4v U[kLdGroup], Fv[kLdGroup];
+  for (int a0 = 0; a0 < 16; a0 += kLdGroup) {
+    f2v U0[kLdGroup], U1[kLdGroup], F0[kLdGroup], F1[kLdGroup];
 #pragma unroll
-      for (int a = 0; a < kLdGroup; a++) {
-        U[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, (a0 + a) * kPlane * 8, 0));
-        Fv[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, (a0 + a) * kPlane * 8, 0));
-      }
-      __builtin_amdgcn_sched_group_barrier(0x020, 2 * kLdGroup, 0);
-#pragma unroll
-      for (int a = 0; a < kLdGroup; a++) {
-        const f4v u = U[a], f = Fv[a];
-        const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
-        r[a0 + a] = bc(u.x) * f0 + bc(u.y) * mul_mi(f0);
-        r[16 + a0 + a] = bc(u.z) * f1 + bc(u.w) * mul_mi(f1);
-      }
+    for (int a = 0; a < kLdGroup; a++) {
+      const int pa = ((a0 + a - pa_shift) & 15) * kPlane * 8;
+      const int pf = (a0 + a) * kPlane * 8;
+      U0[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, x0off, pa, 0));
+      U1[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, x1off, pa, 0));
+      F0[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rf, f0off, pf, 0));
+      F1[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rf, f1off, pf, 0));
     }
-  } else {
-    const int v0 = shift_group(g0 < M16 ? g0 : 0, sh) * 8;
-    const int v1 = shift_group(g0 + 1 < M16 ? g0 + 1 : 0, sh) * 8;
+    __builtin_amdgcn_sched_group_barrier(0x020, 4 * kLdGroup, 0);
 #pragma unroll
-    for (int a0 = 0; a0 < 16; a0 += kLdGroup) {
-      f2v U0[kLdGroup], U1[kLdGroup];
-      f4v Fv[kLdGroup];
-#pragma unroll
-      for (int a = 0; a < kLdGroup; a++) {
-        const int pa = ((a0 + a - sh.a) & 15) * kPlane * 8;
-        U0[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v0, pa, 0));
-        U1[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, v1, pa, 0));
-        Fv[a] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rf, voff, (a0 + a) * kPlane * 8, 0));
-      }
-      __builtin_amdgcn_sched_group_barrier(0x020, 3 * kLdGroup, 0);
-#pragma unroll
-      for (int a = 0; a < kLdGroup; a++) {
-        const f4v f = Fv[a];
-        const v2f f0 = (v2f){f.x, f.y}, f1 = (v2f){f.z, f.w};
-        r[a0 + a] = bc(U0[a].x) * f0 + bc(U0[a].y) * mul_mi(f0);
-        r[16 + a0 + a] = bc(U1[a].x) * f1 + bc(U1[a].y) * mul_mi(f1);
-      }
+    for (int a = 0; a < kLdGroup; a++) {
+      const v2f f0 = (v2f){F0[a].x, F0[a].y}, f1 = (v2f){F1[a].x, F1[a].y};
+      r[a0 + a] = bc(U0[a].x) * f0 + bc(U0[a].y) * mul_mi(f0);
+      r[16 + a0 + a] = bc(U1[a].x) * f1 + bc(U1[a].y) * mul_mi(f1);
     }
   }
   dft16_r<0>(r);
@@ -716,13 +704,13 @@ __device__ __forceinline__ void load_mul_r(const float2* __restrict__ Xb,
 }
 
 __device__ __forceinline__ void store16_r(float2* lds, int tl, const v2f (&r)[33]) {
-  int g0 = 2 * tl;
+  int g0 = tl;
   asm volatile("" : "+v"(g0));   // per-unit address arithmetic, not hoisted VGPRs
-  const bool two = g0 + 1 < M16;
+  const bool two = g0 + kRole < M16;
 #pragma unroll
   for (int a = 0; a < 16; a++) {
     lds[a * M16 + g0] = st2(r[a]);
-    if (two) lds[a * M16 + g0 + 1] = st2(r[16 + a]);
+    if (two) lds[a * M16 + g0 + kRole] = st2(r[16 + a]);
   }
 }
 
@@ -799,7 +787,7 @@ __device__ __forceinline__ void dft31_top2(v2f (&r)[33], float scale, float& m1,
 
 // One output pair (m, 31 - m) -- or X_0 for m = 0 -- of leftover radix-31
 // group 512 + g, g = t / 16, m = t % 16, from the side copy of its inputs;
-// twiddles from tw16[m][j] = (cos, sin)(2 pi jm / 31), j = 1..15.  Returns the
+// twiddles from tw16[j][m] = (cos, sin)(2 pi jm / 31), j = 1..15.  Returns the
 // pair's top-2 powers and the natural index of the larger.
 __device__ __forceinline__ void leftover_pair(const float2* side, const float2* tw16, int t,
                                               float scale, float& m1, float& m2, int& k1) {
@@ -810,7 +798,7 @@ __device__ __forceinline__ void leftover_pair(const float2* side, const float2* 
 #pragma unroll
   for (int j = 1; j <= 15; j++) {
     const v2f a = ld2(x[j]), b = ld2(x[31 - j]);
-    const float2 w = tw16[m * 16 + j];
+    const float2 w = tw16[j * 16 + m];
     A += bc(w.x) * (a + b);
     B += bc(w.y) * (a - b);
   }
@@ -1040,7 +1028,7 @@ __global__ __launch_bounds__(kPipeThreads) void acq_corr_pipe_kernel(
   int u = blockIdx.x;
   if (u >= n_units) return;
   if (t < 256) {
-    const int m = t >> 4, j = t & 15, q = (j * m) % 31;
+    const int j = t >> 4, m = t & 15, q = (j * m) % 31;   // tw16[j][m]: lanes m read 16 consecutive
     tw16[t] = make_float2(kCos31[q], kSin31[q]);
   }
   const int kb = out_base(tl);   // natural index of slot 0 of radix-31 group tl
