@@ -450,10 +450,10 @@ def main():
                        "prns": N_PRN, "bins": N_BINS, "blocks": N_BLK, "samples_per_code": N,
                        "cells_per_search": CELLS_PER_SEARCH,
                        "parallelism": f"weak: one search per GPU per step x {W} GPUs"},
-            "roofline": {"bound": "valu", "kernel": "acq_corr_kernel", "achieved": achieved,
+            "roofline": {"bound": "valu", "kernel": "acq_corr_pipe_kernel", "achieved": achieved,
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_TFLOPS,
-                         "traffic": pmc_traffic("acq_corr_kernel"),
+                         "traffic": pmc_traffic("acq_corr_pipe_kernel"),
                          "kernel_ms_per_launch": acq["corr_ms"],
                          "flop_per_launch": flop_launch},
             "search_latency_ms": acq["dt"] / a.steps * 1e3,

@@ -135,3 +135,21 @@ void gnsscorr_sdr_code_gen(int sv, uint8_t *chips)
   const int d = 1023 - g2d[sv];
   for (int k = 0; k < 1023; k++) chips[k] = g1[k] ^ g2[(k + d) % 1023];
 }
+
+/* GN3S front-end products (SDR/objects/gps_source.cpp:92-93, :733-738): for
+ * each 2-bit code l (LUT {-3,-1,1,3}) and NCO index p, the int16 values the
+ * reference stores, (int16)(LUT[l] * (+8 cos(2 pi p/1024))) as I and
+ * (int16)(LUT[l] * (-8 sin(2 pi p/1024))) as Q (double product, truncation).
+ * out[(l * 1024 + p) * 2 + {0, 1}] = {I, Q}. */
+void gnsscorr_sdr_gn3s_products(int16_t *out)
+{
+  static const int16_t lut[4] = {-3, -1, 1, 3};
+  for (int p = 0; p < 1024; p++) {
+    const double s = -8 * sin(2 * M_PI * p / 1024);
+    const double c = +8 * cos(2 * M_PI * p / 1024);
+    for (int l = 0; l < 4; l++) {
+      out[(l * 1024 + p) * 2 + 0] = (int16_t)(lut[l] * c);
+      out[(l * 1024 + p) * 2 + 1] = (int16_t)(lut[l] * s);
+    }
+  }
+}

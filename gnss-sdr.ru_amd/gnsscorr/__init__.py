@@ -121,6 +121,9 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sdr_corr_create", "gnsscorr_sdr_corr_destroy", "gnsscorr_sdr_init_chan",
     "gnsscorr_sdr_accum_dev", "gnsscorr_sdr_correlate", "gnsscorr_sdr_corr_sync",
     "gnsscorr_sdr_corr_stream",
+    "gnsscorr_sdr_gn3s_products", "gnsscorr_sdr_fe_create", "gnsscorr_sdr_fe_destroy",
+    "gnsscorr_sdr_gn3s_dev", "gnsscorr_sdr_gn3s", "gnsscorr_sdr_downsample_count",
+    "gnsscorr_sdr_downsample_dev", "gnsscorr_sdr_fe_sync", "gnsscorr_sdr_fe_stream",
     "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
     "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
     "gnsscorr_event_elapsed_ms", "gnsscorr_event_destroy", "gnsscorr_dev_fill_if2",
@@ -196,6 +199,15 @@ def lib() -> C.CDLL:
         "gnsscorr_sdr_correlate": (I, [P, P, I, I, P, P, P, P, P]),
         "gnsscorr_sdr_corr_sync": (I, [P]),
         "gnsscorr_sdr_corr_stream": (P, [P]),
+        "gnsscorr_sdr_gn3s_products": (None, [P]),
+        "gnsscorr_sdr_fe_create": (I, [C.POINTER(P), I]),
+        "gnsscorr_sdr_fe_destroy": (I, [P]),
+        "gnsscorr_sdr_gn3s_dev": (I, [P, P, I, I, C.POINTER(C.c_uint32), C.c_uint32, P]),
+        "gnsscorr_sdr_gn3s": (I, [P, P, I, I, C.POINTER(C.c_uint32), C.c_uint32, P]),
+        "gnsscorr_sdr_downsample_count": (I, [I, D, D, P]),
+        "gnsscorr_sdr_downsample_dev": (I, [P, P, I, D, D, P, C.POINTER(C.c_int)]),
+        "gnsscorr_sdr_fe_sync": (I, [P]),
+        "gnsscorr_sdr_fe_stream": (P, [P]),
         "gnsscorr_dev_alloc": (I, [I, C.c_size_t, C.POINTER(P)]),
         "gnsscorr_dev_free": (I, [I, P]),
         "gnsscorr_memcpy_htod": (I, [I, P, P, C.c_size_t]),
@@ -621,6 +633,74 @@ class SdrAcqCtx:
     @property
     def stream(self) -> int:
         return lib().gnsscorr_sdr_acq_stream(self.h)
+
+
+GN3S_BLOCK_IN, GN3S_BLOCK_OUT, GN3S_STEP = 20000, 10240, 2557223528
+
+
+def gn3s_products() -> np.ndarray:
+    """The GN3S front end's int16 product table [4 codes, 1024 phases, 2]."""
+    out = np.zeros((4, 1024, 2), np.int16)
+    lib().gnsscorr_sdr_gn3s_products(_ptr(out))
+    return out
+
+
+def pack_2bit(samples) -> np.ndarray:
+    """One-sample-per-byte 2-bit codes -> packed bytes (sample j in bits 2j..2j+1)."""
+    s = np.ascontiguousarray(samples, np.uint8).reshape(-1, 4) & 3
+    return (s[:, 0] | (s[:, 1] << 2) | (s[:, 2] << 4) | (s[:, 3] << 6)).astype(np.uint8)
+
+
+class SdrFeCtx:
+    """GPS-SDR sample front end: GN3S 2-bit unpack + NCO mix + resample, downsample."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(lib().gnsscorr_sdr_fe_create(C.byref(h), device), "gnsscorr_sdr_fe_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gnsscorr_sdr_fe_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def gn3s(self, data, packed=False, phase=0, step=GN3S_STEP):
+        """data: n_blocks * 20000 bytes (or / 4 when packed); returns (CPX [n*10240, 2], phase)."""
+        d = np.ascontiguousarray(data, np.uint8).ravel()
+        per = GN3S_BLOCK_IN // 4 if packed else GN3S_BLOCK_IN
+        nb = d.size // per
+        out = np.zeros((nb * GN3S_BLOCK_OUT, 2), np.int16)
+        ph = C.c_uint32(phase)
+        _check(lib().gnsscorr_sdr_gn3s(self.h, _ptr(d), int(packed), nb, C.byref(ph),
+                                       C.c_uint32(step), _ptr(out)), "gnsscorr_sdr_gn3s")
+        return out, ph.value
+
+    def gn3s_dev(self, d_in, packed, n_blocks, phase, d_out, step=GN3S_STEP) -> int:
+        ph = C.c_uint32(phase)
+        _check(lib().gnsscorr_sdr_gn3s_dev(self.h, d_in, int(packed), n_blocks, C.byref(ph),
+                                           C.c_uint32(step), d_out), "gnsscorr_sdr_gn3s_dev")
+        return ph.value
+
+    def downsample_dev(self, d_src, n_src, fdest, fsource, d_dest) -> int:
+        n = C.c_int()
+        _check(lib().gnsscorr_sdr_downsample_dev(self.h, d_src, n_src, C.c_double(fdest),
+                                                 C.c_double(fsource), d_dest, C.byref(n)),
+               "gnsscorr_sdr_downsample_dev")
+        return n.value
+
+    @staticmethod
+    def downsample_count(n_src, fdest, fsource) -> int:
+        return lib().gnsscorr_sdr_downsample_count(n_src, C.c_double(fdest), C.c_double(fsource),
+                                                   None)
+
+    def sync(self):
+        _check(lib().gnsscorr_sdr_fe_sync(self.h), "gnsscorr_sdr_fe_sync")
+
+    @property
+    def stream(self) -> int:
+        return lib().gnsscorr_sdr_fe_stream(self.h)
 
 
 class SdrCorrCtx:

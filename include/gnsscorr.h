@@ -420,6 +420,42 @@ int gnsscorr_sdr_corr_sync(gnsscorr_sdr_corr_ctx *ctx);
 void *gnsscorr_sdr_corr_stream(gnsscorr_sdr_corr_ctx *ctx);
 
 /* ======================================================================
+ * GPS-SDR sample front end, bit-exact with
+ *   GPS_Source::Read_GN3S   objects/gps_source.cpp:684-767 (2-bit LUT {-3,-1,1,3},
+ *                           1024-entry table NCO mix, products truncated to int16)
+ *   Resample_GN3S           objects/gps_source.cpp:933-943 (gdec nearest sample)
+ *   downsample              accessories/misc.cpp:174-197 (phase-wrap decimator)
+ * Output samples are the receivers' CPX (int16 I, Q) at 2.048 Msps, ready for
+ * gnsscorr_sdr_acq_strong_dev / gnsscorr_sdr_accum_dev without a host copy.
+ * ==================================================================== */
+#define GNSSCORR_GN3S_BLOCK_IN  20000          /* 2-bit samples per 5-ms read      */
+#define GNSSCORR_GN3S_BLOCK_OUT 10240          /* CPX per 5 ms = 5 packets of 2048 */
+#define GNSSCORR_GN3S_STEP      2557223528u    /* delta_phase (gps_source.cpp:96)  */
+
+typedef struct gnsscorr_sdr_fe_ctx gnsscorr_sdr_fe_ctx;
+
+/* The int16 product table the front end uses: out[(code * 1024 + p) * 2 + {0,1}]. */
+void gnsscorr_sdr_gn3s_products(int16_t *out);
+int gnsscorr_sdr_fe_create(gnsscorr_sdr_fe_ctx **out, int device);
+int gnsscorr_sdr_fe_destroy(gnsscorr_sdr_fe_ctx *ctx);
+/* n_blocks consecutive 5-ms reads.  fmt 0: one sample per byte (low 2 bits,
+ * the reference's gbuff); fmt 1: packed, 4 samples per byte, sample j of a byte
+ * in bits 2j..2j+1.  *phase: the NCO phase before the first sample (0 after
+ * construction in the reference), advanced by n_blocks * 20000 * step.
+ * d_out: n_blocks * 10240 CPX (int16 I, Q).  Asynchronous on the context stream. */
+int gnsscorr_sdr_gn3s_dev(gnsscorr_sdr_fe_ctx *ctx, const uint8_t *d_in, int fmt, int n_blocks,
+                          uint32_t *phase, uint32_t step, int16_t *d_out);
+int gnsscorr_sdr_gn3s(gnsscorr_sdr_fe_ctx *ctx, const uint8_t *h_in, int fmt, int n_blocks,
+                      uint32_t *phase, uint32_t step, int16_t *h_out);
+/* downsample(): number of samples kept from n_src (and the phase step). */
+int gnsscorr_sdr_downsample_count(int n_src, double f_dest, double f_source, uint32_t *step);
+/* downsample() of n_src CPX into d_dest (*n_out samples); requires 0 < f_dest < f_source. */
+int gnsscorr_sdr_downsample_dev(gnsscorr_sdr_fe_ctx *ctx, const int16_t *d_src, int n_src,
+                                double f_dest, double f_source, int16_t *d_dest, int *n_out);
+int gnsscorr_sdr_fe_sync(gnsscorr_sdr_fe_ctx *ctx);
+void *gnsscorr_sdr_fe_stream(gnsscorr_sdr_fe_ctx *ctx);
+
+/* ======================================================================
  * Device buffers / events (so hosts need no other GPU runtime)
  * ==================================================================== */
 int gnsscorr_dev_alloc(int device, size_t bytes, void **d_ptr);

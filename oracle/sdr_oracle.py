@@ -49,7 +49,29 @@ class OracleSDR:
         L.sdro_acq_strong.argtypes = [P, P, I, I, I, I]
         L.sdro_acq_strong.restype = _Res
         L.sdro_prn_codes.argtypes = [P]
+        L.orc_gn3s_block.argtypes = [P, P, C.c_uint32, P, P]
+        L.orc_downsample.argtypes = [P, P, D, D, I]
+        L.orc_downsample.restype = I
         self.L = L
+
+    def gn3s(self, samples, phase=0, step=2557223528):
+        """Read_GN3S + Resample_GN3S over consecutive 5-ms blocks of 20000 bytes
+        (gps_source.cpp:684-767, :933-943); returns (out [n*10240, 2] int16, phase)."""
+        b = np.ascontiguousarray(samples, np.uint8).reshape(-1, 20000)
+        out = np.zeros((b.shape[0] * 10240, 2), np.int16)
+        ph = C.c_uint32(phase)
+        for k in range(b.shape[0]):
+            blk = np.ascontiguousarray(b[k])
+            o = out[k * 10240:(k + 1) * 10240]
+            self.L.orc_gn3s_block(_p(blk), C.byref(ph), step, _p(o), None)
+        return out, ph.value
+
+    def downsample(self, src, fdest, fsource):
+        """downsample() (misc.cpp:174-197) of CPX src [n, 2] int16."""
+        src = np.ascontiguousarray(src, np.int16)
+        out = np.zeros_like(src)
+        k = self.L.orc_downsample(_p(out), _p(src), fdest, fsource, src.shape[0])
+        return out[:k].copy()
 
     def sine_gen(self, f, n=N, fs=FS):
         out = np.zeros((n, 2), np.int16)
@@ -119,7 +141,15 @@ class RefSDR:
         L.ref_sdr_acq_strong.argtypes = [P, D, I, I, I, P]
         L.ref_sdr_code_gen.argtypes = [I, P]
         L.ref_sdr_accum.argtypes = [P, P, P, P, P, I, P]
+        L.ref_sdr_downsample.argtypes = [P, P, D, D, I]
+        L.ref_sdr_downsample.restype = I
         self.L = L
+
+    def downsample(self, src, fdest, fsource):
+        src = np.ascontiguousarray(src, np.int16).copy()
+        out = np.zeros_like(src)
+        k = self.L.ref_sdr_downsample(_p(out), _p(src), fdest, fsource, src.shape[0])
+        return out[:k].copy()
 
     def sine_gen(self, f, n=N, fs=FS):
         out = np.zeros((n, 2), np.int16)

@@ -35,6 +35,21 @@ void ref_sdr_cmag_max(CPX* a, int n, int32* index, int32* mag)
 
 const int16* ref_sdr_prn_codes(void) { return PRN_Codes; }
 
+// downsample (accessories/misc.cpp:174-197) from the reference build; returns
+// the kept count the same way the reference loop does
+int ref_sdr_downsample(CPX* dest, CPX* source, double fdest, double fsource, int samps)
+{
+  downsample(dest, source, fdest, fsource, samps);
+  uint32 step = (uint32)floor((double)4294967296.0 * fdest / fsource), lphase = 0, phase = 0;
+  int k = 0;
+  for (int lcv = 0; lcv < samps; lcv++) {
+    if (phase <= lphase) k++;
+    lphase = phase;
+    phase += step;
+  }
+  return k;
+}
+
 // code_gen (accessories/misc.cpp:28-87): out[k] = chip (0/1) of sv
 void ref_sdr_code_gen(int sv, int16* out)
 {

@@ -12,6 +12,8 @@ oracle ref), plus PRN_Codes from accessories/prn_codes.h.  Stored:
                       wipe-off table built with the reference sine_gen, the
                       code_gen chips of sv 0..31, and Correlator::Accum known
                       answers (x86_cmulsc + x86_prn_accum_new) on random jobs
+  sdr_frontend.npz    downsample() (accessories/misc.cpp:174-197) known answers
+                      from the reference build at the receiver's source rates
 Usage:  python tests/golden/make_sdr_golden.py
 """
 import os
@@ -70,6 +72,18 @@ def main():
                         carrier_sha256=np.array(hashlib.sha256(car.tobytes()).hexdigest()),
                         chips=chips, jobs=np.array(jobs, np.int32), data=np.stack(data),
                         expected=np.stack(exp))
+    # sample front end: downsample() at the USRP rates of Resample_USRP_V1
+    # (gps_source.cpp:823-856: f_sample / decimate = 4.0, 4.096 and 8.0 Msps)
+    fe_src, fe_out, fe_rates = [], [], []
+    for k, fs in enumerate((4.0e6, 4.096e6, 8.0e6, 2.5e6)):
+        n = int(fs / 1000) + 7 * k
+        src = rng.integers(-2000, 2001, (n, 2)).astype(np.int16)
+        fe_src.append(np.pad(src, ((0, 8200 - n), (0, 0))))
+        o = ref.downsample(src, 2.048e6, fs)
+        fe_out.append(np.pad(o, ((0, 4200 - len(o)), (0, 0))))
+        fe_rates.append((fs, n, len(o)))
+    np.savez_compressed(os.path.join(out, "sdr_frontend.npz"), src=np.stack(fe_src),
+                        out=np.stack(fe_out), rates=np.array(fe_rates))
     for k, r in enumerate(res):
         print("scene", k, [(int(v["sv"]) + 1, int(v["code_phase"]), int(v["doppler"]),
                             int(v["magnitude"])) for v in r if v["magnitude"] > 0][:3])

@@ -138,3 +138,54 @@ def test_correlator_flow_tracks_a_planted_signal(oc):
         counts.append(int(st[0]["count"]))
     assert 295 <= counts[-1] <= 302
     assert st[0]["active"] == 1
+
+
+# ---- sample front end (SDR/objects/gps_source.cpp:684-767, :933-943; misc.cpp:174-197)
+def test_downsample_oracle_golden():
+    f = np.load(os.path.join(GOLD, "sdr_frontend.npz"))
+    o = S.OracleSDR()
+    for src, out, (fs, n, k) in zip(f["src"], f["out"], f["rates"]):
+        n, k = int(n), int(k)
+        got = o.downsample(src[:n], 2.048e6, fs)
+        assert got.shape[0] == k and np.array_equal(got, out[:k]), fs
+
+
+def test_downsample_count_closed_form():
+    import gnsscorr
+    o = S.OracleSDR()
+    rng = np.random.default_rng(2)
+    for fs in (2.1e6, 4.0e6, 4.096e6, 5.0e6, 8.0e6, 16.368e6):
+        for n in (1, 2, 7, 4000, 4096, 16368):
+            src = rng.integers(-5, 5, (n, 2)).astype(np.int16)
+            assert gnsscorr.SdrFeCtx.downsample_count(n, 2.048e6, fs) == \
+                o.downsample(src, 2.048e6, fs).shape[0], (fs, n)
+
+
+@pytest.mark.skipif(not S.have_ref(), reason="reference build needs /root/reference")
+def test_downsample_oracle_vs_reference():
+    o, r = S.OracleSDR(), S.RefSDR()
+    rng = np.random.default_rng(4)
+    for fs in (3.0e6, 4.0e6, 6.5536e6, 16.0e6):
+        src = rng.integers(-30000, 30000, (int(fs / 1000) * 2, 2)).astype(np.int16)
+        assert np.array_equal(o.downsample(src, 2.048e6, fs), r.downsample(src, 2.048e6, fs))
+
+
+def test_gn3s_oracle_vs_product_table():
+    """The oracle's double-product path equals the library's int16 product table
+    indexed by (2-bit code, phase >> 22); resample picks floor((i+1)*4000/2048)."""
+    import gnsscorr
+    o = S.OracleSDR()
+    prod = gnsscorr.gn3s_products()
+    rng = np.random.default_rng(7)
+    raw = rng.integers(0, 256, 2 * 20000, dtype=np.uint8)
+    ph0 = 987654321
+    out, ph = o.gn3s(raw, ph0)
+    n = np.arange(2 * 20000, dtype=np.uint64)
+    phases = ((ph0 + n * 2557223528) % (1 << 32)) >> 22
+    mixed = prod[raw & 3, phases.astype(np.int64)].reshape(2, 20000, 2)
+    idx = ((np.arange(10240) + 1) * 4000) // 2048
+    for b in range(2):
+        ok = idx < 20000
+        assert np.array_equal(out.reshape(2, 10240, 2)[b][ok], mixed[b][idx[ok]])
+        assert (out.reshape(2, 10240, 2)[b][~ok] == 0).all()
+    assert ph == (ph0 + 2 * 20000 * 2557223528) % (1 << 32)

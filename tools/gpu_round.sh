@@ -28,5 +28,5 @@ for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc/p$i -o run -- $B > $O/pmc/p$i.log 2>&1
   echo "pmc pass $i ok"
 done
-python tools/pmc_summary.py $O/pmc $O/pmc_summary.json
+python tools/pmc_summary.py $O/pmc $O/pmc_summary.json --traffic $O/pmc_traffic.json
 echo "== done"
