@@ -268,6 +268,7 @@ def run_fullsky(dist, dev, steps, warmup):
 
 SDR_REC, SDR_SV, SDR_ROWS, SDR_N = 64, 32, 120, 2048
 SDR_CORR_CH = 4096
+SDR_FE_BLOCKS = 2000         # GN3S 5-ms reads per front-end launch (10 s of 4 Msps 2-bit samples)
 
 
 def run_sdr(dist, dev, steps, warmup):
@@ -319,8 +320,26 @@ def run_sdr(dist, dev, steps, warmup):
     corr.sync()
     dt_corr = dist.max(time.perf_counter() - t0)
     ms_corr = e0.elapsed_ms(e1) / steps
+    # sample front end: GN3S 2-bit packed bytes -> 2.048 Msps CPX, SDR_FE_BLOCKS x 5 ms
+    fe = gc.SdrFeCtx(device=dev)
+    d_fi = gc.DevBuf(SDR_FE_BLOCKS * gc.GN3S_BLOCK_IN // 4, dev)
+    d_fi.fill_if2(0x5EED0008 + dist.rank)
+    d_fo = gc.DevBuf(SDR_FE_BLOCKS * gc.GN3S_BLOCK_OUT * 4, dev)
+    ph = 0
+    for _ in range(warmup):
+        ph = fe.gn3s_dev(d_fi.ptr, True, SDR_FE_BLOCKS, ph, d_fo.ptr)
+    fe.sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    e0.record(fe.stream)
+    for _ in range(steps):
+        ph = fe.gn3s_dev(d_fi.ptr, True, SDR_FE_BLOCKS, ph, d_fo.ptr)
+    e1.record(fe.stream)
+    fe.sync()
+    dt_fe = dist.max(time.perf_counter() - t0)
+    ms_fe = e0.elapsed_ms(e1) / steps
     return dict(dt_acq=dt_acq, ms_acq=ms_acq, dt_corr=dt_corr, ms_corr=ms_corr, steps=steps,
-                bufs=bufs)
+                bufs=bufs, dt_fe=dt_fe, ms_fe=ms_fe)
 
 
 def cpu_baseline_sdr(bufs, budget_s=5.0):
@@ -532,6 +551,21 @@ def main():
                 "config": f"{SDR_CORR_CH} channels x one 2048-sample packet per launch "
                           "(wipe-off row + 3 code rows from the HBM-resident pre-sampled tables)",
                 "kernel_ms_per_launch": sdr["ms_corr"],
+            }
+            fe_in = SDR_FE_BLOCKS * gc.GN3S_BLOCK_IN
+            fe_bytes = fe_in // 4 + SDR_FE_BLOCKS * gc.GN3S_BLOCK_OUT * 4
+            out["sdr_frontend"] = {
+                "metric": "input samples/sec (GPS-SDR GN3S 2-bit unpack + NCO mix + resample, "
+                          "bit-exact)",
+                "value": fe_in * sdr["steps"] * W / sdr["dt_fe"], "unit": "samples/s",
+                "config": f"{SDR_FE_BLOCKS} x 5-ms GN3S reads (packed 2-bit, 4 Msps) -> "
+                          f"{SDR_FE_BLOCKS * 5} packets of 2048 CPX per launch",
+                "kernel_ms_per_launch": sdr["ms_fe"],
+                "realtime_streams_per_gpu": SDR_FE_BLOCKS * 5e-3 / (sdr["ms_fe"] * 1e-3),
+                "roofline": {"bound": "hbm", "achieved": fe_bytes / (sdr["ms_fe"] * 1e-3) / 1e9,
+                             "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": fe_bytes / (sdr["ms_fe"] * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                             "traffic": pmc_traffic("gn3s_kernel")},
             }
         if W == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_acq(acq["meta"])
