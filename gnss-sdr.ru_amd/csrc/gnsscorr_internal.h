@@ -22,6 +22,7 @@ extern "C" {
 void gnsscorr_osg_table_image(int8_t *img);
 void gnsscorr_osg_packed_table(uint32_t *pk);
 void gnsscorr_set_error(const char *fmt, ...);
+int gnsscorr_track_iq(const gnsscorr_track_ctx *ctx);
 /* GPS-SDR tables (sdr_host.c): packed (i, q) int16 pairs, N = 2048 */
 void gnsscorr_sdr_twiddles(int16_t *w, int16_t *iw);
 void gnsscorr_sdr_code_gen(int sv, uint8_t *chips);

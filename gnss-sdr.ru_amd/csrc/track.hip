@@ -364,6 +364,8 @@ struct gnsscorr_track_ctx {
   int64_t tic = 0, tic_ref = 0;
 };
 
+extern "C" int gnsscorr_track_iq(const gnsscorr_track_ctx* ctx) { return ctx && ctx->cfg.iq; }
+
 static int set_dev(int dev) {
   HIP_TRY(hipSetDevice(dev));
   return GNSSCORR_OK;

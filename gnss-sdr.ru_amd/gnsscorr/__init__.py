@@ -41,6 +41,22 @@ SIG = np.dtype([("system", "<i4"), ("prn", "<i4"), ("fch", "<i4"), ("data_bits",
 assert NCO_CMD.itemsize == 24 and CHAN_STATE.itemsize == 56 and TRACK_RESULT.itemsize == 64
 assert ACQ_ROW.itemsize == 16 and ACQ_RESULT.itemsize == 32 and SIG.itemsize == 48
 
+OSG_LOOP = np.dtype([("state", "<i4"), ("n_freq", "<i4"), ("i_confirm", "<i4"),
+                     ("n_thresh", "<i4"), ("codes", "<i4"), ("del_freq", "<i4"),
+                     ("sign_pos", "<i4"), ("prev_sign_pos", "<i4"), ("sign_count", "<i4"),
+                     ("ms_count", "<i4"), ("ms_set", "<i4"), ("search_max_prn_delay", "<i4"),
+                     ("search_max_f", "<i4"), ("cn0", "<i4"), ("bit", "<i4"), ("exited", "<i4"),
+                     ("accum", "<i2", (6,)), ("prev_accum", "<i2", (6,)),
+                     ("early_mag", "<i8"), ("prompt_mag", "<i8"), ("late_mag", "<i8"),
+                     ("cross", "<i8"), ("dot", "<i8"), ("carr_error", "<i8"),
+                     ("old_carr_error", "<i8"), ("freq_error", "<i8"), ("carr_nco", "<i8"),
+                     ("old_carr_nco", "<i8"), ("carr_freq", "<i8"), ("carr_freq_basis", "<i8"),
+                     ("code_error", "<i8"), ("old_code_error", "<i8"), ("code_freq", "<i8"),
+                     ("code_freq_basis", "<i8"), ("code_nco", "<i8"), ("old_code_nco", "<i8"),
+                     ("ch_time", "<i8"), ("carrier_freq", "<i8"), ("carrier_cold_corr", "<i8"),
+                     ("ms_sign", "<u8")])
+assert OSG_LOOP.itemsize == 264
+
 SGT_CHAN = np.dtype([("code_id", "<i4"), ("stream", "<i4"), ("status", "<i4"),
                      ("n_epochs", "<i4"), ("pos", "<i8"), ("pad", "<i8"),
                      ("rem_code", "<f8"), ("rem_carr", "<f8"), ("code_freq", "<f8"),
@@ -124,6 +140,8 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sdr_gn3s_products", "gnsscorr_sdr_fe_create", "gnsscorr_sdr_fe_destroy",
     "gnsscorr_sdr_gn3s_dev", "gnsscorr_sdr_gn3s", "gnsscorr_sdr_downsample_count",
     "gnsscorr_sdr_downsample_dev", "gnsscorr_sdr_fe_sync", "gnsscorr_sdr_fe_stream",
+    "gnsscorr_osg_loop_cfg_init", "gnsscorr_osg_loop_reset", "gnsscorr_osg_isr_dev",
+    "gnsscorr_osg_closed_loop_dev",
     "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
     "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
     "gnsscorr_event_elapsed_ms", "gnsscorr_event_destroy", "gnsscorr_dev_fill_if2",
@@ -200,6 +218,11 @@ def lib() -> C.CDLL:
         "gnsscorr_sdr_corr_sync": (I, [P]),
         "gnsscorr_sdr_corr_stream": (P, [P]),
         "gnsscorr_sdr_gn3s_products": (None, [P]),
+        "gnsscorr_osg_loop_cfg_init": (None, [P, D, D, D, I, I, D, C.c_long, C.c_long, C.c_long,
+                                              C.c_long, C.c_long, I]),
+        "gnsscorr_osg_loop_reset": (None, [P, I, P, P, P]),
+        "gnsscorr_osg_isr_dev": (I, [P, P, I, P, P, P]),
+        "gnsscorr_osg_closed_loop_dev": (I, [P, P, P, I64, I64, I, I, P, P, P, P]),
         "gnsscorr_sdr_fe_create": (I, [C.POINTER(P), I]),
         "gnsscorr_sdr_fe_destroy": (I, [P]),
         "gnsscorr_sdr_gn3s_dev": (I, [P, P, I, I, C.POINTER(C.c_uint32), C.c_uint32, P]),
@@ -633,6 +656,47 @@ class SdrAcqCtx:
     @property
     def stream(self) -> int:
         return lib().gnsscorr_sdr_acq_stream(self.h)
+
+
+class OsgLoopCfg(C.Structure):
+    _fields_ = [("carrier_ref", C.c_int64), ("code_ref", C.c_int64), ("d_freq", C.c_int64),
+                ("fll_i1", C.c_int32), ("fll_i2", C.c_int32), ("fll_i3", C.c_int32),
+                ("dll_i1", C.c_int32), ("dll_i2", C.c_int32), ("acq_thresh", C.c_int32),
+                ("confirm_m", C.c_int32), ("n_of_m_thresh", C.c_int32),
+                ("carrier_shift", C.c_int32), ("code_shift", C.c_int32),
+                ("clock_mult", C.c_double)]
+
+
+def osg_loop_cfg(samp_rate=16.0e6, gps_if=2.42e6, clock_mult=5.0, carrier_bits=30, code_bits=29,
+                 bin_width=1000.0, bnp=25, bnf=1400, bnd=2, fll_t_ms=1, dll_t_ms=1,
+                 acq_thresh=1800) -> OsgLoopCfg:
+    """Receiver loop constants as the reference derives them (globals.h defaults)."""
+    cfg = OsgLoopCfg()
+    lib().gnsscorr_osg_loop_cfg_init(C.byref(cfg), samp_rate, gps_if, clock_mult, carrier_bits,
+                                     code_bits, bin_width, bnp, bnf, bnd, fll_t_ms, dll_t_ms,
+                                     acq_thresh)
+    return cfg
+
+
+def osg_loop_reset(cfg: OsgLoopCfg, prns):
+    """Start state of every channel (reset_all_correlator_channles) -> (loops, cmds)."""
+    prns = np.ascontiguousarray(prns, np.int32)
+    loops = np.zeros(len(prns), OSG_LOOP)
+    cmds = np.zeros(len(prns), NCO_CMD)
+    lib().gnsscorr_osg_loop_reset(C.byref(cfg), len(prns), _ptr(prns), _ptr(loops), _ptr(cmds))
+    return loops, cmds
+
+
+def osg_isr_dev(track: "TrackCtx", cfg: OsgLoopCfg, n_ch, d_loops, d_cmds, d_res):
+    _check(lib().gnsscorr_osg_isr_dev(track.h, C.byref(cfg), n_ch, d_loops, d_cmds, d_res),
+           "gnsscorr_osg_isr_dev")
+
+
+def osg_closed_loop_dev(track: "TrackCtx", cfg: OsgLoopCfg, d_if, stream_stride, nsamp, n_calls,
+                        n_ch, d_loops, d_cmds, d_res_hist, d_loop_hist=None):
+    _check(lib().gnsscorr_osg_closed_loop_dev(track.h, C.byref(cfg), d_if, stream_stride, nsamp,
+                                              n_calls, n_ch, d_loops, d_cmds, d_res_hist,
+                                              d_loop_hist), "gnsscorr_osg_closed_loop_dev")
 
 
 GN3S_BLOCK_IN, GN3S_BLOCK_OUT, GN3S_STEP = 20000, 10240, 2557223528

@@ -134,6 +134,73 @@ int gnsscorr_track_sync(gnsscorr_track_ctx *ctx);
 void *gnsscorr_track_stream(gnsscorr_track_ctx *ctx);
 
 /* ======================================================================
+ * OSG channel loops on the GPU, bit-exact with gpsisr
+ * (osgnss_next_step/src/isr/osgpsisr.c:360-768): per dump, the acquisition /
+ * n-of-m confirm / FLL-assisted-PLL + DLL pull-in / tracking state machine in
+ * the reference's fixed-point arithmetic (rss, fix_atan2, sqrt_newton, long =
+ * int64), writing the next call's NCO words, slew and epoch load straight into
+ * the device command array.  With gnsscorr_track_dev this closes the loop on
+ * the GPU: no host round trip per 512-us interrupt.
+ * ==================================================================== */
+typedef struct {          /* tracking_channel (OSG/include/structs.h:86-131), loop fields */
+  int32_t state;          /* 0 off, 1 acquisition, 2 confirm, 3 pull-in, 4 tracking */
+  int32_t n_freq, i_confirm, n_thresh, codes, del_freq;
+  int32_t sign_pos, prev_sign_pos, sign_count, ms_count, ms_set;
+  int32_t search_max_prn_delay, search_max_f;
+  int32_t cn0, bit;       /* char in the reference                               */
+  int32_t exited;         /* 1: a dump reached CHANNEL_OFF (the reference exit(0)s) */
+  int16_t accum[6];       /* struct accum order: iP qP iL qL iE qE (short)       */
+  int16_t prev_accum[6];
+  int64_t early_mag, prompt_mag, late_mag;            /* accum_mean            */
+  int64_t cross, dot, carr_error, old_carr_error, freq_error;
+  int64_t carr_nco, old_carr_nco, carr_freq, carr_freq_basis;
+  int64_t code_error, old_code_error, code_freq, code_freq_basis, code_nco, old_code_nco;
+  int64_t ch_time, carrier_freq, carrier_cold_corr;
+  uint64_t ms_sign;
+} gnsscorr_osg_loop;      /* 264 bytes */
+
+typedef struct {          /* receiver constants the loops read (globals.h, init code) */
+  int64_t carrier_ref, code_ref, d_freq;   /* gps_carrier_ref, gps_code_ref, d_freq */
+  int32_t fll_i1, fll_i2, fll_i3;          /* FLL_a_PLL_i1..3                   */
+  int32_t dll_i1, dll_i2;                  /* DLL_i1, DLL_i2                    */
+  int32_t acq_thresh;                      /* acq_thresh (globals.h:38)         */
+  int32_t confirm_m, n_of_m_thresh;        /* CONFIRM_M, N_OF_M_THRESH           */
+  int32_t carrier_shift, code_shift;       /* MAX_DIGIT - {CARRIER,CODE}_NCO bits */
+  double  clock_mult;                      /* SYSTEM_CLOCK_MULTIPLIER (double)  */
+} gnsscorr_osg_loop_cfg;
+
+/* Constants as the reference computes them at start-up: correlator_init
+ * (correlator.c:110-121) and osgnss_next_step.c:391-399 (calc_* / convert_*,
+ * osgpsisr.c:213-330).  Defaults of globals.h: fs 16e6, IF 2.42e6, clock x5,
+ * NCO bits 30/29, bin 1000 Hz, Bnp 25, Bnf 1400, Bnd 2, 1 ms, acq_thresh 1800. */
+void gnsscorr_osg_loop_cfg_init(gnsscorr_osg_loop_cfg *cfg, double samp_rate, double gps_if,
+                                double clock_mult, int carrier_nco_bits, int code_nco_bits,
+                                double bin_width, long bnp, long bnf, long bnd, long fll_t_ms,
+                                long dll_t_ms, int acq_thresh);
+/* The start state of osgnss_next_step.c:73-84 (reset_all_correlator_channles):
+ * acquisition, n_freq 0, del_freq 1, 2045 half-chip delays, +-5 bins; cmds get
+ * the PRN, the reference carrier/code words, no slew, no epoch load. */
+void gnsscorr_osg_loop_reset(const gnsscorr_osg_loop_cfg *cfg, int n_ch, const int32_t *prns,
+                             gnsscorr_osg_loop *loops, gnsscorr_nco_cmd *cmds);
+/* One interrupt's channel processing after a gnsscorr_track_dev call that used
+ * d_cmds and wrote d_res: register bookkeeping of the call (epoch load
+ * consumed, slew cleared by a dump), then gpsisr for every channel that dumped.
+ * Updates d_loops and d_cmds in place for the next call.  Asynchronous on the
+ * tracking context's stream. */
+int gnsscorr_osg_isr_dev(gnsscorr_track_ctx *ctx, const gnsscorr_osg_loop_cfg *cfg, int n_ch,
+                         gnsscorr_osg_loop *d_loops, gnsscorr_nco_cmd *d_cmds,
+                         const gnsscorr_track_result *d_res);
+/* n_calls closed-loop interrupts: for k in 0..n_calls-1, gnsscorr_track_dev on
+ * IF d_if + k*nsamp samples (every stream), then gnsscorr_osg_isr_dev.  The
+ * per-call results (n_calls * n_ch) and loop states (optional, may be NULL)
+ * are recorded for inspection.  Asynchronous. */
+int gnsscorr_osg_closed_loop_dev(gnsscorr_track_ctx *ctx, const gnsscorr_osg_loop_cfg *cfg,
+                                 const int8_t *d_if, int64_t stream_stride, int64_t nsamp,
+                                 int n_calls, int n_ch, gnsscorr_osg_loop *d_loops,
+                                 gnsscorr_nco_cmd *d_cmds, gnsscorr_track_result *d_res_hist,
+                                 gnsscorr_osg_loop *d_loop_hist);
+
+/* ======================================================================
  * Parallel code-phase acquisition (SoftGNSS acquisition.sci semantics)
  * Replaces: GPS  POSTPROCESSING_SCILAB_RECEIVERS/GPS/L1/acquisition.sci:46-192
  *           GLO  POSTPROCESSING_SCILAB_RECEIVERS/GLONASS/L1/acquisition.sci:46-198
