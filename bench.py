@@ -462,9 +462,10 @@ def main():
     ap.add_argument("--skip-track", action="store_true")
     a = ap.parse_args()
     dist = Dist()
-    dev = dist.local
-    if gc.device_count() < 1:
+    n_dev = gc.device_count()
+    if n_dev < 1:
         raise SystemExit("bench.py: no HIP device visible")
+    dev = dist.local % n_dev     # one rank per GPU; wraps only when rehearsing on fewer GPUs
 
     acq = run_acq(dist, dev, a.steps, a.warmup)
     trk = None if a.skip_track else run_track(dist, dev, max(a.steps, 20), a.warmup)
