@@ -26,6 +26,7 @@ int gnsscorr_track_iq(const gnsscorr_track_ctx *ctx);
 /* GPS-SDR tables (sdr_host.c): packed (i, q) int16 pairs, N = 2048 */
 void gnsscorr_sdr_twiddles(int16_t *w, int16_t *iw);
 void gnsscorr_sdr_code_gen(int sv, uint8_t *chips);
+void gnsscorr_sdr_post_dft(int16_t *out);
 #ifdef __cplusplus
 }
 #endif

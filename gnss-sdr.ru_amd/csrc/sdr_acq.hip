@@ -23,6 +23,16 @@
 // All arithmetic is the reference's int16/int32 with its wrap points; butterflies
 // of one rank are independent, so only the rank order has to be kept.
 // Roofline: integer VALU + LDS (each rank = 2048 LDS reads/writes of 4 B).
+//
+// Medium / weak acquisition (acquisition.cpp:309-570), same arithmetic:
+//   sdr_prep_rows_kernel  doPrepIF at 1/10/310 ms into a per-record persistent
+//                         row store (the object's baseband_rows member)
+//   sdr_coh_kernel<WEAK>  one 1024-thread workgroup per (record, sv, row): ten
+//                         1-ms inverse FFTs at once in LDS (80 KiB), the
+//                         post-correlation DFT per delay column (v_dot2 =
+//                         sse_cacc's pmaddwd), x86_cmag, and for weak the 15
+//                         code-Doppler-shifted non-coherent sums in registers
+//   sdr_select_mw_kernel  the strict-greater scan of doAcqMedium / doAcqWeak
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -68,28 +78,36 @@ __device__ __forceinline__ uint32_t cmulsc(uint32_t a, uint32_t b, int shift, bo
 
 __device__ __forceinline__ int brev11(int k) { return (int)(__brev((uint32_t)k) >> 21); }
 
-// 11 radix-2 DIT ranks in LDS (fft.cpp:156-180 with the rank/bfly loops of :314-334)
+// one radix-2 DIT butterfly of rank r with the reference's wrap points
+// (fft.cpp:403-441: optional >>1 pre-scaling, (b*w + 8192) >> 14, int16 sums)
+__device__ __forceinline__ void bfly(uint32_t* x, int a, int b, int32_t wi, int32_t wq, bool scale) {
+  const uint32_t A = x[a], B = x[b];
+  int16_t ai = lo16(A), aq = hi16(A), bi0 = lo16(B), bq0 = hi16(B);
+  if (scale) { ai >>= 1; aq >>= 1; bi0 >>= 1; bq0 >>= 1; }
+  int32_t bi = (int32_t)bi0 * wi - (int32_t)bq0 * wq;
+  int32_t bq = (int32_t)bi0 * wq + (int32_t)bq0 * wi;
+  bi = (bi + 8192) >> 14;
+  bq = (bq + 8192) >> 14;
+  x[b] = pack((int16_t)(ai - (int16_t)bi), (int16_t)(aq - (int16_t)bq));
+  x[a] = pack((int16_t)(ai + (int16_t)bi), (int16_t)(aq + (int16_t)bq));
+}
+
+// 11 radix-2 DIT ranks in LDS (fft.cpp:156-180 with the rank/bfly loops of
+// :314-334) over F independent transforms at x + f*kN, T threads; each thread
+// applies its butterflies to all F transforms (one twiddle load per F).
 // tw: packed (c, s) Q14 twiddles, 1024 entries, forward or inverse
+template <int T, int F>
 __device__ void dit_ranks(uint32_t* x, const uint32_t* tw, uint32_t scale_mask) {
   for (int r = 0; r < kM; r++) {
     const bool scale = (scale_mask >> r) & 1u;
 #pragma unroll
-    for (int u = 0; u < (kN / 2) / kThreads; u++) {
-      const int t = threadIdx.x + u * kThreads;
+    for (int u = 0; u < (kN / 2) / T; u++) {
+      const int t = threadIdx.x + u * T;
       const int j = t & ((1 << r) - 1);
       const int a = ((t >> r) << (r + 1)) + j;
-      const int b = a + (1 << r);
       const uint32_t w = tw[j << (kM - 1 - r)];
-      const int32_t wi = lo16(w), wq = hi16(w);
-      const uint32_t A = x[a], B = x[b];
-      int16_t ai = lo16(A), aq = hi16(A), bi0 = lo16(B), bq0 = hi16(B);
-      if (scale) { ai >>= 1; aq >>= 1; bi0 >>= 1; bq0 >>= 1; }
-      int32_t bi = (int32_t)bi0 * wi - (int32_t)bq0 * wq;
-      int32_t bq = (int32_t)bi0 * wq + (int32_t)bq0 * wi;
-      bi = (bi + 8192) >> 14;
-      bq = (bq + 8192) >> 14;
-      x[b] = pack((int16_t)(ai - (int16_t)bi), (int16_t)(aq - (int16_t)bq));
-      x[a] = pack((int16_t)(ai + (int16_t)bi), (int16_t)(aq + (int16_t)bq));
+#pragma unroll
+      for (int f = 0; f < F; f++) bfly(x + f * kN, a, a + (1 << r), lo16(w), hi16(w), scale);
     }
     __syncthreads();
   }
@@ -107,7 +125,7 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_kernel(
   for (int k = threadIdx.x; k < kN; k += kThreads)
     x[brev11(k)] = cmulsc(src[k], wp[k], 14, saturate != 0);   // + doShuffle
   __syncthreads();
-  dit_ranks(x, tw, 0u);                                         // R1: no scaling
+  dit_ranks<kThreads, 1>(x, tw, 0u);                                         // R1: no scaling
   uint32_t* dst = X + ((size_t)rec * 4 + j) * kN;
   for (int k = threadIdx.x; k < kN; k += kThreads) dst[k] = x[k];
 }
@@ -130,7 +148,7 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
   for (int k = threadIdx.x; k < kN; k += kThreads)
     x[brev11(k)] = cmulsc(xr[(k + lcv) & (kN - 1)], cr[k], 10, saturate != 0);
   __syncthreads();
-  dit_ranks(x, tw, kR2);
+  dit_ranks<kThreads, 1>(x, tw, kR2);
   // x86_cmag (int32 wrap) + x86_max (first index of the strict maximum, > 0)
   int32_t best = 0, idx = 0;
   for (int k = threadIdx.x; k < kN; k += kThreads) {
@@ -181,6 +199,184 @@ __global__ void sdr_select_kernel(const int2* __restrict__ row_out, const int32_
   res[g] = r;
 }
 
+// ---------------------------------------------------------------------------
+// Medium / weak acquisition (acquisition.cpp:309-570)
+// ---------------------------------------------------------------------------
+constexpr int kStoreRows = 1240;      // baseband_rows (acquisition.cpp:107-110)
+constexpr int kWipe = 10 * kN;        // 10-ms wipe-off tables, repeated (:123-137)
+constexpr int kCoh = 1024;            // threads of the coherent kernels
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int32_t dot2(uint32_t a, uint32_t b, int32_t c) {
+  // a.i*b.lo + a.q*b.hi + c in int32 (wrap): one pmaddwd half of sse_cacc
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a), __builtin_bit_cast(short2_t, b),
+                                c, false);
+}
+
+// doPrepIF for ms = 1, 10 or 310 ms (acquisition.cpp:191-236): one workgroup
+// per (record, row r = j*ms + m): 1-ms block m mixed by the (-fif - 250 j)
+// wipe-off at table offset (m % 10)*2048, forward FFT, stored as row r of the
+// record's persistent row store.  Rows >= 4*ms are left as they are.
+__global__ __launch_bounds__(kThreads) void sdr_prep_rows_kernel(
+    const uint32_t* __restrict__ buff, int ms, const uint32_t* __restrict__ wipe10,
+    const uint32_t* __restrict__ tw_fwd, uint32_t* __restrict__ store, int saturate) {
+  __shared__ uint32_t x[kN];
+  __shared__ uint32_t tw[kN / 2];
+  const int nr = 4 * ms;
+  const int rec = blockIdx.x / nr, r = blockIdx.x % nr, j = r / ms, m = r % ms;
+  const uint32_t* src = buff + ((size_t)rec * ms + m) * kN;
+  const uint32_t* wp = wipe10 + (size_t)j * kWipe + (size_t)(m % 10) * kN;
+  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_fwd[k];
+  for (int k = threadIdx.x; k < kN; k += kThreads)
+    x[brev11(k)] = cmulsc(src[k], wp[k], 14, saturate != 0);
+  __syncthreads();
+  dit_ranks<kThreads, 1>(x, tw, 0u);
+  uint32_t* dst = store + ((size_t)rec * kStoreRows + r) * kN;
+  for (int k = threadIdx.x; k < kN; k += kThreads) dst[k] = x[k];
+}
+
+__device__ __forceinline__ int weak_shift(int i, int lcv, int lcv2) {
+#pragma clang fp contract(off)
+  // acquisition.cpp:483-489: (double)i*.02*IF_SAMPLE_FREQUENCY*doppler/L1
+  const double doppler = (double)(lcv * 1000) + (double)(float)(lcv2 * 250);
+  const double cd = (double)i * .02 * 2048000.0 * doppler / 1.57542e9;
+  return (int)floor(cd);
+}
+
+__device__ __forceinline__ void better(int32_t v, int32_t i, int32_t& best, int32_t& idx) {
+  if (v > best || (v == best && i < idx)) { best = v; idx = i; }
+}
+
+// One workgroup per (record, sv, row).  Medium: row = (lcv - lmin)*4 + lcv2,
+// one pass over store rows lcv2*20 + m (acquisition.cpp:338-345, the 20-row
+// stride of the reference).  Weak: row = ((lcv - lmin)*4 + lcv2)*2 + k, 15
+// passes i over rows lcv2*310 + i*20 + k*10 + m (:466-479).  A pass: the ten
+// 1-ms rows read circularly from offset lcv, cmulsc by the PRN spectrum
+// (shift 10 / 9), ten inverse FFTs at once in LDS (R2 scaling); then each
+// delay column's post-correlation DFT against the 10 dft rows (sse_cacc as
+// v_dot2 pairs, >> 16 to int16, :363-373) and x86_cmag.  Medium keeps the
+// first strict maximum over the 10 x 2048 powers; weak adds the powers into
+// per-thread int32 accumulators at column (c + shift) mod 2048 (:521-534),
+// where a thread owns output columns tid and tid + 1024, and takes the
+// maximum after the 15 passes.  Out: (max, flat index j*2048 + column).
+template <bool WEAK>
+__global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
+    const uint32_t* __restrict__ store, const uint32_t* __restrict__ codes,
+    const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ dft,
+    const int32_t* __restrict__ svs, int n_sv, int lmin, int n_rows, int saturate,
+    int2* __restrict__ row_out) {
+  __shared__ uint32_t coh[10 * kN];
+  __shared__ uint32_t tw[kN / 2];
+  __shared__ uint32_t dw[200];
+  __shared__ int2 red[kCoh / 64];
+  const int row = blockIdx.x % n_rows;
+  const int s = (blockIdx.x / n_rows) % n_sv;
+  const int rec = blockIdx.x / (n_rows * n_sv);
+  const int lcv = lmin + (WEAK ? row >> 3 : row >> 2);
+  const int lcv2 = WEAK ? (row >> 1) & 3 : row & 3;
+  const int kk = WEAK ? row & 1 : 0;
+  for (int k = threadIdx.x; k < kN / 2; k += kCoh) tw[k] = tw_inv[k];
+  if (threadIdx.x < 200) dw[threadIdx.x] = dft[threadIdx.x];
+  const uint32_t* cr = codes + (size_t)svs[s] * kN;
+  const uint32_t* rb = store + (size_t)rec * kStoreRows * kN;
+  const bool sat = saturate != 0;
+  uint32_t acc[2][10];
+#pragma unroll
+  for (int q = 0; q < 2; q++)
+#pragma unroll
+    for (int j = 0; j < 10; j++) acc[q][j] = 0;
+  int32_t best = 0, idx = 0;
+  constexpr int kPasses = WEAK ? 15 : 1;
+  for (int i = 0; i < kPasses; i++) {
+    const int row0 = WEAK ? lcv2 * 310 + i * 20 + kk * 10 : lcv2 * 20;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int k = threadIdx.x + q * kCoh;
+      const uint32_t cv = cr[k];
+      const int src = (k + lcv) & (kN - 1);
+      const int dst = brev11(k);
+#pragma unroll
+      for (int m = 0; m < 10; m++)
+        coh[m * kN + dst] = cmulsc(rb[(size_t)(row0 + m) * kN + src], cv, WEAK ? 9 : 10, sat);
+    }
+    __syncthreads();
+    dit_ranks<kCoh, 10>(coh, tw, kR2);
+    const int shift = WEAK ? weak_shift(i, lcv, lcv2) : 0;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int c_out = threadIdx.x + q * kCoh;
+      const int c_in = (c_out - shift) & (kN - 1);
+      uint32_t d[10];
+#pragma unroll
+      for (int m = 0; m < 10; m++) d[m] = coh[m * kN + c_in];
+#pragma unroll 2
+      for (int j = 0; j < 10; j++) {
+        int32_t ia = 0, qa = 0;
+#pragma unroll
+        for (int m = 0; m < 10; m++) {
+          ia = dot2(d[m], dw[(j * 10 + m) * 2], ia);
+          qa = dot2(d[m], dw[(j * 10 + m) * 2 + 1], qa);
+        }
+        const int32_t ti = (int16_t)(ia >> 16), tq = (int16_t)(qa >> 16);
+        const uint32_t p = (uint32_t)(ti * ti) + (uint32_t)(tq * tq);
+        if (WEAK) acc[q][j] += p;
+        else better((int32_t)p, j * kN + c_out, best, idx);
+      }
+    }
+    if (WEAK) __syncthreads();   // coh is rewritten by the next pass
+  }
+  if (WEAK) {
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+#pragma unroll
+      for (int j = 0; j < 10; j++) better((int32_t)acc[q][j], j * kN + threadIdx.x + q * kCoh, best, idx);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int32_t ob = __shfl_xor(best, o, 64), oi = __shfl_xor(idx, o, 64);
+    better(ob, oi, best, idx);
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = make_int2(best, idx);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int2 r = red[0];
+    for (int w = 1; w < kCoh / 64; w++) {
+      const int2 o = red[w];
+      if (o.x > r.x || (o.x == r.x && o.y < r.y)) r = o;
+    }
+    if (r.x <= 0) r = make_int2(0, 0);
+    row_out[blockIdx.x] = r;
+  }
+}
+
+// per (record, sv): strict-greater scan over the rows in the reference's loop
+// order (lcv, lcv2[, k]); code_phase = index % 2048 and doppler = lcv*1000 +
+// lcv2*250 + (index / 2048)*25 (acquisition.cpp:397-405, :543-551)
+__global__ void sdr_select_mw_kernel(const int2* __restrict__ row_out,
+                                     const int32_t* __restrict__ svs, int n_sv, int n_rec,
+                                     int lmin, int n_rows, int weak,
+                                     gnsscorr_sdr_acq_result* __restrict__ res) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_rec * n_sv) return;
+  const int2* rr = row_out + (size_t)g * n_rows;
+  gnsscorr_sdr_acq_result r = {};
+  r.sv = svs[g % n_sv];
+  int32_t mag = 0;
+  for (int row = 0; row < n_rows; row++) {
+    const int2 v = rr[row];
+    if (v.x > mag) {
+      mag = v.x;
+      const int lcv = lmin + (weak ? row >> 3 : row >> 2), lcv2 = weak ? (row >> 1) & 3 : row & 3;
+      r.code_phase = v.y % kN;
+      r.doppler = lcv * 1000 + lcv2 * 250 + (v.y / kN) * 25;
+      r.magnitude = (uint32_t)v.x;
+      r.row = row;
+    }
+  }
+  r.success = r.magnitude > 0u;   // THRESH_MEDIUM = THRESH_WEAK = 0 (config.h:73-74)
+  res[g] = r;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -195,14 +391,18 @@ struct gnsscorr_sdr_acq_ctx {
   int2* d_rows = nullptr;
   gnsscorr_sdr_acq_result* d_res = nullptr;
   size_t cap_rec = 0, cap_rows = 0, cap_sv = 0;
+  // medium / weak: 10-ms wipe-offs, post-correlation DFT rows, and the
+  // per-record persistent baseband_rows store (kStoreRows x 2048 CPX)
+  uint32_t *d_wipe10 = nullptr, *d_dft = nullptr, *d_store = nullptr;
+  size_t store_rec = 0;
 };
 
 extern "C" int gnsscorr_sdr_acq_destroy(gnsscorr_sdr_acq_ctx* c) {
   if (!c) return GNSSCORR_OK;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ps[] = {c->d_wipe, c->d_codes, c->d_twf, c->d_twi, c->d_X,
-                c->d_buff, c->d_svs,   c->d_rows, c->d_res};
+  void* ps[] = {c->d_wipe, c->d_codes, c->d_twf,    c->d_twi, c->d_X,    c->d_buff,
+                c->d_svs,  c->d_rows,  c->d_res, c->d_wipe10, c->d_dft, c->d_store};
   for (void* p : ps) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -228,12 +428,16 @@ extern "C" int gnsscorr_sdr_acq_create(gnsscorr_sdr_acq_ctx** out, const gnsscor
   // PRN spectra (gen_fft_codes.m)
   uint32_t* h = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(4 * kN + 51 * kN + kN));
   int16_t* tmp = (int16_t*)malloc(sizeof(int16_t) * 2 * (size_t)51 * kN);
-  int rc = (h && tmp) ? GNSSCORR_OK : GNSSCORR_ENOMEM;
+  uint32_t* w10 = (uint32_t*)malloc(sizeof(uint32_t) * (4 * (size_t)kWipe + 200));
+  int rc = (h && tmp && w10) ? GNSSCORR_OK : GNSSCORR_ENOMEM;
   if (!rc) {
+    // sine_gen over 10 ms (acquisition.cpp:123-128); the 1-ms tables are its head
     for (int j = 0; j < 4; j++) {
-      gnsscorr_sdr_sine_gen(tmp, -cfg->fif - 250.0 * j, 2048000.0, kN);
-      memcpy(h + (size_t)j * kN, tmp, sizeof(uint32_t) * kN);
+      gnsscorr_sdr_sine_gen((int16_t*)(w10 + (size_t)j * kWipe), -cfg->fif - 250.0 * j, 2048000.0,
+                            kWipe);
+      memcpy(h + (size_t)j * kN, w10 + (size_t)j * kWipe, sizeof(uint32_t) * kN);
     }
+    gnsscorr_sdr_post_dft((int16_t*)(w10 + 4 * (size_t)kWipe));
     gnsscorr_sdr_prn_codes(tmp);
     memcpy(h + 4 * kN, tmp, sizeof(uint32_t) * 51 * kN);
     gnsscorr_sdr_twiddles((int16_t*)(h + 55 * kN), (int16_t*)(h + 55 * kN + kN / 2));
@@ -254,9 +458,16 @@ extern "C" int gnsscorr_sdr_acq_create(gnsscorr_sdr_acq_ctx** out, const gnsscor
     if (e == hipSuccess)
       e = hipMemcpy(c->d_twi, h + 55 * kN + kN / 2, sizeof(uint32_t) * kN / 2,
                     hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&c->d_wipe10, sizeof(uint32_t) * 4 * kWipe);
+    if (e == hipSuccess) e = hipMalloc(&c->d_dft, sizeof(uint32_t) * 200);
+    if (e == hipSuccess)
+      e = hipMemcpy(c->d_wipe10, w10, sizeof(uint32_t) * 4 * kWipe, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(c->d_dft, w10 + 4 * (size_t)kWipe, sizeof(uint32_t) * 200, hipMemcpyHostToDevice);
   }
   free(h);
   free(tmp);
+  free(w10);
   if (rc || e != hipSuccess) {
     if (e != hipSuccess) gnsscorr_set_error("gnsscorr_sdr_acq_create: %s", hipGetErrorString(e));
     gnsscorr_sdr_acq_destroy(c);
@@ -372,4 +583,164 @@ extern "C" int gnsscorr_sdr_acq_sync(gnsscorr_sdr_acq_ctx* c) {
 
 extern "C" void* gnsscorr_sdr_acq_stream(gnsscorr_sdr_acq_ctx* c) {
   return c ? (void*)c->stream : nullptr;
+}
+
+// ============================================================================
+// medium / weak acquisition (Acquisition::doPrepIF at 10 / 310 ms,
+// doAcqMedium, doAcqWeak)
+// ============================================================================
+static int prep_ms(int type) {
+  return type == GNSSCORR_SDR_ACQ_STRONG ? 1 : type == GNSSCORR_SDR_ACQ_MEDIUM ? 10
+       : type == GNSSCORR_SDR_ACQ_WEAK   ? 310 : 0;
+}
+
+// the row store persists across calls (the Acquisition object's baseband_rows
+// member); growing it keeps the rows of the records it already held and zeroes
+// the new ones (the zero pages of the reference's fresh allocation)
+static int ensure_store(gnsscorr_sdr_acq_ctx* c, int n_rec) {
+  if ((size_t)n_rec <= c->store_rec) return GNSSCORR_OK;
+  const size_t per = sizeof(uint32_t) * (size_t)kStoreRows * kN;
+  uint32_t* p = nullptr;
+  HIP_TRY(hipMalloc(&p, per * n_rec));
+  hipError_t e = hipMemsetAsync((char*)p + per * c->store_rec, 0, per * (n_rec - c->store_rec),
+                                c->stream);
+  if (e == hipSuccess && c->store_rec)
+    e = hipMemcpyAsync(p, c->d_store, per * c->store_rec, hipMemcpyDeviceToDevice, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    gnsscorr_set_error("gnsscorr_sdr_acq: row store: %s", hipGetErrorString(e));
+    return GNSSCORR_EDEVICE;
+  }
+  (void)hipFree(c->d_store);
+  c->d_store = p;
+  c->store_rec = (size_t)n_rec;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sdr_acq_prep_dev(gnsscorr_sdr_acq_ctx* c, int type, const int16_t* d_buff,
+                                         int n_rec) {
+  const int ms = prep_ms(type);
+  if (!c || !d_buff || n_rec < 1 || ms == 0) {
+    gnsscorr_set_error("gnsscorr_sdr_acq_prep_dev: bad arguments (type 0/1/2, n_rec >= 1)");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  int rc = ensure_store(c, n_rec);
+  if (rc) return rc;
+  hipLaunchKernelGGL(sdr_prep_rows_kernel, dim3(4 * ms * n_rec), dim3(kThreads), 0, c->stream,
+                     (const uint32_t*)d_buff, ms, c->d_wipe10, c->d_twf, c->d_store,
+                     c->cfg.saturate);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+static int mw_rows(int type, int doppmin, int doppmax, int* lmin, int* n_rows) {
+  const int lo = doppmin / 1000, hi = doppmax / 1000;   // C truncation, as the reference
+  if (type == GNSSCORR_SDR_ACQ_MEDIUM) {                // lcv <= doppmax/1000 (:324)
+    if (hi < lo || lo < -kMaxLcv || hi > kMaxLcv) return GNSSCORR_EINVAL;
+    *n_rows = 4 * (hi - lo + 1);
+  } else if (type == GNSSCORR_SDR_ACQ_WEAK) {           // lcv < doppmax/1000 (:452)
+    if (hi <= lo || lo < -kMaxLcv || hi > kMaxLcv + 1) return GNSSCORR_EINVAL;
+    *n_rows = 8 * (hi - lo);
+  } else {
+    return GNSSCORR_EINVAL;
+  }
+  *lmin = lo;
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sdr_acq_search_dev(gnsscorr_sdr_acq_ctx* c, int type, int n_rec, int n_sv,
+                                           const int32_t* d_svs, int doppmin, int doppmax,
+                                           gnsscorr_sdr_acq_result* d_res) {
+  if (!c || !d_svs || !d_res || n_rec < 1 || n_sv < 1) return GNSSCORR_EINVAL;
+  int lmin = 0, n_rows = 0;
+  if (mw_rows(type, doppmin, doppmax, &lmin, &n_rows)) {
+    gnsscorr_set_error("gnsscorr_sdr_acq_search_dev: type must be MEDIUM (1) or WEAK (2) with "
+                       "-100 <= doppmin/1000 <= doppmax/1000 <= 100 (weak: < and <= 101)");
+    return GNSSCORR_EINVAL;
+  }
+  if ((size_t)n_rec > c->store_rec) {
+    gnsscorr_set_error("gnsscorr_sdr_acq_search_dev: %d records but the row store holds %zu "
+                       "(call gnsscorr_sdr_acq_prep_dev first)", n_rec, c->store_rec);
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  int rc = grow((void**)&c->d_rows, &c->cap_rows, (size_t)n_rec * n_sv * n_rows, sizeof(int2));
+  if (rc) return rc;
+  const dim3 grid(n_rec * n_sv * n_rows);
+  if (type == GNSSCORR_SDR_ACQ_WEAK)
+    hipLaunchKernelGGL(sdr_coh_kernel<true>, grid, dim3(kCoh), 0, c->stream, c->d_store,
+                       c->d_codes, c->d_twi, c->d_dft, d_svs, n_sv, lmin, n_rows,
+                       c->cfg.saturate, c->d_rows);
+  else
+    hipLaunchKernelGGL(sdr_coh_kernel<false>, grid, dim3(kCoh), 0, c->stream, c->d_store,
+                       c->d_codes, c->d_twi, c->d_dft, d_svs, n_sv, lmin, n_rows,
+                       c->cfg.saturate, c->d_rows);
+  const int G = n_rec * n_sv;
+  hipLaunchKernelGGL(sdr_select_mw_kernel, dim3((G + 63) / 64), dim3(64), 0, c->stream, c->d_rows,
+                     d_svs, n_sv, n_rec, lmin, n_rows, type == GNSSCORR_SDR_ACQ_WEAK ? 1 : 0,
+                     d_res);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sdr_acq_acquire(gnsscorr_sdr_acq_ctx* c, int type, const int16_t* h_buff,
+                                        int n_rec, int n_sv, const int32_t* h_svs, int doppmin,
+                                        int doppmax, gnsscorr_sdr_acq_result* h_res) {
+  if (!c || !h_buff || !h_svs || !h_res || n_rec < 1 || n_sv < 1) return GNSSCORR_EINVAL;
+  if (type == GNSSCORR_SDR_ACQ_STRONG)
+    return gnsscorr_sdr_acq_strong(c, h_buff, n_rec, n_sv, h_svs, doppmin, doppmax, h_res);
+  int lmin = 0, n_rows = 0;
+  if (mw_rows(type, doppmin, doppmax, &lmin, &n_rows)) {
+    gnsscorr_set_error("gnsscorr_sdr_acq_acquire: bad type or Doppler range");
+    return GNSSCORR_EINVAL;
+  }
+  for (int k = 0; k < n_sv; k++)
+    if (h_svs[k] < 0 || h_svs[k] >= 32) {
+      gnsscorr_set_error("gnsscorr_sdr_acq_acquire: sv %d out of range 0..31", h_svs[k]);
+      return GNSSCORR_EINVAL;
+    }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  const int ms = prep_ms(type);
+  size_t cap_b = 0, cap_s = 0, cap_r = 0;
+  int16_t* d_b = nullptr;
+  int32_t* d_s = nullptr;
+  gnsscorr_sdr_acq_result* d_r = nullptr;
+  auto cleanup = [&]() {
+    (void)hipFree(d_b);
+    (void)hipFree(d_s);
+    (void)hipFree(d_r);
+  };
+  int rc;
+  if ((rc = grow((void**)&d_b, &cap_b, (size_t)n_rec * ms * kN, sizeof(uint32_t))) ||
+      (rc = grow((void**)&d_s, &cap_s, (size_t)n_sv, sizeof(int32_t))) ||
+      (rc = grow((void**)&d_r, &cap_r, (size_t)n_rec * n_sv, sizeof(gnsscorr_sdr_acq_result)))) {
+    cleanup();
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(d_b, h_buff, sizeof(uint32_t) * (size_t)n_rec * ms * kN,
+                                hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(d_s, h_svs, sizeof(int32_t) * n_sv, hipMemcpyHostToDevice, c->stream);
+  if (e != hipSuccess) {
+    cleanup();
+    gnsscorr_set_error("gnsscorr_sdr_acq_acquire: %s", hipGetErrorString(e));
+    return GNSSCORR_EDEVICE;
+  }
+  rc = gnsscorr_sdr_acq_prep_dev(c, type, d_b, n_rec);
+  if (!rc) rc = gnsscorr_sdr_acq_search_dev(c, type, n_rec, n_sv, d_s, doppmin, doppmax, d_r);
+  if (!rc) {
+    e = hipMemcpyAsync(h_res, d_r, sizeof(gnsscorr_sdr_acq_result) * (size_t)n_rec * n_sv,
+                       hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      gnsscorr_set_error("gnsscorr_sdr_acq_acquire: %s", hipGetErrorString(e));
+      rc = GNSSCORR_EDEVICE;
+    }
+  } else {
+    (void)hipStreamSynchronize(c->stream);
+  }
+  cleanup();
+  return rc;
 }

@@ -6,6 +6,10 @@
  *                          floor(16383*cos(phase)) with a float phase accumulator
  *                          and the C++ float overloads cos(float)/sin(float)
  *  gnsscorr_sdr_twiddles   SDR/objects/fft.cpp:114-147: floor(16384*cos/sin)
+ *  gnsscorr_sdr_post_dft   the 10 x 10 post-correlation DFT rows of the medium /
+ *                          weak acquisition: wipeoff_gen (misc.cpp:148-168, fp64
+ *                          phase) at lcv*25 - 112.5 Hz, fs 1 kHz
+ *                          (acquisition.cpp:119-120)
  *  gnsscorr_sdr_prn_codes  SDR/accessories/gen_fft_codes.m + prn_gen.m: the
  *                          PRN_Codes table (conj FFT of the 2.048 Msps resampled
  *                          C/A code, scaled to 9 bits, rounded half away from 0)
@@ -38,6 +42,24 @@ void gnsscorr_sdr_twiddles(int16_t *w, int16_t *iw)
     w[2 * k + 1] = (int16_t)s;
     iw[2 * k] = (int16_t)c;
     iw[2 * k + 1] = (int16_t)(-s);
+  }
+}
+
+/* dft[j][m] as two packed int16 pairs per entry: {i, nq} and {q, ni} (MIX,
+ * sdr_structs.h:53-60), the operands of the two pmaddwd halves of sse_cacc */
+void gnsscorr_sdr_post_dft(int16_t *out /* [10][10][4] */)
+{
+  for (int j = 0; j < 10; j++) {
+    double ph = 0.0;
+    const double step = 6.283185307179586 * ((float)j * 25.0 - 112.5) / 1000.0;
+    for (int m = 0; m < 10; m++, ph += step) {
+      const int16_t c = (int16_t)floor(16383.0 * cos(ph)), s = (int16_t)floor(16383.0 * sin(ph));
+      int16_t *o = out + 4 * (j * 10 + m);
+      o[0] = c;
+      o[1] = (int16_t)(-s);
+      o[2] = s;
+      o[3] = c;
+    }
   }
 }
 

@@ -82,6 +82,8 @@ SDR_JOB = np.dtype([("packet", "<i4"), ("data_off", "<i4"), ("samps", "<i4"), ("
                     ("sbin", "<i4"), ("soff", "<i4"), ("cbin", "<i4", (3,)),
                     ("coff", "<i4", (3,))])
 assert SDR_CHAN.itemsize == 128 and SDR_CORR.itemsize == 24 and SDR_JOB.itemsize == 48
+SDR_ACQ_STRONG, SDR_ACQ_MEDIUM, SDR_ACQ_WEAK = 0, 1, 2   # ACQ_TYPE_* (acquisition.cpp:584-599)
+SDR_ACQ_MS = {0: 1, 1: 10, 2: 310}                       # ms per request (acquisition.cpp:628-641)
 SDR_RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
                        ("magnitude", "<u4"), ("success", "<i4"), ("row", "<i4")])
 
@@ -133,7 +135,8 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sgt_stream",
     "gnsscorr_sdr_prn_codes", "gnsscorr_sdr_sine_gen", "gnsscorr_sdr_acq_create",
     "gnsscorr_sdr_acq_destroy", "gnsscorr_sdr_acq_strong", "gnsscorr_sdr_acq_strong_dev",
-    "gnsscorr_sdr_acq_sync", "gnsscorr_sdr_acq_stream",
+    "gnsscorr_sdr_acq_sync", "gnsscorr_sdr_acq_stream", "gnsscorr_sdr_acq_prep_dev",
+    "gnsscorr_sdr_acq_search_dev", "gnsscorr_sdr_acq_acquire",
     "gnsscorr_sdr_corr_create", "gnsscorr_sdr_corr_destroy", "gnsscorr_sdr_init_chan",
     "gnsscorr_sdr_accum_dev", "gnsscorr_sdr_correlate", "gnsscorr_sdr_corr_sync",
     "gnsscorr_sdr_corr_stream",
@@ -209,6 +212,9 @@ def lib() -> C.CDLL:
         "gnsscorr_sdr_acq_strong": (I, [P, P, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_strong_dev": (I, [P, P, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_sync": (I, [P]),
+        "gnsscorr_sdr_acq_prep_dev": (I, [P, I, P, I]),
+        "gnsscorr_sdr_acq_search_dev": (I, [P, I, I, I, P, I, I, P]),
+        "gnsscorr_sdr_acq_acquire": (I, [P, I, P, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_stream": (P, [P]),
         "gnsscorr_sdr_corr_create": (I, [C.POINTER(P), C.POINTER(SdrCorrCfg)]),
         "gnsscorr_sdr_corr_destroy": (I, [P]),
@@ -645,6 +651,28 @@ class SdrAcqCtx:
                                              doppmin, doppmax, _ptr(res)),
                "gnsscorr_sdr_acq_strong")
         return res
+
+    def acquire(self, acq_type, buffers, svs, doppmin=-15000, doppmax=15000) -> np.ndarray:
+        """Acquisition::Acquire for one request type (doPrepIF + doAcqStrong /
+        doAcqMedium / doAcqWeak).  buffers: (n_rec, ms*2048, 2) int16 with ms =
+        1 / 10 / 310; returns SDR_RESULT [n_rec, n_sv].  Medium and weak preps
+        update the context's persistent per-record row store."""
+        ms = SDR_ACQ_MS[acq_type]
+        b = np.ascontiguousarray(buffers, np.int16).reshape(-1, ms * 2048, 2)
+        svs = np.ascontiguousarray(svs, np.int32)
+        res = np.zeros((b.shape[0], len(svs)), SDR_RESULT)
+        _check(lib().gnsscorr_sdr_acq_acquire(self.h, acq_type, _ptr(b), b.shape[0], len(svs),
+                                              _ptr(svs), doppmin, doppmax, _ptr(res)),
+               "gnsscorr_sdr_acq_acquire")
+        return res
+
+    def prep_dev(self, acq_type, d_buff, n_rec):
+        _check(lib().gnsscorr_sdr_acq_prep_dev(self.h, acq_type, d_buff, n_rec),
+               "gnsscorr_sdr_acq_prep_dev")
+
+    def search_dev(self, acq_type, n_rec, n_sv, d_svs, d_res, doppmin=-15000, doppmax=15000):
+        _check(lib().gnsscorr_sdr_acq_search_dev(self.h, acq_type, n_rec, n_sv, d_svs, doppmin,
+                                                 doppmax, d_res), "gnsscorr_sdr_acq_search_dev")
 
     def strong_dev(self, d_buff, n_rec, n_sv, d_svs, d_res, doppmin=-15000, doppmax=15000):
         _check(lib().gnsscorr_sdr_acq_strong_dev(self.h, d_buff, n_rec, n_sv, d_svs, doppmin,

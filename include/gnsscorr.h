@@ -415,6 +415,31 @@ int gnsscorr_sdr_acq_strong(gnsscorr_sdr_acq_ctx *ctx, const int16_t *h_buff, in
 int gnsscorr_sdr_acq_strong_dev(gnsscorr_sdr_acq_ctx *ctx, const int16_t *d_buff, int n_rec,
                                 int n_sv, const int32_t *d_svs, int doppmin, int doppmax,
                                 gnsscorr_sdr_acq_result *d_res);
+/* ---- medium / weak acquisition (SDR/objects/acquisition.cpp:191-236,
+ * 309-570; replaces Acquisition::Acquire's doPrepIF + doAcqMedium / doAcqWeak).
+ * The context keeps, per record, the reference object's baseband_rows member:
+ * 1240 prepared 1-ms spectra that persist between calls.  A prep of type t
+ * writes rows 0 .. 4*ms-1 (ms = 1 / 10 / 310) and leaves the rest as they
+ * were (zero at creation).  doAcqMedium reads rows lcv2*20 + 0..9 after a
+ * 10-ms prep, so for lcv2 >= 2 it sees rows an earlier weak prep left; this
+ * is reproduced.  Results: code_phase = argmax % 2048 (no 2048 - x here),
+ * doppler = lcv*1000 + lcv2*250 + (argmax / 2048)*25, row = (lcv - lmin)*4 +
+ * lcv2 (medium) or ((lcv - lmin)*4 + lcv2)*2 + k (weak, k = even/odd 10 ms). */
+#define GNSSCORR_SDR_ACQ_STRONG 0  /* ACQ_TYPE_STRONG: 1 ms                     */
+#define GNSSCORR_SDR_ACQ_MEDIUM 1  /* ACQ_TYPE_MEDIUM: 10 ms coherent + DFT     */
+#define GNSSCORR_SDR_ACQ_WEAK   2  /* ACQ_TYPE_WEAK: 15 x (10 ms + DFT) non-coh */
+/* d_buff: n_rec records of ms x 2048 CPX each (ms = 1 / 10 / 310 by type). */
+int gnsscorr_sdr_acq_prep_dev(gnsscorr_sdr_acq_ctx *ctx, int type, const int16_t *d_buff,
+                              int n_rec);
+/* type MEDIUM: -100 <= doppmin/1000 <= doppmax/1000 <= 100 (lcv inclusive);
+ * type WEAK:   -100 <= doppmin/1000 <  doppmax/1000 <= 101 (lcv exclusive). */
+int gnsscorr_sdr_acq_search_dev(gnsscorr_sdr_acq_ctx *ctx, int type, int n_rec, int n_sv,
+                                const int32_t *d_svs, int doppmin, int doppmax,
+                                gnsscorr_sdr_acq_result *d_res);
+/* Acquisition::Acquire for one request type over host buffers: prep + search. */
+int gnsscorr_sdr_acq_acquire(gnsscorr_sdr_acq_ctx *ctx, int type, const int16_t *h_buff,
+                             int n_rec, int n_sv, const int32_t *h_svs, int doppmin, int doppmax,
+                             gnsscorr_sdr_acq_result *h_res);
 int gnsscorr_sdr_acq_sync(gnsscorr_sdr_acq_ctx *ctx);
 void *gnsscorr_sdr_acq_stream(gnsscorr_sdr_acq_ctx *ctx);
 

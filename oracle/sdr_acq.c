@@ -13,6 +13,12 @@
  *   sdro_prep_if       Acquisition::doPrepIF, SDR/objects/acquisition.cpp:191-236 (1 ms)
  *   sdro_acq_strong    Acquisition::doAcqStrong, acquisition.cpp:244-301
  *   sdro_prn_codes     SDR/accessories/gen_fft_codes.m + prn_gen.m (the PRN_Codes table)
+ *   sdro_wipeoff_gen   SDR/accessories/misc.cpp:148-168 (fp64 phase, MIX rows)
+ *   sdro_cacc          SDR/simd/x86.cpp:220-249 (= sse_cacc, sse.cpp:732-800)
+ *   sdro_prep_rows     Acquisition::doPrepIF for 1 / 10 / 310 ms (acquisition.cpp:191-236)
+ *                      into the persistent baseband_rows store (1240 rows)
+ *   sdro_acq_medium    Acquisition::doAcqMedium, acquisition.cpp:309-425
+ *   sdro_acq_weak      Acquisition::doAcqWeak, acquisition.cpp:433-570
  *
  * Parity pinned: tests/test_oracle_sdr.py checks every function against the
  * reference primitives compiled from their own sources with -DNO_SIMD
@@ -161,6 +167,184 @@ sdro_result sdro_acq_strong(sdro_cpx rows[4][SDRO_N], const sdro_cpx *code, int 
       }
     }
   r.success = r.magnitude > 0;   /* THRESH_STRONG = 0 (config.h:72) */
+  return r;
+}
+
+/* ---- medium / weak acquisition ------------------------------------------ */
+void sdro_wipeoff_gen(sdro_mix *dst, double f, double fs, int n)
+{
+  double phase = 0.0;
+  const double step = SDRO_TWO_PI * f / fs;
+  for (int k = 0; k < n; k++) {
+    const int16_t c = (int16_t)floor(16383.0 * cos(phase));
+    const int16_t s = (int16_t)floor(16383.0 * sin(phase));
+    dst[k].i = dst[k].ni = c;
+    dst[k].q = s;
+    dst[k].nq = (int16_t)(-s);
+    phase += step;
+  }
+}
+
+void sdro_cacc(const sdro_cpx *a, const sdro_mix *b, int n, int32_t *iacc, int32_t *qacc)
+{
+  uint32_t ia = 0, qa = 0;                     /* int32 wrap, as paddd */
+  for (int k = 0; k < n; k++) {
+    ia += (uint32_t)(a[k].i * b[k].i + a[k].q * b[k].nq);
+    qa += (uint32_t)(a[k].i * b[k].q + a[k].q * b[k].ni);
+  }
+  *iacc = (int32_t)ia;
+  *qacc = (int32_t)qa;
+}
+
+/* doPrepIF (acquisition.cpp:191-236) for ms = 1, 10 or 310: row j*ms + m of the
+ * store is the forward FFT of ms block m mixed by the (-fif - 250 j) wipe-off.
+ * The wipe-off tables hold 10 ms and repeat (memcpy x 31, :131-137), so sample
+ * n of the buffer uses wipe entry n % 20480.  Rows >= 4*ms are NOT written:
+ * they keep whatever an earlier, longer prep left (the object's member). */
+void sdro_prep_rows(const sdro_cpx *buff, int ms, double fif, int saturate, sdro_cpx *rows)
+{
+  sdro_cpx *wipe = (sdro_cpx *)malloc(sizeof(sdro_cpx) * SDRO_WIPE);
+  sdro_mix w[SDRO_N / 2], iw[SDRO_N / 2];
+  static const int32_t r1[16] = {0};
+  sdro_twiddles(SDRO_N, w, iw);
+  for (int j = 0; j < 4; j++) {
+    sdro_sine_gen(wipe, -fif - 250.0 * j, SDRO_FS, SDRO_WIPE);
+    for (int m = 0; m < ms; m++) {
+      const int off = (m * SDRO_N) % SDRO_WIPE;
+      sdro_cpx *dst = rows + (size_t)(j * ms + m) * SDRO_N;
+      sdro_cmulsc(buff + (size_t)m * SDRO_N, wipe + off, dst, SDRO_N, 14, saturate);
+      sdro_fft(dst, SDRO_N, w, r1);
+    }
+  }
+  free(wipe);
+}
+
+/* post-correlation DFT of one delay column: 10 coherent 1-ms values against the
+ * 10 dft_rows (wipeoff_gen at lcv*25 - 112.5 Hz, acquisition.cpp:119-120), each
+ * sum >> 16 stored as int16 (:364-373), then x86_cmag (int32 wrap) */
+static void post_dft(const sdro_cpx *coh, int col, sdro_mix dft[10][10], int32_t pw[10])
+{
+  sdro_cpx d[10];
+  for (int m = 0; m < 10; m++) d[m] = coh[(size_t)m * SDRO_N + col];
+  for (int j = 0; j < 10; j++) {
+    int32_t ia, qa;
+    sdro_cacc(d, dft[j], 10, &ia, &qa);
+    const int16_t ti = (int16_t)(ia >> 16), tq = (int16_t)(qa >> 16);
+    pw[j] = (int32_t)((uint32_t)(ti * ti) + (uint32_t)(tq * tq));
+  }
+}
+
+/* first index of the strict maximum, running start 0 (x86_max, x86.cpp:274-293) */
+static void max_first(const int32_t *a, int n, int32_t *index, int32_t *mag)
+{
+  int32_t best = 0, idx = 0;
+  for (int k = 0; k < n; k++)
+    if (a[k] > best) { best = a[k]; idx = k; }
+  *index = idx;
+  *mag = best;
+}
+
+static void coherent_10(const sdro_cpx *rows, int row0, int lcv, const sdro_cpx *code, int shift,
+                        int saturate, const sdro_mix *iw, sdro_cpx *coh)
+{
+  static const int32_t r2[16] = {0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 1, 1, 1, 1, 1};
+  sdro_cpx sh[SDRO_N];
+  for (int m = 0; m < 10; m++) {
+    const sdro_cpx *row = rows + (size_t)(row0 + m) * SDRO_N;
+    for (int k = 0; k < SDRO_N; k++) sh[k] = row[(k + lcv + SDRO_N) & (SDRO_N - 1)];
+    sdro_cmulsc(sh, code, coh + (size_t)m * SDRO_N, SDRO_N, shift, saturate);
+    sdro_fft(coh + (size_t)m * SDRO_N, SDRO_N, iw, r2);
+  }
+}
+
+sdro_result sdro_acq_medium(const sdro_cpx *rows, const sdro_cpx *code, int sv, int doppmin,
+                            int doppmax, int saturate)
+{
+  sdro_mix w[SDRO_N / 2], iw[SDRO_N / 2], dft[10][10];
+  sdro_twiddles(SDRO_N, w, iw);
+  for (int j = 0; j < 10; j++) sdro_wipeoff_gen(dft[j], (float)j * 25.0 - 112.5, 1000.0, 10);
+  sdro_cpx *coh = (sdro_cpx *)malloc(sizeof(sdro_cpx) * 10 * SDRO_N);
+  int32_t *power = (int32_t *)malloc(sizeof(int32_t) * 10 * SDRO_N);
+  sdro_result r;
+  memset(&r, 0, sizeof r);
+  r.sv = sv;
+  int32_t mag = 0;
+  const int lmin = doppmin / 1000;
+  for (int lcv = lmin; lcv <= doppmax / 1000; lcv++)      /* inclusive, :324 */
+    for (int lcv2 = 0; lcv2 < 4; lcv2++) {
+      /* baseband_rows[lcv2*20 + lcv3 + k*10] with k = 0 (:341): a 20-row stride
+       * over a 10-ms prep, so lcv2 = 1 reads the 500 Hz rows and lcv2 >= 2 reads
+       * rows 40..79, which this prep did not write */
+      coherent_10(rows, lcv2 * 20, lcv, code, 10, saturate, iw, coh);
+      int32_t pw[10];
+      for (int c = 0; c < SDRO_N; c++) {
+        post_dft(coh, c, dft, pw);
+        for (int j = 0; j < 10; j++) power[j * SDRO_N + c] = pw[j];
+      }
+      int32_t idx, m;
+      max_first(power, 10 * SDRO_N, &idx, &m);
+      if (m > mag) {
+        mag = m;
+        r.code_phase = idx % SDRO_N;
+        r.doppler = (int32_t)((lcv * 1000) + (lcv2 * 250) + (idx / SDRO_N) * 25.0);
+        r.magnitude = (uint32_t)m;
+        r.row = (lcv - lmin) * 4 + lcv2;
+      }
+    }
+  r.success = r.magnitude > 0;   /* THRESH_MEDIUM = 0 (config.h:73) */
+  free(coh);
+  free(power);
+  return r;
+}
+
+int sdro_weak_shift(int i, int lcv, int lcv2)
+{
+  /* acquisition.cpp:483-489 */
+  const double doppler = (double)(lcv * 1000) + (float)(lcv2 * 250);
+  const double code_doppler = (double)i * .02 * 2048000 * doppler / 1.57542e9;
+  return (int)floor(code_doppler);
+}
+
+sdro_result sdro_acq_weak(const sdro_cpx *rows, const sdro_cpx *code, int sv, int doppmin,
+                          int doppmax, int saturate)
+{
+  sdro_mix w[SDRO_N / 2], iw[SDRO_N / 2], dft[10][10];
+  sdro_twiddles(SDRO_N, w, iw);
+  for (int j = 0; j < 10; j++) sdro_wipeoff_gen(dft[j], (float)j * 25.0 - 112.5, 1000.0, 10);
+  sdro_cpx *coh = (sdro_cpx *)malloc(sizeof(sdro_cpx) * 10 * SDRO_N);
+  uint32_t *power = (uint32_t *)malloc(sizeof(uint32_t) * 10 * SDRO_N);
+  sdro_result r;
+  memset(&r, 0, sizeof r);
+  r.sv = sv;
+  int32_t mag = 0;
+  const int lmin = doppmin / 1000;
+  for (int lcv = lmin; lcv < doppmax / 1000; lcv++)       /* exclusive, :452 */
+    for (int lcv2 = 0; lcv2 < 4; lcv2++)
+      for (int k = 0; k < 2; k++) {
+        memset(power, 0, sizeof(uint32_t) * 10 * SDRO_N);
+        for (int i = 0; i < 15; i++) {
+          coherent_10(rows, lcv2 * 310 + i * 20 + k * 10, lcv, code, 9, saturate, iw, coh);
+          const int shift = sdro_weak_shift(i, lcv, lcv2);
+          int32_t pw[10];
+          for (int c = 0; c < SDRO_N; c++) {
+            post_dft(coh, c, dft, pw);
+            const int dst = (c + shift + SDRO_N) % SDRO_N;
+            for (int j = 0; j < 10; j++) power[j * SDRO_N + dst] += (uint32_t)pw[j];
+          }
+        }
+        int32_t idx, m;
+        max_first((const int32_t *)power, 10 * SDRO_N, &idx, &m);
+        if (m > mag) {
+          mag = m;
+          r.code_phase = idx % SDRO_N;
+          r.doppler = (int32_t)((lcv * 1000) + (lcv2 * 250) + (idx / SDRO_N) * 25.0);
+          r.magnitude = (uint32_t)m;
+          r.row = ((lcv - lmin) * 4 + lcv2) * 2 + k;
+        }
+      }
+  r.success = r.magnitude > 0;   /* THRESH_WEAK = 0 (config.h:74) */
+  free(coh);
+  free(power);
   return r;
 }
 

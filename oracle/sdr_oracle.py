@@ -25,6 +25,7 @@ IF_SDR = 38400.0
 RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
                    ("magnitude", "<u4"), ("success", "<i4"), ("row", "<i4")])
 R1 = np.zeros(16, np.int32)
+ROWS = 1240            # baseband_rows (acquisition.cpp:107-110)
 R2 = np.array([0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 1, 1, 1, 1, 1], np.int32)
 
 
@@ -49,6 +50,13 @@ class OracleSDR:
         L.sdro_acq_strong.argtypes = [P, P, I, I, I, I]
         L.sdro_acq_strong.restype = _Res
         L.sdro_prn_codes.argtypes = [P]
+        L.sdro_prep_rows.argtypes = [P, I, D, I, P]
+        L.sdro_acq_medium.argtypes = [P, P, I, I, I, I]
+        L.sdro_acq_medium.restype = _Res
+        L.sdro_acq_weak.argtypes = [P, P, I, I, I, I]
+        L.sdro_acq_weak.restype = _Res
+        L.sdro_weak_shift.argtypes = [I, I, I]
+        L.sdro_weak_shift.restype = I
         L.orc_gn3s_block.argtypes = [P, P, C.c_uint32, P, P]
         L.orc_downsample.argtypes = [P, P, D, D, I]
         L.orc_downsample.restype = I
@@ -123,6 +131,27 @@ class OracleSDR:
         self.L.sdro_prn_codes(_p(out))
         return out
 
+    # -- medium / weak: an Acquisition object's persistent baseband_rows store
+    def new_rows(self):
+        return np.zeros((ROWS, N, 2), np.int16)
+
+    def prep_rows(self, rows, buff, ms, fif=IF_SDR, saturate=False):
+        buff = np.ascontiguousarray(buff, np.int16).reshape(-1, 2)
+        assert buff.shape[0] >= ms * N and rows.shape == (ROWS, N, 2)
+        self.L.sdro_prep_rows(_p(buff), ms, fif, int(saturate), _p(rows))
+
+    def acq_search(self, kind, rows, codes, svs, doppmin=-15000, doppmax=15000, saturate=False):
+        fn = self.L.sdro_acq_medium if kind == "medium" else self.L.sdro_acq_weak
+        out = np.zeros(len(svs), RESULT)
+        for k, sv in enumerate(svs):
+            code = np.ascontiguousarray(codes[sv], np.int16)
+            r = fn(_p(rows), _p(code), int(sv), doppmin, doppmax, int(saturate))
+            out[k] = (r.sv, r.code_phase, r.doppler, r.magnitude, r.success, r.row)
+        return out
+
+    def weak_shift(self, i, lcv, lcv2):
+        return self.L.sdro_weak_shift(i, lcv, lcv2)
+
 
 class _Res(C.Structure):
     _fields_ = [("sv", C.c_int32), ("code_phase", C.c_int32), ("doppler", C.c_int32),
@@ -143,6 +172,12 @@ class RefSDR:
         L.ref_sdr_accum.argtypes = [P, P, P, P, P, I, P]
         L.ref_sdr_downsample.argtypes = [P, P, D, D, I]
         L.ref_sdr_downsample.restype = I
+        L.ref_sdr_acq_session.argtypes = [D]
+        L.ref_sdr_acq_session.restype = P
+        L.ref_sdr_acq_session_free.argtypes = [P]
+        L.ref_sdr_acq_prep.argtypes = [P, P, I]
+        L.ref_sdr_acq_medium.argtypes = [P, I, I, I, P]
+        L.ref_sdr_acq_weak.argtypes = [P, I, I, I, P]
         self.L = L
 
     def downsample(self, src, fdest, fsource):
@@ -200,6 +235,41 @@ class RefSDR:
             self.L.ref_sdr_acq_strong(_p(buff), fif, int(sv), doppmin, doppmax, _p(o))
             out[k] = tuple(int(v) for v in o)
         return out
+
+
+class RefAcqSession:
+    """The reference Acquisition object's medium/weak path (doPrepIF +
+    doAcqMedium / doAcqWeak over the -DNO_SIMD primitives, sdr_ref_harness.cpp),
+    with its baseband_rows member persisting between requests."""
+
+    def __init__(self, ref: RefSDR, fif=IF_SDR):
+        self.L = ref.L
+        self.h = self.L.ref_sdr_acq_session(fif)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.ref_sdr_acq_session_free(self.h)
+            self.h = None
+
+    def prep(self, buff, ms):
+        buff = np.ascontiguousarray(buff, np.int16).reshape(-1, 2)
+        assert buff.shape[0] >= ms * N
+        self.L.ref_sdr_acq_prep(self.h, _p(buff), ms)
+
+    def search(self, kind, svs, doppmin=-15000, doppmax=15000):
+        fn = self.L.ref_sdr_acq_medium if kind == "medium" else self.L.ref_sdr_acq_weak
+        out = np.zeros(len(svs), RESULT)
+        o = np.zeros(6, np.int32)
+        for k, sv in enumerate(svs):
+            fn(self.h, int(sv), doppmin, doppmax, _p(o))
+            out[k] = tuple(int(v) for v in o)
+        return out
+
+
+def make_long_buffer(sigs, ms, seed=1, amp_noise=2.0, fif=IF_SDR):
+    """ms consecutive 1-ms CPX blocks [ms*2048, 2] of one continuous signal
+    (make_buffer over the whole span)."""
+    return make_buffer(sigs, n=ms * N, seed=seed, amp_noise=amp_noise, fif=fif)
 
 
 def ca_chips(prn: int) -> np.ndarray:

@@ -8,6 +8,9 @@
 // Acquisition::doPrepIF (acquisition.cpp:191-236, 1 ms) and doAcqStrong
 // (acquisition.cpp:244-301), with the x86_* (wrapping) primitives standing in
 // for the production sse_* ones (equal outside int16 saturation).
+// ref_sdr_acq_session / _prep / _medium / _weak do the same for doPrepIF at
+// 10 and 310 ms, doAcqMedium (acquisition.cpp:309-425) and doAcqWeak
+// (acquisition.cpp:433-570), over a session holding the object's members.
 #include "includes.h"
 #include "fft.h"
 #include "prn_codes.h"
@@ -133,6 +136,172 @@ void ref_sdr_acq_strong(const CPX* buff, double fif, int sv, int doppmin, int do
   delete[] rows;
   delete[] baseband;
   for (int j = 0; j < 4; j++) delete[] wipe[j];
+}
+
+// ---- medium / weak acquisition over the reference primitives --------------
+// A session holds the Acquisition members that persist between requests
+// (acquisition.cpp:95-142): the 310-ms baseband, the padded baseband_rows
+// store of 1240 rows x (2048 + 201), the 10-ms wipe-offs copied 31 times and
+// the 10 x 10 post-correlation DFT rows.  The reference allocates the rows
+// with new[] (no value initialisation); calloc stands in for the zero pages
+// such a 22 MB allocation gets from a fresh mmap.
+struct RefAcqSession {
+  CPX *baseband, *shift, *wipe[4], *coherent, *power;
+  CPX **rows;
+  MIX *dft, *dft_rows[10];
+  FFT *fwd, *inv;
+  double fif;
+};
+
+void* ref_sdr_acq_session(double fif)
+{
+  const int n = SAMPS_MS;
+  int32 R1[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int32 R2[16] = {0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 1, 1, 1, 1, 1};
+  RefAcqSession* s = new RefAcqSession;
+  s->fif = fif;
+  s->baseband = (CPX*)calloc((size_t)4 * 310 * n, sizeof(CPX));
+  s->shift = (CPX*)calloc((size_t)4 * 310 * (n + 201), sizeof(CPX));
+  s->rows = new CPX*[1240];
+  for (int k = 0; k < 1240; k++) s->rows[k] = &s->shift[(size_t)k * (n + 201)];
+  s->coherent = new CPX[10 * n];
+  s->power = new CPX[10 * n];
+  s->dft = new MIX[100];
+  for (int k = 0; k < 10; k++) {
+    s->dft_rows[k] = &s->dft[k * 10];
+    wipeoff_gen(s->dft_rows[k], (float)k * 25.0 - 112.5, 1000.0, 10);
+  }
+  for (int j = 0; j < 4; j++) {
+    s->wipe[j] = new CPX[310 * n];
+    sine_gen(s->wipe[j], -fif - 250.0 * j, SAMPLE_FREQUENCY, 10 * n);
+    for (int k = 1; k < 31; k++) memcpy(&s->wipe[j][k * 10 * n], s->wipe[j], 10 * n * sizeof(CPX));
+  }
+  s->fwd = new FFT(n, R1);
+  s->inv = new FFT(n, R2);
+  return s;
+}
+
+void ref_sdr_acq_session_free(void* p)
+{
+  RefAcqSession* s = (RefAcqSession*)p;
+  free(s->baseband);
+  free(s->shift);
+  delete[] s->rows;
+  delete[] s->coherent;
+  delete[] s->power;
+  delete[] s->dft;
+  for (int j = 0; j < 4; j++) delete[] s->wipe[j];
+  delete s->fwd;
+  delete s->inv;
+  delete s;
+}
+
+// doPrepIF (acquisition.cpp:191-236), ms = 1, 10 or 310
+void ref_sdr_acq_prep(void* p, const CPX* buff, int ms)
+{
+  RefAcqSession* s = (RefAcqSession*)p;
+  const int n = SAMPS_MS;
+  memcpy(s->baseband, buff, (size_t)ms * n * sizeof(CPX));
+  for (int j = 1; j < 4; j++)
+    x86_cmulsc(&s->baseband[0], s->wipe[j], &s->baseband[(size_t)j * ms * n], ms * n, 14);
+  x86_cmuls(s->baseband, s->wipe[0], ms * n, 14);
+  for (int k = 0; k < 4 * ms; k++) s->fwd->doFFT(&s->baseband[(size_t)k * n], true);
+  for (int k = 0; k < 4 * ms; k++) {
+    CPX* r = s->rows[k];
+    memcpy(r, &s->baseband[(size_t)(k + 1) * n - 100], 100 * sizeof(CPX));
+    memcpy(r + 100, &s->baseband[(size_t)k * n], n * sizeof(CPX));
+    memcpy(r + 100 + n, &s->baseband[(size_t)k * n], 100 * sizeof(CPX));
+  }
+}
+
+// the 1-ms-block post-correlation DFT of one delay column (acquisition.cpp:350-373)
+static void ref_post_dft(RefAcqSession* s, int col, CPX temp[10])
+{
+  const int n = SAMPS_MS;
+  int32 data[32];
+  int32* q = (int32*)&s->coherent[col];
+  for (int m = 0; m < 10; m++) { data[m] = *q; q += n; }
+  for (int j = 0; j < 10; j++) {
+    int32 ia, qa;
+    x86_cacc((CPX*)data, s->dft_rows[j], 10, &ia, &qa);
+    temp[j].i = ia >> 16;
+    temp[j].q = qa >> 16;
+  }
+}
+
+// out: sv, code_phase, doppler, magnitude, success, row  (acquisition.cpp:309-425)
+void ref_sdr_acq_medium(void* p, int sv, int doppmin, int doppmax, int32* out)
+{
+  RefAcqSession* s = (RefAcqSession*)p;
+  const int n = SAMPS_MS;
+  CPX* code = (CPX*)&PRN_Codes[2 * sv * n];
+  int32 mag = 0, magt, indext, res[6] = {sv, 0, 0, 0, 0, 0};
+  for (int lcv = doppmin / 1000; lcv <= doppmax / 1000; lcv++)
+    for (int lcv2 = 0; lcv2 < 4; lcv2++) {
+      const int k = 0;
+      for (int l3 = 0; l3 < 10; l3++) {
+        x86_cmulsc(&s->rows[lcv2 * 20 + l3 + k * 10][100 + lcv], code, &s->coherent[l3 * n], n, 10);
+        s->inv->doiFFT(&s->coherent[l3 * n], true);
+      }
+      for (int l3 = 0; l3 < n; l3++) {
+        CPX temp[10];
+        ref_post_dft(s, l3, temp);
+        int32* q = (int32*)&s->power[l3];
+        for (int j = 0; j < 10; j++) { *q = *(int32*)&temp[j]; q += n; }
+      }
+      x86_cmag(&s->power[0], 10 * n);
+      x86_max((int32*)s->power, &indext, &magt, 10 * n);
+      if (magt > mag) {
+        mag = magt;
+        res[1] = indext % n;
+        res[2] = (lcv * 1000) + (lcv2 * 250) + (indext / n) * 25.0;
+        res[3] = mag;
+        res[5] = (lcv - doppmin / 1000) * 4 + lcv2;
+      }
+    }
+  res[4] = (uint32)res[3] > THRESH_MEDIUM ? 1 : 0;
+  memcpy(out, res, sizeof res);
+}
+
+// out: sv, code_phase, doppler, magnitude, success, row  (acquisition.cpp:433-570)
+void ref_sdr_acq_weak(void* p, int sv, int doppmin, int doppmax, int32* out)
+{
+  RefAcqSession* s = (RefAcqSession*)p;
+  const int n = SAMPS_MS;
+  CPX* code = (CPX*)&PRN_Codes[2 * sv * n];
+  int32 mag = 0, magt, indext, res[6] = {sv, 0, 0, 0, 0, 0};
+  for (int lcv = doppmin / 1000; lcv < doppmax / 1000; lcv++)
+    for (int lcv2 = 0; lcv2 < 4; lcv2++)
+      for (int k = 0; k < 2; k++) {
+        memset(s->power, 0x0, 10 * n * sizeof(CPX));
+        for (int i = 0; i < 15; i++) {
+          for (int l3 = 0; l3 < 10; l3++) {
+            x86_cmulsc(&s->rows[lcv2 * 310 + l3 + i * 20 + k * 10][100 + lcv], code,
+                       &s->coherent[l3 * n], n, 9);
+            s->inv->doiFFT(&s->coherent[l3 * n], true);
+          }
+          double doppler = (double)(lcv * 1000) + (float)(lcv2 * 250);
+          double code_doppler = (double)i * .02 * IF_SAMPLE_FREQUENCY * doppler / L1;
+          int32 shift = (int32)floor(code_doppler);
+          for (int l3 = 0; l3 < n; l3++) {
+            CPX temp[10];
+            ref_post_dft(s, l3, temp);
+            x86_cmag(&temp[0], 10);
+            int32* q = (int32*)&s->power[(l3 + shift + SAMPS_MS) % SAMPS_MS];
+            for (int j = 0; j < 10; j++) { *q += ((int32*)temp)[j]; q += n; }
+          }
+        }
+        x86_max((int32*)s->power, &indext, &magt, 10 * n);
+        if (magt > mag) {
+          mag = magt;
+          res[1] = indext % n;
+          res[2] = (lcv * 1000) + (lcv2 * 250) + (indext / n) * 25.0;
+          res[3] = mag;
+          res[5] = ((lcv - doppmin / 1000) * 4 + lcv2) * 2 + k;
+        }
+      }
+  res[4] = (uint32)res[3] > THRESH_WEAK ? 1 : 0;
+  memcpy(out, res, sizeof res);
 }
 
 }  // extern "C"

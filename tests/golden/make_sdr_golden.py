@@ -14,7 +14,12 @@ oracle ref), plus PRN_Codes from accessories/prn_codes.h.  Stored:
                       answers (x86_cmulsc + x86_prn_accum_new) on random jobs
   sdr_frontend.npz    downsample() (accessories/misc.cpp:174-197) known answers
                       from the reference build at the receiver's source rates
-Usage:  python tests/golden/make_sdr_golden.py
+  sdr_acq_mw.npz      medium / weak acquisition (doPrepIF at 10 / 310 ms,
+                      doAcqMedium, doAcqWeak, acquisition.cpp:191-236,309-570)
+                      over the reference primitives, one session: medium on a
+                      fresh object, weak, then medium again (it reads rows the
+                      weak prep left, the reference's 20-row stride)
+Usage:  python tests/golden/make_sdr_golden.py [mw]   (mw: only sdr_acq_mw.npz)
 """
 import os
 import subprocess
@@ -36,8 +41,37 @@ SCENES = [  # (seed, amp_noise, signals)
 ]
 
 
+MW_SIGS = [dict(prn=5, code_phase=300.0, doppler=2250.0, amp=0.45),
+           dict(prn=17, code_phase=800.3, doppler=-4100.0, amp=0.15),
+           dict(prn=26, code_phase=10.0, doppler=1000.0, amp=0.09)]
+MW_WEAK_SVS = [4, 16, 25, 9]
+
+
+def make_mw(ref, out):
+    """Medium / weak session fixture (see module docstring)."""
+    buf = S.make_long_buffer(MW_SIGS, 310, seed=21, amp_noise=1.5)
+    sess = S.RefAcqSession(ref)
+    svs = np.arange(32)
+    sess.prep(buf, 10)
+    med0 = sess.search("medium", svs)
+    sess.prep(buf, 310)
+    weak = sess.search("weak", MW_WEAK_SVS, -5000, 5000)
+    sess.prep(buf, 10)
+    med1 = sess.search("medium", svs, -7000, 3000)
+    np.savez_compressed(os.path.join(out, "sdr_acq_mw.npz"), buffer=buf.astype(np.int8),
+                        medium_fresh=med0, weak_svs=np.array(MW_WEAK_SVS, np.int32), weak=weak,
+                        medium_after_weak=med1, fif=np.array(S.IF_SDR))
+    for name, r in (("medium", med0), ("weak", weak), ("medium2", med1)):
+        top = sorted(r, key=lambda v: -int(v["magnitude"]))[:3]
+        print(name, [(int(v["sv"]) + 1, int(v["code_phase"]), int(v["doppler"]),
+                      int(v["magnitude"])) for v in top])
+
+
 def main():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    if sys.argv[1:] == ["mw"]:
+        make_mw(S.RefSDR(), os.path.dirname(os.path.abspath(__file__)))
+        return
     ref = S.RefSDR()
     out = os.path.dirname(os.path.abspath(__file__))
     np.savez_compressed(os.path.join(out, "sdr_prn_codes.npz"), prn_codes=ref.prn_codes())
@@ -84,6 +118,7 @@ def main():
         fe_rates.append((fs, n, len(o)))
     np.savez_compressed(os.path.join(out, "sdr_frontend.npz"), src=np.stack(fe_src),
                         out=np.stack(fe_out), rates=np.array(fe_rates))
+    make_mw(ref, out)
     for k, r in enumerate(res):
         print("scene", k, [(int(v["sv"]) + 1, int(v["code_phase"]), int(v["doppler"]),
                             int(v["magnitude"])) for v in r if v["magnitude"] > 0][:3])

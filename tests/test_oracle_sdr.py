@@ -189,3 +189,64 @@ def test_gn3s_oracle_vs_product_table():
         assert np.array_equal(out.reshape(2, 10240, 2)[b][ok], mixed[b][idx[ok]])
         assert (out.reshape(2, 10240, 2)[b][~ok] == 0).all()
     assert ph == (ph0 + 2 * 20000 * 2557223528) % (1 << 32)
+
+
+# ---- medium / weak acquisition (acquisition.cpp:191-236, 309-570) ---------------
+def _mw_session_oracle(o, codes, buf, fif):
+    """The golden's request sequence on the C restatement's row store."""
+    rows = o.new_rows()
+    o.prep_rows(rows, buf, 10, fif)
+    med0 = o.acq_search("medium", rows, codes, np.arange(32))
+    o.prep_rows(rows, buf, 310, fif)
+    return rows, med0
+
+
+def test_acq_medium_weak_golden(o):
+    f = np.load(os.path.join(GOLD, "sdr_acq_mw.npz"))
+    codes = np.load(os.path.join(GOLD, "sdr_prn_codes.npz"))["prn_codes"]
+    buf = f["buffer"].astype(np.int16)
+    rows, med0 = _mw_session_oracle(o, codes, buf, float(f["fif"]))
+    assert (med0 == f["medium_fresh"]).all()
+    assert (o.acq_search("weak", rows, codes, f["weak_svs"], -5000, 5000) == f["weak"]).all()
+    o.prep_rows(rows, buf, 10, float(f["fif"]))
+    assert (o.acq_search("medium", rows, codes, np.arange(32), -7000, 3000) ==
+            f["medium_after_weak"]).all()
+    # the planted signals: PRN 5 strong enough for both, PRN 26 only non-coherently
+    w = {int(r["sv"]): r for r in f["weak"]}
+    assert w[4]["doppler"] == 2350 and w[25]["magnitude"] > 3 * w[9]["magnitude"]
+
+
+def test_weak_code_doppler_shift(o):
+    # acquisition.cpp:483-489 at the extremes of the +-15 kHz search
+    assert o.weak_shift(0, 14, 3) == 0
+    assert o.weak_shift(14, 14, 3) == int(np.floor(14 * .02 * 2048000 * 14750.0 / 1.57542e9))
+    assert o.weak_shift(14, -15, 0) == int(np.floor(14 * .02 * 2048000 * -15000.0 / 1.57542e9))
+    assert o.weak_shift(14, -15, 0) < 0
+
+
+@need_ref
+def test_medium_weak_oracle_matches_reference_build(o):
+    ref = S.RefSDR()
+    codes = ref.prn_codes()
+    rng = np.random.default_rng(8)
+    for amp, sat_range in ((2.0, 3), (90.0, 5)):
+        buf = S.make_long_buffer([dict(prn=11, code_phase=500.5, doppler=-1250.0, amp=amp / 4)],
+                                 310, seed=int(rng.integers(1 << 20)), amp_noise=amp)
+        sess = S.RefAcqSession(ref)
+        rows = o.new_rows()
+        sess.prep(buf, 310)
+        o.prep_rows(rows, buf, 310)
+        assert (o.acq_search("weak", rows, codes, [10, 3], -2000, 0) ==
+                sess.search("weak", [10, 3], -2000, 0)).all()
+        sess.prep(buf, 10)
+        o.prep_rows(rows, buf, 10)
+        assert (o.acq_search("medium", rows, codes, [10, 3, 31], -sat_range * 1000, 1999) ==
+                sess.search("medium", [10, 3, 31], -sat_range * 1000, 1999)).all()
+    # full-scale int16 input: the FFT ranks, the >> 16 and cmag wrap identically
+    big = rng.integers(-32768, 32768, (310 * 2048, 2)).astype(np.int16)
+    sess = S.RefAcqSession(ref)
+    rows = o.new_rows()
+    sess.prep(big, 10)
+    o.prep_rows(rows, big, 10)
+    assert (o.acq_search("medium", rows, codes, [0, 7], -1000, 1000) ==
+            sess.search("medium", [0, 7], -1000, 1000)).all()
