@@ -357,8 +357,29 @@ def run_sdr(dist, dev, steps, warmup):
     fe.sync()
     dt_fe = dist.max(time.perf_counter() - t0)
     ms_fe = e0.elapsed_ms(e1) / steps
+    # medium / weak acquisition: one receiver's full request (32 sv, +-15 kHz) per step,
+    # doPrepIF (10 / 310 ms) + doAcqMedium / doAcqWeak, the 310-ms record resident in HBM
+    long = rng.integers(-3, 4, (310 * SDR_N, 2)).astype(np.int16)
+    d_l = gc.DevBuf.from_array(long, dev)
+    mw = {}
+    for kind, t, k_steps in (("medium", gc.SDR_ACQ_MEDIUM, steps), ("weak", gc.SDR_ACQ_WEAK,
+                                                                   max(steps // 5, 3))):
+        for _ in range(2):
+            acq.prep_dev(t, d_l.ptr, 1)
+            acq.search_dev(t, 1, SDR_SV, d_sv.ptr, d_r.ptr, -15000, 15000)
+        acq.sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        e0.record(acq.stream)
+        for _ in range(k_steps):
+            acq.prep_dev(t, d_l.ptr, 1)
+            acq.search_dev(t, 1, SDR_SV, d_sv.ptr, d_r.ptr, -15000, 15000)
+        e1.record(acq.stream)
+        acq.sync()
+        mw[kind] = dict(dt=dist.max(time.perf_counter() - t0), ms=e0.elapsed_ms(e1) / k_steps,
+                        steps=k_steps)
     return dict(dt_acq=dt_acq, ms_acq=ms_acq, dt_corr=dt_corr, ms_corr=ms_corr, steps=steps,
-                bufs=bufs, dt_fe=dt_fe, ms_fe=ms_fe)
+                bufs=bufs, dt_fe=dt_fe, ms_fe=ms_fe, mw=mw, long=long)
 
 
 def cpu_baseline_sdr(bufs, budget_s=5.0):
@@ -375,6 +396,34 @@ def cpu_baseline_sdr(bufs, budget_s=5.0):
                 sample=f"{n} doAcqStrong searches (32 sv x 120 rows) of the scalar C restatement "
                        f"(oracle/sdr_acq.c, bit-exact with the reference -DNO_SIMD build), "
                        f"{dt:.1f} s")
+
+
+SDR_MW_ROWS = {"medium": 4 * 31, "weak": 8 * 30}      # +-15 kHz (acquisition.cpp:324, :452)
+SDR_MW_PASSES = {"medium": 1, "weak": 15}
+# integer-op model per row pass: ten cmulsc'd 2048-sample rows (8 ops/sample),
+# ten 2048-point int16 IFFTs (11 x 1024 butterflies x 12 ops), 2048 columns x 10 post-DFT
+# bins x (10 complex MACs = 80 ops + |.|^2 3 + accumulate/compare 1)
+SDR_MW_OPS_PASS = 10 * SDR_N * 8 + 10 * 11 * 1024 * 12 + SDR_N * 10 * 84
+
+
+def cpu_baseline_sdr_mw(long, kind, budget_s=4.0):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sdr_oracle
+    o = sdr_oracle.OracleSDR()
+    codes = o.prn_codes()
+    rows = o.new_rows()
+    o.prep_rows(rows, long, 310 if kind == "weak" else 10)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:   # one sv x one 1-kHz step (4 / 8 rows) per call
+        lo = -15000 + 1000 * (n % 30)
+        o.acq_search(kind, rows, codes, [n % SDR_SV], lo, lo + (0 if kind == "medium" else 1000))
+        n += 1
+    dt = time.perf_counter() - t0
+    rows_done = n * (4 if kind == "medium" else 8)
+    return dict(value=rows_done * 10 * SDR_N / dt, unit="cells/s", cores=1, kind="port",
+                sample=f"{rows_done} doAcq{kind.capitalize()} rows (one sv x one 1-kHz step per "
+                       f"call) of the scalar C restatement (oracle/sdr_acq.c, bit-exact with the "
+                       f"reference -DNO_SIMD primitives), {dt:.1f} s")
 
 
 def cpu_baseline_sgt(budget_s=6.0):
@@ -581,6 +630,24 @@ def main():
                           "(wipe-off row + 3 code rows from the HBM-resident pre-sampled tables)",
                 "kernel_ms_per_launch": sdr["ms_corr"],
             }
+            for kind, m in sdr["mw"].items():
+                cells = SDR_SV * SDR_MW_ROWS[kind] * 10 * SDR_N
+                ops = SDR_SV * SDR_MW_ROWS[kind] * SDR_MW_PASSES[kind] * SDR_MW_OPS_PASS
+                out[f"sdr_acquisition_{kind}"] = {
+                    "metric": f"acquisition cells/sec (GPS-SDR {kind} acquisition, bit-exact)",
+                    "value": cells * m["steps"] * W / m["dt"], "unit": "cells/s",
+                    "config": f"one receiver's full doAcq{kind.capitalize()} request per step: "
+                              f"32 sv x {SDR_MW_ROWS[kind]} rows (+-15 kHz) x 10 post-DFT bins "
+                              f"(25 Hz) x 2048 delays, "
+                              + ("10 ms coherent" if kind == "medium" else
+                                 "15 x 10 ms coherent, non-coherent sum with code-Doppler shift")
+                              + " (310-ms record resident in HBM, doPrepIF included)",
+                    "ms_per_search": m["ms"],
+                    "roofline": {"bound": "valu", "kernel": "sdr_coh_kernel",
+                                 "achieved": ops / (m["ms"] * 1e-3) / 1e12, "peak": PEAK_INT_TOPS,
+                                 "unit": "Tops/s (int32 op model, DESIGN.md)",
+                                 "frac": ops / (m["ms"] * 1e-3) / 1e12 / PEAK_INT_TOPS},
+                }
             fe_in = SDR_FE_BLOCKS * gc.GN3S_BLOCK_IN
             fe_bytes = fe_in // 4 + SDR_FE_BLOCKS * gc.GN3S_BLOCK_OUT * 4
             out["sdr_frontend"] = {
@@ -606,6 +673,9 @@ def main():
                 out["glonass_tracking"]["cpu_baseline"] = cpu_baseline_sgt()
             if sdr:
                 out["sdr_acquisition"]["cpu_baseline"] = cpu_baseline_sdr(sdr["bufs"])
+                for kind in sdr["mw"]:
+                    out[f"sdr_acquisition_{kind}"]["cpu_baseline"] = \
+                        cpu_baseline_sdr_mw(sdr["long"], kind)
         print(json.dumps(out))
     dist.close()
 
