@@ -24,6 +24,7 @@
 // One workgroup = one channel x one call.  256 threads x 64 samples covers a
 // 1-ms chunk at 16.368 Msps; IF is read as 16-byte vector loads.
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -39,6 +40,13 @@
     }                                                                                   \
   } while (0)
 
+// Diagnostic hook (tools/trk_stamps.hip defines it; a no-op in the library)
+#ifndef TRACK_PSTAMP
+#define TRACK_PSTAMP(i) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int kRun = 64;              // samples per thread
@@ -46,6 +54,10 @@ constexpr int kMaxThreads = 1024;
 constexpr int kMaxNsamp = kRun * kMaxThreads;
 constexpr int kMaxEpochs = kMaxNsamp / GNSSCORR_OSG_ROW + 2;
 constexpr uint64_t kNever = ~0ull;
+constexpr int kPitch = 9;             // 16-byte chunks per staged lane run (8 + 1 pad)
+constexpr int kStageMaxBytes = 48 * 1024;
+constexpr int kPkStage = 2400;        // LDS words of the E/P/L row (D <= 2399: slew <= 353)
+constexpr int kMaxCpw = 4;            // channels per workgroup
 
 // 8-phase LO (correlator.c:203-204) as 4-bit two's-complement nibbles.
 constexpr uint32_t kLutI = 0xEEF1221Fu;  // i_lo = {-1, 1, 2, 2, 1,-1,-2,-2}
@@ -84,20 +96,28 @@ __device__ __forceinline__ void msbit_step(int& ms, int& bit) {
   ms %= 20;
 }
 
+// Wave-wide reductions without the LDS crossbar (ds_bpermute): a DPP
+// Hillis-Steele scan inside each 16-lane row (row_shr 1/2/4/8, identity
+// shifted in), then the four row results (lanes 15/31/47/63) combined in
+// scalar registers.  Every lane of the wave must be active.
+template <typename Op>
+__device__ __forceinline__ int wave_reduce(int v, int ident, Op op) {
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x111, 0xF, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x112, 0xF, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x114, 0xF, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x118, 0xF, 0xF, false));
+  const int a = __builtin_amdgcn_readlane(v, 15), b = __builtin_amdgcn_readlane(v, 31);
+  const int c = __builtin_amdgcn_readlane(v, 47), d = __builtin_amdgcn_readlane(v, 63);
+  return op(op(a, b), op(c, d));
+}
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, 0, [](int x, int y) { return (int)((uint32_t)x + (uint32_t)y); });
 }
 __device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, INT_MIN, [](int x, int y) { return max(x, y); });
 }
 __device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, INT_MAX, [](int x, int y) { return min(x, y); });
 }
 
 __device__ __forceinline__ int sbyte(int x, int b) { return __builtin_amdgcn_sbfe(x, 8 * b, 8); }
@@ -148,42 +168,152 @@ __device__ __forceinline__ void corr_sample(int I, int Q, uint32_t& phase, uint3
   }
 }
 
+// ---- IQ fast path: segment sums with v_dot4 ---------------------------------
+// Between two code-NCO carries (one half-chip, ~8 samples) the E/P/L bits are
+// constant, so acc_X += bit_X * ival(n) over the segment equals bit_X times the
+// segment sum S = sum ival(n) (int32 wrap keeps it exact).  ival/qval of a
+// pair of samples (n, n+1) is ONE v_dot4_i32_i8 of the IF word {I0,Q0,I1,Q1}
+// with the LO word {il(a), ql(a), il(b), ql(b)} resp. {ql(a), -il(a), ql(b),
+// -il(b)} (correlator.c:213-215), a / b the 8-phase LO indices of the two
+// samples; the 64 (a, b) LO word pairs sit in LDS.  A carry between the two
+// samples splits the pair with byte masks.
+__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+
+// |segment sum| <= 64 samples x 512 < 2^23: 24-bit multiplies are exact
+__device__ __forceinline__ void seg_flush(int si, int sq, int lb, int pb, int eb, Acc& cur) {
+  cur.a[0] += (uint32_t)__mul24(lb, si);
+  cur.a[1] += (uint32_t)__mul24(lb, sq);
+  cur.a[2] += (uint32_t)__mul24(pb, si);
+  cur.a[3] += (uint32_t)__mul24(pb, sq);
+  cur.a[4] += (uint32_t)__mul24(eb, si);
+  cur.a[5] += (uint32_t)__mul24(eb, sq);
+}
+
+// the carry branch of correlator.c:243-283 (half-chip step, dump, bit reload);
+// tb: the channel's packed E/P/L row (LDS-staged, or the global table + base)
+template <typename TB>
+__device__ __forceinline__ void code_carry(const Chan& c, uint32_t& hc, int& lb, int& pb, int& eb,
+                                           Acc& cur, Acc& first, bool& switched, TB tb) {
+  hc = (hc + 1u) & 0xFFFFu;
+  const uint32_t ld = hc;
+  if (hc >= c.D) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) { first.a[k] = cur.a[k]; cur.a[k] = 0; }
+    switched = true;
+    hc = 0;
+  }
+  const uint32_t w = tb[ld];
+  lb = (int)(int8_t)(w & 0xFFu);
+  pb = (int)(int8_t)((w >> 8) & 0xFFu);
+  eb = (int)(int8_t)((w >> 16) & 0xFFu);
+}
+
+// one sample (the odd last sample of a tail run): x = {I, Q, 0, 0}
+template <typename TB>
+__device__ __forceinline__ void corr_single(uint32_t x, uint32_t& p0, uint32_t& kph, const Chan& c,
+                                            uint32_t& hc, int& lb, int& pb, int& eb, int& si,
+                                            int& sq, Acc& cur, Acc& first, bool& switched,
+                                            const uint2* __restrict__ lo2, TB tb) {
+  const uint2 lo = lo2[p0 >> 29];
+  p0 += c.cinc;
+  si = dot4(x, lo.x & 0xFFFFu, si);
+  sq = dot4(x, lo.y & 0xFFFFu, sq);
+  const uint32_t k0 = kph + c.kinc2;
+  const bool c0 = k0 < kph;
+  kph = k0;
+  if (c0) {
+    seg_flush(si, sq, lb, pb, eb, cur);
+    code_carry(c, hc, lb, pb, eb, cur, first, switched, tb);
+    si = 0;
+    sq = 0;
+  }
+}
+
+// samples n0, n0+1 (IF word x), carrier phases p0 / p0 + cinc
+template <typename TB>
+__device__ __forceinline__ void corr_pair(uint32_t x, uint32_t& p0, uint32_t& kph, const Chan& c,
+                                          uint32_t& hc, int& lb, int& pb, int& eb, int& si,
+                                          int& sq, Acc& cur, Acc& first, bool& switched,
+                                          const uint2* __restrict__ lo2, TB tb) {
+  const uint32_t p1 = p0 + c.cinc;
+  const uint2 lo = lo2[(p0 >> 29) | ((p1 >> 26) & 0x38u)];
+  p0 = p1 + c.cinc;
+  const uint32_t k0 = kph + c.kinc2;
+  const uint32_t k1 = k0 + c.kinc2;
+  const bool c0 = k0 < kph, c1 = k1 < k0;
+  kph = k1;
+  if (!c0) {
+    si = dot4(x, lo.x, si);
+    sq = dot4(x, lo.y, sq);
+  } else {   // carry after the first sample of the pair
+    si = dot4(x, lo.x & 0xFFFFu, si);
+    sq = dot4(x, lo.y & 0xFFFFu, sq);
+    seg_flush(si, sq, lb, pb, eb, cur);
+    code_carry(c, hc, lb, pb, eb, cur, first, switched, tb);
+    si = dot4(x, lo.x & 0xFFFF0000u, 0);
+    sq = dot4(x, lo.y & 0xFFFF0000u, 0);
+  }
+  if (c1) {
+    seg_flush(si, sq, lb, pb, eb, cur);
+    code_carry(c, hc, lb, pb, eb, cur, first, switched, tb);
+    si = 0;
+    sq = 0;
+  }
+}
+
 __device__ __forceinline__ int xcd_channel(int b, int G) {
   const int q = G >> 3, r = G & 7, x = b & 7, slot = b >> 3;
   return x * q + (x < r ? x : r) + slot;
 }
 
+// One workgroup = cpw channels (cpw = 1024 / threads-per-channel, at most
+// kMaxCpw) x one call; thread group q = threadIdx.x / T runs channel
+// grp*cpw + q.  When every active channel of the workgroup reads the same IF
+// stream (the channels of one receiver), the stream's 64-sample runs are
+// staged once in LDS with coalesced 16-byte loads and shared by the cpw
+// channels: each lane's run would otherwise be 8 loads that put every lane on
+// its own cache line (8x the L2 -> CU bytes, once per channel).
 template <bool IQ>
-__global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
-    const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp,
+__global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
+    const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp, int n_channels, int cpw,
     const gnsscorr_nco_cmd* __restrict__ cmds, gnsscorr_chan_state* __restrict__ state,
     gnsscorr_track_result* __restrict__ res, int32_t* __restrict__ all_dumps, int max_dumps,
-    const uint32_t* __restrict__ pk, int64_t tic_count) {
-  __shared__ int32_t s_sum[kMaxEpochs][6];
+    const uint32_t* __restrict__ pk, int64_t tic_count, int stage_ok) {
+  __shared__ int32_t s_sum[kMaxCpw][kMaxEpochs][6];
+  __shared__ uint2 s_lo[64];
+  __shared__ int s_stream[kMaxCpw];
+  // dynamic LDS: [cpw][kPkStage E/P/L words of the channel's row][staged IF runs]
+  extern __shared__ uint4 s_dyn[];
+  const int T = (int)blockDim.x / cpw;
+  // wave-uniform (T is a multiple of 64): keeps the channel's command, state
+  // and NCO constants in scalar registers
+  const int q = __builtin_amdgcn_readfirstlane((int)threadIdx.x / T);
+  const int tid = (int)threadIdx.x - q * T;
+  uint32_t* s_pk = reinterpret_cast<uint32_t*>(s_dyn) + q * kPkStage;
+  uint4* s_if = s_dyn + cpw * (kPkStage / 4);   // lane runs of 128 B at a 144 B pitch
   // XCD-aware order: workgroup b runs on XCD b % 8, so give every XCD a
   // contiguous channel range -- the channels of one receiver (consecutive
   // channels sharing an IF stream) then hit the same 4 MiB L2 and the stream
   // is fetched from HBM once instead of once per XCD.
-  const int chn = xcd_channel(blockIdx.x, gridDim.x);
-  const gnsscorr_nco_cmd cmd = cmds[chn];
-  gnsscorr_chan_state st = state[chn];
+  TRACK_PSTAMP(0);
+  const int chn = xcd_channel(blockIdx.x, gridDim.x) * cpw + q;
+  const bool have = chn < n_channels;
+  gnsscorr_nco_cmd cmd = {};
+  gnsscorr_chan_state st = {};
+  if (have) {
+    cmd = cmds[chn];
+    st = state[chn];
+  }
   if (cmd.epoch_load >= 0) {  // epoch set, correlator.c:177-182
     const int v = cmd.epoch_load & 0xFFFF;
     st.msbit_reg = v;
     st.ms_counter = v & 0xff;
     st.bit_counter = v >> 8;
   }
-  if (cmd.prn <= 0 || cmd.prn > 32) {  // idle channel (correlator.c:185)
-    if (threadIdx.x == 0) {
-      gnsscorr_track_result r;
-      memset(&r, 0, sizeof r);
-      r.n_dumps = cmd.prn > 32 ? -1 : 0;
-      r.msbit_reg = st.msbit_reg;
-      res[chn] = r;
-      state[chn] = st;
-    }
-    return;
-  }
+  const bool active = have && cmd.prn > 0 && cmd.prn <= 32;   // correlator.c:185
+  if (tid == 0) s_stream[q] = active ? cmd.stream : -1;
 
   Chan c;
   c.P0 = st.carrier_phase;
@@ -198,14 +328,58 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
     else if (c.D <= 0xFFFFu) c.j1 = 1ull + (c.D - h1);
     else c.j1 = kNever;  // uint16 half-chip can never reach D
   }
-  c.base = cmd.prn * GNSSCORR_OSG_ROW;
-
+  c.base = (active ? cmd.prn : 0) * GNSSCORR_OSG_ROW;
+  TRACK_PSTAMP(1);
   const uint64_t Rtot = ((uint64_t)c.K0 + (uint64_t)nsamp * c.kinc2) >> 32;
   const uint32_t ndump = n_dumps_after(c, Rtot);
   const int n_epochs = (int)ndump + 1;
 
-  for (int i = threadIdx.x; i < n_epochs * 6; i += blockDim.x) (&s_sum[0][0])[i] = 0;
+  if (active)
+    for (int i = tid; i < n_epochs * 6; i += T) (&s_sum[q][0][0])[i] = 0;
+  if (IQ && threadIdx.x < 64) {   // LO words of the sample pair (a, b) = (t & 7, t >> 3)
+    const int a = threadIdx.x & 7, b = threadIdx.x >> 3;
+    const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
+    const uint32_t qa = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * a, 4) & 0xFFu;
+    const uint32_t ib = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * b, 4) & 0xFFu;
+    const uint32_t qb = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * b, 4) & 0xFFu;
+    s_lo[threadIdx.x] = make_uint2(ia | qa << 8 | ib << 16 | qb << 24,
+                                   qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24);
+  }
+  // The half-chip table indices of this call lie in [0, max(D, hc0, hc0+1)]
+  // (correlator.c:243-251; the dump reloads from the pre-reset index D):
+  // stage that part of the channel's row in LDS so the reload at every code
+  // carry is an LDS read, not a dependent global-memory round trip.
+  const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
+  const bool pk_lds = IQ && active && c.j1 != kNever && pk_hi < (uint32_t)kPkStage;
+  if (pk_lds)
+    for (uint32_t i = tid; i <= pk_hi; i += T) s_pk[i] = pk[c.base + (int)i];
   __syncthreads();
+  int sst = -1;
+  bool uni = true;
+  for (int k = 0; k < cpw; k++) {
+    const int v = s_stream[k];
+    if (v >= 0) {
+      if (sst < 0) sst = v;
+      else if (v != sst) uni = false;
+    }
+  }
+  const bool stage = IQ && stage_ok && uni && sst >= 0;
+  if (stage) {
+    // full 64-sample runs only; consecutive threads load consecutive 16-byte chunks
+    const int4* g = reinterpret_cast<const int4*>(ifbuf + (int64_t)sst * stream_stride * 2);
+    const int n_full = nsamp / kRun, n_chunks = n_full * (kRun * 2 / 16);
+    for (int ch = threadIdx.x; ch < n_chunks; ch += blockDim.x) {
+      const int4 v = g[ch];
+      s_if[(ch >> 3) * kPitch + (ch & 7)] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    // the whole sample pairs of the tail run go to the next slot (an odd last
+    // sample is read from global memory by its lane)
+    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(g) + n_full * (kRun / 2);
+    uint32_t* t32 = reinterpret_cast<uint32_t*>(s_if + n_full * kPitch);
+    for (int wi = threadIdx.x; wi < (nsamp - n_full * kRun) / 2; wi += blockDim.x) t32[wi] = g32[wi];
+    __syncthreads();
+  }
+  TRACK_PSTAMP(2);
 
   // ---- per-thread run of kRun samples --------------------------------------
   Acc cur, first;
@@ -213,21 +387,72 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
   for (int k = 0; k < 6; k++) { cur.a[k] = 0; first.a[k] = 0; }
   bool switched = false;
   int e0 = 0;
-  const int n0 = threadIdx.x * kRun;
-  if (n0 < nsamp) {
+  const int n0 = tid * kRun;
+  const bool runs = active && n0 < nsamp;
+  if (runs) {
     const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
     uint32_t kph = (uint32_t)X;
     uint32_t phase = c.P0 + (uint32_t)n0 * c.cinc;
     uint32_t hc, ld, ep;
     hc_after(c, X >> 32, hc, ld, ep);
     e0 = (int)ep;
-    const uint32_t w = pk[c.base + (int)ld];
+    const uint32_t w = pk_lds ? s_pk[ld] : pk[c.base + (int)ld];
     int lb = (int)(int8_t)(w & 0xFFu);
     int pb = (int)(int8_t)((w >> 8) & 0xFFu);
     int eb = (int)(int8_t)((w >> 16) & 0xFFu);
     constexpr int kBps = IQ ? 2 : 1;
     const int8_t* src = ifbuf + (int64_t)cmd.stream * stream_stride * kBps + (int64_t)n0 * kBps;
-    if (n0 + kRun <= nsamp) {
+    if (IQ && pk_lds) {   // (a channel whose half-chip range exceeds the staged row takes
+                          //  the per-sample path below, reading the table from global memory)
+      const int4* v = reinterpret_cast<const int4*>(src);
+      constexpr int kVec = kRun * kBps / 16;
+      const int L = min(kRun, nsamp - n0);
+      auto body = [&](auto tb) {
+        int si = 0, sq = 0;
+        if (L == kRun || stage) {
+          // one 16-byte chunk (4 pairs) per iteration with the next one in
+          // flight: a rolled loop keeps the register footprint small enough
+          // for two 1024-thread workgroups per CU.  The tail run (staged in
+          // LDS) goes through the same loop with its missing pairs masked, so
+          // it does not serialise behind the full runs of its wave.
+          const int np = L >> 1;
+          const uint4* run = stage ? &s_if[tid * kPitch] : reinterpret_cast<const uint4*>(v);
+          uint4 nx = run[0];
+#pragma unroll 1
+          for (int j = 0; j < kVec; j++) {
+            const uint4 u = nx;
+            if (j + 1 < kVec) nx = run[j + 1];
+            const uint32_t words[4] = {u.x, u.y, u.z, u.w};
+            if (4 * j + 4 <= np) {
+#pragma unroll
+              for (int wd = 0; wd < 4; wd++)
+                corr_pair(words[wd], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched,
+                          s_lo, tb);
+            } else {
+              for (int wd = 0; wd < 4; wd++)
+                if (4 * j + wd < np)
+                  corr_pair(words[wd], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first,
+                            switched, s_lo, tb);
+            }
+          }
+          if (L & 1)
+            corr_single((uint32_t)(uint8_t)src[2 * (L - 1)] |
+                            (uint32_t)(uint8_t)src[2 * (L - 1) + 1] << 8,
+                        phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched, s_lo, tb);
+        } else {   // tail run without staging (one lane): same arithmetic, word loads
+          const uint32_t* w32 = reinterpret_cast<const uint32_t*>(src);
+          for (int k = 0; k < (L >> 1); k++)
+            corr_pair(w32[k], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched, s_lo,
+                      tb);
+          if (L & 1)
+            corr_single((uint32_t)(uint8_t)src[2 * (L - 1)] |
+                            (uint32_t)(uint8_t)src[2 * (L - 1) + 1] << 8,
+                        phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched, s_lo, tb);
+        }
+        seg_flush(si, sq, lb, pb, eb, cur);
+      };
+      body(s_pk);
+    } else if (n0 + kRun <= nsamp) {
       const int4* v = reinterpret_cast<const int4*>(src);
       constexpr int kVec = kRun * kBps / 16;
 #pragma unroll
@@ -259,11 +484,13 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
     }
   }
 
+  TRACK_PSTAMP(3);
   // ---- epoch-segmented reduction ------------------------------------------
   // thread contributes (e0, switched ? first : cur) and (e0+1, cur) if switched
+  // (a wave never spans two thread groups: T is a multiple of 64)
   const int e_hi_mine = e0 + (switched ? 1 : 0);
-  const int e_lo = wave_min(n0 < nsamp ? e0 : 0x7fffffff);
-  const int e_hi = wave_max(n0 < nsamp ? e_hi_mine : -1);
+  const int e_lo = wave_min(runs ? e0 : 0x7fffffff);
+  const int e_hi = wave_max(runs ? e_hi_mine : -1);
   const int lane = threadIdx.x & 63;
   for (int e = e_lo; e <= e_hi; e++) {
 #pragma unroll
@@ -272,13 +499,23 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
       if (e == e0) v += switched ? first.a[k] : cur.a[k];
       if (switched && e == e0 + 1) v += cur.a[k];
       const int s = wave_sum((int)v);
-      if (lane == 0) atomicAdd(&s_sum[e][k], s);
+      if (lane == 0) atomicAdd(&s_sum[q][e][k], s);
     }
   }
   __syncthreads();
+  TRACK_PSTAMP(4);
 
-  // ---- per-channel epilogue (one thread) ------------------------------------
-  if (threadIdx.x != 0) return;
+  // ---- per-channel epilogue (one thread per channel) ------------------------
+  if (tid != 0 || !have) return;
+  if (!active) {   // idle channel: only the epoch load (correlator.c:177-185)
+    gnsscorr_track_result r;
+    memset(&r, 0, sizeof r);
+    r.n_dumps = cmd.prn > 32 ? -1 : 0;
+    r.msbit_reg = st.msbit_reg;
+    res[chn] = r;
+    state[chn] = st;
+    return;
+  }
   gnsscorr_track_result r;
   memset(&r, 0, sizeof r);
   r.n_dumps = (int)ndump;
@@ -296,7 +533,7 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
     uint32_t v[6];
 #pragma unroll
     for (int k = 0; k < 6; k++)
-      v[k] = (uint32_t)s_sum[d][k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
+      v[k] = (uint32_t)s_sum[q][d][k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
     if (all_dumps && (int)d < max_dumps)
       for (int k = 0; k < 6; k++) all_dumps[((int64_t)chn * max_dumps + d) * 6 + k] = (int32_t)v[k];
     if (d + 1 == ndump)
@@ -307,7 +544,7 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
   }
   uint32_t nacc[6];
   for (int k = 0; k < 6; k++)
-    nacc[k] = (uint32_t)s_sum[ndump][k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
+    nacc[k] = (uint32_t)s_sum[q][ndump][k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
 
   const uint64_t Wtot = ((uint64_t)c.P0 + (uint64_t)nsamp * c.cinc) >> 32;
   uint32_t cycle_end;
@@ -343,6 +580,7 @@ __global__ __launch_bounds__(kMaxThreads) void osg_track_kernel(
   st.bit_counter = bit;
   st.msbit_reg = msbit;
   state[chn] = st;
+  TRACK_PSTAMP(5);
 }
 
 }  // namespace
@@ -362,6 +600,7 @@ struct gnsscorr_track_ctx {
   size_t if_cap = 0;
   int max_dumps = 0;
   int64_t tic = 0, tic_ref = 0;
+  int stage_if = 1;   // GNSSCORR_TRACK_STAGE_IF=0: lanes read their IF runs from global memory
 };
 
 extern "C" int gnsscorr_track_iq(const gnsscorr_track_ctx* ctx) { return ctx && ctx->cfg.iq; }
@@ -394,6 +633,7 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   c->max_dumps = cfg->max_nsamp / GNSSCORR_OSG_ROW + 2;
   c->tic_ref = (int64_t)(cfg->samp_rate * cfg->tic_period);
   c->tic = c->tic_ref;
+  if (const char* e = getenv("GNSSCORR_TRACK_STAGE_IF")) c->stage_if = atoi(e) != 0;
   const int C = cfg->n_channels;
   auto fail = [&](int code) {
     gnsscorr_track_destroy(c);
@@ -460,15 +700,20 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   }
   int threads = (int)((nsamp + kRun - 1) / kRun);
   threads = (threads + 63) & ~63;
-  dim3 grid(c->cfg.n_channels), block(threads);
+  const int cpw = min(kMaxCpw, kMaxThreads / threads);
+  const int C = c->cfg.n_channels;
+  dim3 grid((C + cpw - 1) / cpw), block(threads * cpw);
+  const size_t stage_bytes = (size_t)((nsamp + kRun - 1) / kRun) * kPitch * 16;
+  const int stage = c->cfg.iq && c->stage_if && stage_bytes <= (size_t)kStageMaxBytes;
+  const size_t dyn = c->cfg.iq ? (size_t)cpw * kPkStage * 4 + (stage ? stage_bytes : 0) : 0;
   if (c->cfg.iq)
-    hipLaunchKernelGGL(osg_track_kernel<true>, grid, block, 0, c->stream, d_if, stride,
-                       (int)nsamp, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps, c->d_pk,
-                       tic_count);
+    hipLaunchKernelGGL(osg_track_kernel<true>, grid, block, dyn, c->stream, d_if, stride,
+                       (int)nsamp, C, cpw, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps,
+                       c->d_pk, tic_count, stage);
   else
     hipLaunchKernelGGL(osg_track_kernel<false>, grid, block, 0, c->stream, d_if, stride,
-                       (int)nsamp, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps, c->d_pk,
-                       tic_count);
+                       (int)nsamp, C, cpw, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps,
+                       c->d_pk, tic_count, 0);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
