@@ -52,12 +52,11 @@ namespace {
 constexpr int kRun = 64;              // samples per thread
 constexpr int kMaxThreads = 1024;
 constexpr int kMaxNsamp = kRun * kMaxThreads;
-constexpr int kMaxEpochs = kMaxNsamp / GNSSCORR_OSG_ROW + 2;
 constexpr uint64_t kNever = ~0ull;
 constexpr int kPitch = 9;             // 16-byte chunks per staged lane run (8 + 1 pad)
 constexpr int kStageMaxBytes = 48 * 1024;
-constexpr int kPkStage = 2400;        // LDS words of the E/P/L row (D <= 2399: slew <= 353)
-constexpr int kMaxCpw = 4;            // channels per workgroup
+constexpr int kPk8Stage = 3072;       // LDS bytes of the E/P/L row (D <= 3071: slew <= 1025)
+constexpr int kMaxCpw = 4;            // channels per workgroup (32 waves/CU: two 1024-thread WGs)
 
 // 8-phase LO (correlator.c:203-204) as 4-bit two's-complement nibbles.
 constexpr uint32_t kLutI = 0xEEF1221Fu;  // i_lo = {-1, 1, 2, 2, 1,-1,-2,-2}
@@ -181,14 +180,30 @@ __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
   return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
 }
 
-// |segment sum| <= 64 samples x 512 < 2^23: 24-bit multiplies are exact
+// |segment sum| <= 64 samples x 512 < 2^23 and bits are -1/0/+1: the 24-bit
+// multiply-add is exact (int32 wrap on the accumulator, as the reference).
+// Written as v_mad_i32_i24 directly: left alone, the compiler fuses the
+// 24-bit multiply and the add into a 64-bit v_mad_u64_u32.
+__device__ __forceinline__ uint32_t mad24(int a, int b, uint32_t c) {
+  uint32_t d;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 __device__ __forceinline__ void seg_flush(int si, int sq, int lb, int pb, int eb, Acc& cur) {
-  cur.a[0] += (uint32_t)__mul24(lb, si);
-  cur.a[1] += (uint32_t)__mul24(lb, sq);
-  cur.a[2] += (uint32_t)__mul24(pb, si);
-  cur.a[3] += (uint32_t)__mul24(pb, sq);
-  cur.a[4] += (uint32_t)__mul24(eb, si);
-  cur.a[5] += (uint32_t)__mul24(eb, sq);
+  cur.a[0] = mad24(lb, si, cur.a[0]);
+  cur.a[1] = mad24(lb, sq, cur.a[1]);
+  cur.a[2] = mad24(pb, si, cur.a[2]);
+  cur.a[3] = mad24(pb, sq, cur.a[3]);
+  cur.a[4] = mad24(eb, si, cur.a[4]);
+  cur.a[5] = mad24(eb, sq, cur.a[5]);
+}
+
+// E/P/L bits of one half-chip as three 2-bit two's-complement fields
+// (late | prompt << 2 | early << 4; values -1 / 0 / +1), see pack8_table()
+__device__ __forceinline__ void unpack8(uint32_t w, int& lb, int& pb, int& eb) {
+  lb = __builtin_amdgcn_sbfe((int)w, 0, 2);
+  pb = __builtin_amdgcn_sbfe((int)w, 2, 2);
+  eb = __builtin_amdgcn_sbfe((int)w, 4, 2);
 }
 
 // the carry branch of correlator.c:243-283 (half-chip step, dump, bit reload);
@@ -204,10 +219,7 @@ __device__ __forceinline__ void code_carry(const Chan& c, uint32_t& hc, int& lb,
     switched = true;
     hc = 0;
   }
-  const uint32_t w = tb[ld];
-  lb = (int)(int8_t)(w & 0xFFu);
-  pb = (int)(int8_t)((w >> 8) & 0xFFu);
-  eb = (int)(int8_t)((w >> 16) & 0xFFu);
+  unpack8(tb[ld], lb, pb, eb);
 }
 
 // one sample (the odd last sample of a tail run): x = {I, Q, 0, 0}
@@ -244,6 +256,11 @@ __device__ __forceinline__ void corr_pair(uint32_t x, uint32_t& p0, uint32_t& kp
   const uint32_t k1 = k0 + c.kinc2;
   const bool c0 = k0 < kph, c1 = k1 < k0;
   kph = k1;
+  if (!(c0 | c1)) {   // no code carry in the pair (3 of 4 pairs at 8 samples/half-chip)
+    si = dot4(x, lo.x, si);
+    sq = dot4(x, lo.y, sq);
+    return;
+  }
   if (!c0) {
     si = dot4(x, lo.x, si);
     sq = dot4(x, lo.y, sq);
@@ -280,19 +297,23 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
     const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp, int n_channels, int cpw,
     const gnsscorr_nco_cmd* __restrict__ cmds, gnsscorr_chan_state* __restrict__ state,
     gnsscorr_track_result* __restrict__ res, int32_t* __restrict__ all_dumps, int max_dumps,
-    const uint32_t* __restrict__ pk, int64_t tic_count, int stage_ok) {
-  __shared__ int32_t s_sum[kMaxCpw][kMaxEpochs][6];
+    const uint32_t* __restrict__ pk, const uint8_t* __restrict__ pk8, int64_t tic_count,
+    int stage_ok) {
   __shared__ uint2 s_lo[64];
   __shared__ int s_stream[kMaxCpw];
-  // dynamic LDS: [cpw][kPkStage E/P/L words of the channel's row][staged IF runs]
+  // dynamic LDS: [cpw][ep_cap][6] epoch sums | [cpw][kPk8Stage] E/P/L row bytes |
+  // staged IF runs (lane runs of 128 B at a 144 B pitch)
   extern __shared__ uint4 s_dyn[];
+  const int ep_cap = nsamp / GNSSCORR_OSG_ROW + 2;   // >= epochs of one call
+  const int sum_words = ((cpw * ep_cap * 6) + 3) & ~3;
   const int T = (int)blockDim.x / cpw;
   // wave-uniform (T is a multiple of 64): keeps the channel's command, state
   // and NCO constants in scalar registers
   const int q = __builtin_amdgcn_readfirstlane((int)threadIdx.x / T);
   const int tid = (int)threadIdx.x - q * T;
-  uint32_t* s_pk = reinterpret_cast<uint32_t*>(s_dyn) + q * kPkStage;
-  uint4* s_if = s_dyn + cpw * (kPkStage / 4);   // lane runs of 128 B at a 144 B pitch
+  int32_t* s_sum = reinterpret_cast<int32_t*>(s_dyn) + q * ep_cap * 6;
+  uint8_t* s_pk8 = reinterpret_cast<uint8_t*>(s_dyn) + sum_words * 4 + q * kPk8Stage;
+  uint4* s_if = s_dyn + sum_words / 4 + cpw * (kPk8Stage / 16);
   // XCD-aware order: workgroup b runs on XCD b % 8, so give every XCD a
   // contiguous channel range -- the channels of one receiver (consecutive
   // channels sharing an IF stream) then hit the same 4 MiB L2 and the stream
@@ -335,7 +356,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   const int n_epochs = (int)ndump + 1;
 
   if (active)
-    for (int i = tid; i < n_epochs * 6; i += T) (&s_sum[q][0][0])[i] = 0;
+    for (int i = tid; i < n_epochs * 6; i += T) s_sum[i] = 0;
   if (IQ && threadIdx.x < 64) {   // LO words of the sample pair (a, b) = (t & 7, t >> 3)
     const int a = threadIdx.x & 7, b = threadIdx.x >> 3;
     const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
@@ -350,9 +371,9 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   // stage that part of the channel's row in LDS so the reload at every code
   // carry is an LDS read, not a dependent global-memory round trip.
   const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
-  const bool pk_lds = IQ && active && c.j1 != kNever && pk_hi < (uint32_t)kPkStage;
+  const bool pk_lds = IQ && active && c.j1 != kNever && pk_hi < (uint32_t)kPk8Stage;
   if (pk_lds)
-    for (uint32_t i = tid; i <= pk_hi; i += T) s_pk[i] = pk[c.base + (int)i];
+    for (uint32_t i = tid; i <= pk_hi; i += T) s_pk8[i] = pk8[c.base + (int)i];
   __syncthreads();
   int sst = -1;
   bool uni = true;
@@ -396,10 +417,15 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
     uint32_t hc, ld, ep;
     hc_after(c, X >> 32, hc, ld, ep);
     e0 = (int)ep;
-    const uint32_t w = pk_lds ? s_pk[ld] : pk[c.base + (int)ld];
-    int lb = (int)(int8_t)(w & 0xFFu);
-    int pb = (int)(int8_t)((w >> 8) & 0xFFu);
-    int eb = (int)(int8_t)((w >> 16) & 0xFFu);
+    int lb, pb, eb;
+    if (pk_lds) {
+      unpack8(s_pk8[ld], lb, pb, eb);
+    } else {
+      const uint32_t w = pk[c.base + (int)ld];
+      lb = (int)(int8_t)(w & 0xFFu);
+      pb = (int)(int8_t)((w >> 8) & 0xFFu);
+      eb = (int)(int8_t)((w >> 16) & 0xFFu);
+    }
     constexpr int kBps = IQ ? 2 : 1;
     const int8_t* src = ifbuf + (int64_t)cmd.stream * stream_stride * kBps + (int64_t)n0 * kBps;
     if (IQ && pk_lds) {   // (a channel whose half-chip range exceeds the staged row takes
@@ -451,7 +477,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
         }
         seg_flush(si, sq, lb, pb, eb, cur);
       };
-      body(s_pk);
+      body(s_pk8);
     } else if (n0 + kRun <= nsamp) {
       const int4* v = reinterpret_cast<const int4*>(src);
       constexpr int kVec = kRun * kBps / 16;
@@ -499,7 +525,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
       if (e == e0) v += switched ? first.a[k] : cur.a[k];
       if (switched && e == e0 + 1) v += cur.a[k];
       const int s = wave_sum((int)v);
-      if (lane == 0) atomicAdd(&s_sum[q][e][k], s);
+      if (lane == 0) atomicAdd(&s_sum[e * 6 + k], s);
     }
   }
   __syncthreads();
@@ -533,7 +559,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
     uint32_t v[6];
 #pragma unroll
     for (int k = 0; k < 6; k++)
-      v[k] = (uint32_t)s_sum[q][d][k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
+      v[k] = (uint32_t)s_sum[d * 6 + k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
     if (all_dumps && (int)d < max_dumps)
       for (int k = 0; k < 6; k++) all_dumps[((int64_t)chn * max_dumps + d) * 6 + k] = (int32_t)v[k];
     if (d + 1 == ndump)
@@ -544,7 +570,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   }
   uint32_t nacc[6];
   for (int k = 0; k < 6; k++)
-    nacc[k] = (uint32_t)s_sum[q][ndump][k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
+    nacc[k] = (uint32_t)s_sum[ndump * 6 + k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
 
   const uint64_t Wtot = ((uint64_t)c.P0 + (uint64_t)nsamp * c.cinc) >> 32;
   uint32_t cycle_end;
@@ -592,6 +618,7 @@ struct gnsscorr_track_ctx {
   gnsscorr_track_cfg cfg;
   hipStream_t stream = nullptr;
   uint32_t* d_pk = nullptr;
+  uint8_t* d_pk8 = nullptr;   // the same table as 2-bit E/P/L fields (unpack8)
   gnsscorr_chan_state* d_state = nullptr;
   gnsscorr_nco_cmd* d_cmds = nullptr;
   gnsscorr_track_result* d_res = nullptr;
@@ -641,6 +668,7 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   };
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_pk, sizeof(uint32_t) * GNSSCORR_OSG_PK_LEN) != hipSuccess ||
+      hipMalloc(&c->d_pk8, GNSSCORR_OSG_PK_LEN) != hipSuccess ||
       hipMalloc(&c->d_state, sizeof(gnsscorr_chan_state) * C) != hipSuccess ||
       hipMalloc(&c->d_cmds, sizeof(gnsscorr_nco_cmd) * C) != hipSuccess ||
       hipMalloc(&c->d_res, sizeof(gnsscorr_track_result) * C) != hipSuccess ||
@@ -652,6 +680,13 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   if (!pk) return fail(GNSSCORR_ENOMEM);
   gnsscorr_osg_packed_table(pk);
   hipError_t e = hipMemcpy(c->d_pk, pk, sizeof(uint32_t) * GNSSCORR_OSG_PK_LEN, hipMemcpyHostToDevice);
+  // pack8: each int8 bit (-1 / 0 / +1) of {late, prompt, early} as a 2-bit field
+  for (int i = 0; i < GNSSCORR_OSG_PK_LEN; i++) {
+    uint32_t b = 0;
+    for (int k = 0; k < 3; k++) b |= ((uint32_t)(int8_t)(pk[i] >> (8 * k)) & 3u) << (2 * k);
+    reinterpret_cast<uint8_t*>(pk)[i] = (uint8_t)b;
+  }
+  if (e == hipSuccess) e = hipMemcpy(c->d_pk8, pk, GNSSCORR_OSG_PK_LEN, hipMemcpyHostToDevice);
   free(pk);
   if (e != hipSuccess || hipMemset(c->d_state, 0, sizeof(gnsscorr_chan_state) * C) != hipSuccess) {
     gnsscorr_set_error("gnsscorr_track_create: upload failed: %s", hipGetErrorString(e));
@@ -665,7 +700,7 @@ extern "C" int gnsscorr_track_destroy(gnsscorr_track_ctx* c) {
   if (!c) return GNSSCORR_OK;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_pk, c->d_state, c->d_cmds, c->d_res, c->d_dumps, c->d_if};
+  void* bufs[] = {c->d_pk, c->d_pk8, c->d_state, c->d_cmds, c->d_res, c->d_dumps, c->d_if};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -705,15 +740,17 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   dim3 grid((C + cpw - 1) / cpw), block(threads * cpw);
   const size_t stage_bytes = (size_t)((nsamp + kRun - 1) / kRun) * kPitch * 16;
   const int stage = c->cfg.iq && c->stage_if && stage_bytes <= (size_t)kStageMaxBytes;
-  const size_t dyn = c->cfg.iq ? (size_t)cpw * kPkStage * 4 + (stage ? stage_bytes : 0) : 0;
+  // dynamic LDS: epoch sums, E/P/L row bytes, staged IF (kernel layout)
+  const size_t sum_bytes = (size_t)((cpw * ((int)nsamp / GNSSCORR_OSG_ROW + 2) * 6 + 3) & ~3) * 4;
+  const size_t dyn = sum_bytes + (c->cfg.iq ? (size_t)cpw * kPk8Stage + (stage ? stage_bytes : 0) : 0);
   if (c->cfg.iq)
     hipLaunchKernelGGL(osg_track_kernel<true>, grid, block, dyn, c->stream, d_if, stride,
                        (int)nsamp, C, cpw, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps,
-                       c->d_pk, tic_count, stage);
+                       c->d_pk, c->d_pk8, tic_count, stage);
   else
-    hipLaunchKernelGGL(osg_track_kernel<false>, grid, block, 0, c->stream, d_if, stride,
+    hipLaunchKernelGGL(osg_track_kernel<false>, grid, block, dyn, c->stream, d_if, stride,
                        (int)nsamp, C, cpw, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps,
-                       c->d_pk, tic_count, 0);
+                       c->d_pk, c->d_pk8, tic_count, 0);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }

@@ -52,7 +52,8 @@ int main(int argc, char** argv) {
   const int64_t stride = (int64_t)K * NS;
   if (gnsscorr_track_replay_dev(ctx, d_if, stride, NS, K, d_c, d_r)) { printf("replay failed\n"); return 1; }
   (void)hipDeviceSynchronize();
-  const int W = (C + 3) / 4;   // workgroups: cpw = 4 channels each at 16368 samples
+  const int T = ((NS + 63) / 64 + 63) / 64 * 64, cpw = std::min(4, 1024 / T);
+  const int W = (C + cpw - 1) / cpw;   // workgroups (the library's launch geometry)
   std::vector<unsigned long long> st((size_t)C * 16);
   (void)hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost);   // last step's stamps
   unsigned long long t0 = ~0ull, t1 = 0;
