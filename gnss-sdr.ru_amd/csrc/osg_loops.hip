@@ -351,7 +351,7 @@ extern "C" int gnsscorr_osg_isr_dev(gnsscorr_track_ctx* ctx, const gnsscorr_osg_
     return GNSSCORR_EINVAL;
   }
   hipStream_t s = (hipStream_t)gnsscorr_track_stream(ctx);
-  hipLaunchKernelGGL(osg_isr_kernel, dim3((n_ch + 255) / 256), dim3(256), 0, s, n_ch, *cfg,
+  hipLaunchKernelGGL(osg_isr_kernel, dim3((n_ch + 63) / 64), dim3(64), 0, s, n_ch, *cfg,
                      d_loops, d_cmds, d_res, (gnsscorr_osg_loop*)nullptr);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
@@ -376,7 +376,10 @@ extern "C" int gnsscorr_osg_closed_loop_dev(gnsscorr_track_ctx* ctx,
     int rc = gnsscorr_track_dev(ctx, d_if + k * bytes_per_call, stream_stride, nsamp, d_cmds, r,
                                 nullptr, tic);
     if (rc) return rc;
-    hipLaunchKernelGGL(osg_isr_kernel, dim3((n_ch + 255) / 256), dim3(256), 0, s, n_ch, *cfg,
+    // one wave per workgroup: the per-channel state machine is a serial chain
+    // (64-bit divides in the discriminators), so spread it over as many CUs as
+    // possible instead of stacking four waves on a SIMD
+    hipLaunchKernelGGL(osg_isr_kernel, dim3((n_ch + 63) / 64), dim3(64), 0, s, n_ch, *cfg,
                        d_loops, d_cmds, r, d_loop_hist ? d_loop_hist + (size_t)k * n_ch : nullptr);
     HIP_TRY(hipGetLastError());
   }
