@@ -82,6 +82,30 @@ SDR_JOB = np.dtype([("packet", "<i4"), ("data_off", "<i4"), ("samps", "<i4"), ("
                     ("sbin", "<i4"), ("soff", "<i4"), ("cbin", "<i4", (3,)),
                     ("coff", "<i4", (3,))])
 assert SDR_CHAN.itemsize == 128 and SDR_CORR.itemsize == 24 and SDR_JOB.itemsize == 48
+# gnsscorr_sdr_channel: the Channel object's state (objects/channel.h:53-132)
+_CH_CORE = [("carrier_nco", "<f8"), ("code_nco", "<f8"), ("len", "<i4"), ("count", "<i4"),
+            ("state", "<i4"), ("sv", "<i4"), ("chan", "<i4"), ("I", "<i4", (3,)),
+            ("Q", "<i4", (3,)), ("P", "<i4", (3,)), ("I_prev", "<i4"), ("Q_prev", "<i4"),
+            ("I_avg", "<f4"), ("Q_var", "<f4"), ("P_avg", "<f4"), ("cn0", "<f4"),
+            ("bit_lock", "<i4"), ("bit_lock_pend", "<i4"), ("bit_lock_ticks", "<i4"),
+            ("I_sum20", "<i4"), ("Q_sum20", "<i4"), ("I_buff", "<i4", (20,)),
+            ("Q_buff", "<i4", (20,)), ("P_buff", "<i4", (20,)), ("epoch_20ms", "<i4"),
+            ("epoch_1ms", "<i4"), ("best_epoch", "<i4"), ("valid_frame", "<i4", (5,)),
+            ("navigate", "<i4"), ("z_lock", "<i4"), ("converged", "<i4"), ("frame_z", "<i4"),
+            ("z_count", "<i4"), ("z_count_pend", "<i4"), ("word_buff", "<u4", (12,)),
+            ("frame_lock", "<i4"), ("frame_lock_pend", "<i4"), ("bit_number", "<i4"),
+            ("subframe", "<i4"), ("freq_lock", "<i4"), ("freq_lock_ticks", "<i4"),
+            ("pll", "<f4", (17,)), ("dll", "<f4", (7,))]
+SDR_CHANNEL_CORE = np.dtype(_CH_CORE, align=True)
+SDR_CHANNEL = np.dtype(_CH_CORE + [("fft_buff", "<u4", (512,))], align=True)
+SDR_SUBFRAME = np.dtype([("sv", "<i4"), ("subframe", "<i4"), ("word_buff", "<u4", (12,)),
+                         ("chan", "<i4"), ("ms", "<i4")])
+SDR_FEEDBACK = np.dtype([("carrier_nco", "<f8"), ("code_nco", "<f8"), ("kill", "<u4"),
+                         ("reset_1ms", "<u4"), ("reset_20ms", "<u4"), ("set_z_count", "<u4"),
+                         ("z_count", "<u4"), ("length", "<u4"), ("navigate", "<u4"),
+                         ("pad", "<u4")])
+assert SDR_CHANNEL_CORE.itemsize == 584 and SDR_CHANNEL.itemsize == 2632
+assert SDR_SUBFRAME.itemsize == 64 and SDR_FEEDBACK.itemsize == 48
 SDR_ACQ_STRONG, SDR_ACQ_MEDIUM, SDR_ACQ_WEAK = 0, 1, 2   # ACQ_TYPE_* (acquisition.cpp:584-599)
 SDR_ACQ_MS = {0: 1, 1: 10, 2: 310}                       # ms per request (acquisition.cpp:628-641)
 SDR_RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
@@ -135,6 +159,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sgt_stream",
     "gnsscorr_sdr_prn_codes", "gnsscorr_sdr_sine_gen", "gnsscorr_sdr_acq_create",
     "gnsscorr_sdr_acq_destroy", "gnsscorr_sdr_acq_strong", "gnsscorr_sdr_acq_strong_dev",
+    "gnsscorr_sdr_channel_start", "gnsscorr_sdr_channel_accum_dev",
     "gnsscorr_sdr_acq_sync", "gnsscorr_sdr_acq_stream", "gnsscorr_sdr_acq_prep_dev",
     "gnsscorr_sdr_acq_search_dev", "gnsscorr_sdr_acq_acquire",
     "gnsscorr_sdr_corr_create", "gnsscorr_sdr_corr_destroy", "gnsscorr_sdr_init_chan",
@@ -213,6 +238,8 @@ def lib() -> C.CDLL:
         "gnsscorr_sdr_acq_strong_dev": (I, [P, P, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_sync": (I, [P]),
         "gnsscorr_sdr_acq_prep_dev": (I, [P, I, P, I]),
+        "gnsscorr_sdr_channel_start": (I, [P, I, I, I, I]),
+        "gnsscorr_sdr_channel_accum_dev": (I, [P, I, I, P, P, P, P, P, I, P]),
         "gnsscorr_sdr_acq_search_dev": (I, [P, I, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_acquire": (I, [P, I, P, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_stream": (P, [P]),
@@ -820,6 +847,46 @@ class SdrCorrCtx:
                                             int(acq_doppler), float(packets_since_acq)),
                "gnsscorr_sdr_init_chan")
         return out[0]
+
+    @staticmethod
+    def channel_start(chan, sv, acq_doppler, corr_len=1) -> np.ndarray:
+        """Channel::Clear + Channel::Start (objects/channel.cpp:71-170)."""
+        out = np.zeros(1, SDR_CHANNEL)
+        _check(lib().gnsscorr_sdr_channel_start(_ptr(out), int(chan), int(sv), int(acq_doppler),
+                                                int(corr_len)), "gnsscorr_sdr_channel_start")
+        return out[0]
+
+    def channel_accum_dev(self, n_ch, n_ms, d_corr, d_chans, d_fb, d_fb_last, d_events,
+                          max_events, d_n_events):
+        _check(lib().gnsscorr_sdr_channel_accum_dev(self.h, n_ch, n_ms, d_corr, d_chans, d_fb,
+                                                    d_fb_last, d_events, max_events, d_n_events),
+               "gnsscorr_sdr_channel_accum_dev")
+
+    def channel_accum(self, corr, chans, max_events=4096, all_feedback=True):
+        """n_ms Channel::Accum calls per channel: corr (n_ms, n_ch, 6) int32 rows
+        (I_E, I_P, I_L, Q_E, Q_P, Q_L); chans SDR_CHANNEL[n_ch] updated in place.
+        Returns (feedback SDR_FEEDBACK[n_ms, n_ch] or [n_ch], subframes sorted by (ms, chan))."""
+        corr = np.ascontiguousarray(corr, np.int32)
+        n_ms, n_ch = corr.shape[0], corr.shape[1]
+        assert chans.dtype == SDR_CHANNEL and len(chans) == n_ch
+        d_c = DevBuf.from_array(corr)
+        d_s = DevBuf.from_array(chans)
+        d_fb = DevBuf(max(n_ms, 1) * n_ch * SDR_FEEDBACK.itemsize) if all_feedback else None
+        d_last = DevBuf(n_ch * SDR_FEEDBACK.itemsize)
+        d_ev = DevBuf(max(max_events, 1) * SDR_SUBFRAME.itemsize)
+        d_n = DevBuf.from_array(np.zeros(1, np.int32))
+        self.channel_accum_dev(n_ch, n_ms, d_c.ptr, d_s.ptr, d_fb.ptr if d_fb else None,
+                               d_last.ptr, d_ev.ptr, max_events, d_n.ptr)
+        self.sync()
+        chans[:] = d_s.download(np.uint8).view(SDR_CHANNEL)
+        n = int(d_n.download(np.int32)[0])
+        ev = d_ev.download(np.uint8).view(SDR_SUBFRAME)[:min(n, max_events)]
+        ev = ev[np.lexsort((ev["chan"], ev["ms"]))]
+        if all_feedback:
+            fb = d_fb.download(np.uint8).view(SDR_FEEDBACK)[:n_ms * n_ch].reshape(n_ms, n_ch)
+        else:
+            fb = d_last.download(np.uint8).view(SDR_FEEDBACK)
+        return fb, ev, n
 
     def accum_dev(self, d_packets, n_jobs, d_jobs, d_out):
         _check(lib().gnsscorr_sdr_accum_dev(self.h, d_packets, n_jobs, d_jobs, d_out),

@@ -512,6 +512,60 @@ int gnsscorr_sdr_corr_sync(gnsscorr_sdr_corr_ctx *ctx);
 void *gnsscorr_sdr_corr_stream(gnsscorr_sdr_corr_ctx *ctx);
 
 /* ======================================================================
+ * GPS-SDR channel: Channel::Accum
+ * (objects/channel.cpp:182-279) batched over channels on the GPU, one thread
+ * per channel running its 1-ms calls in order:
+ *   integrate / 20-ms running sums / bit-edge histogram   :185-213
+ *   DumpAccum: powers, P_avg, FrequencyLock (512-point int16 FFT of the
+ *              squared prompt), PLL (3rd order), DLL, Error/Kill  :282-500, 945-993
+ *   EstCN0 :322-355, BitLock :524-611, BitStuff :615-651,
+ *   ProcessDataBit / FrameSync / ParityCheck / ValidFrameFormat :655-904,
+ *   Epoch :502-518, NCO_Command_S feedback :227-278.
+ * Integer state, bit decisions, frame sync, parity and subframes are exact;
+ * the float / double loop state follows the reference's float/double
+ * expression types with FMA contraction off (atan / log10 may differ from
+ * glibc in the last bit).  Valid subframes (ProcessDataBit's pipe write to
+ * the ephemeris task, :687) come out as gnsscorr_sdr_subframe events.
+ * ==================================================================== */
+typedef struct {           /* the Channel object's state (objects/channel.h:53-132) */
+  double   carrier_nco, code_nco;
+  int32_t  len, count, state, sv, chan;     /* state: 0 EMPTY .. 3 NORMAL          */
+  int32_t  I[3], Q[3], P[3], I_prev, Q_prev;
+  float    I_avg, Q_var, P_avg, cn0;
+  int32_t  bit_lock, bit_lock_pend, bit_lock_ticks, I_sum20, Q_sum20;
+  int32_t  I_buff[20], Q_buff[20], P_buff[20];
+  int32_t  epoch_20ms, epoch_1ms, best_epoch;
+  int32_t  valid_frame[5], navigate, z_lock, converged, frame_z, z_count, z_count_pend;
+  uint32_t word_buff[12];
+  int32_t  frame_lock, frame_lock_pend, bit_number, subframe;
+  int32_t  freq_lock, freq_lock_ticks;
+  float    pll[17];        /* Phase_lock_loop: PLLBW FLLBW a3 b3 w0p w0p2 w0p3 a2 w0f w0f2
+                              gain w x z pll_lock fll_lock t (fll_lock: see DESIGN.md) */
+  float    dll[7];         /* Delay_lock_loop: DLLBW x z a w0 w02 t                    */
+  uint32_t fft_buff[512];  /* CPX fft_buff[FREQ_LOCK_POINTS]                          */
+} gnsscorr_sdr_channel;    /* 2632 bytes */
+
+typedef struct {           /* Channel_2_Ephemeris_S (structs.h:60-66) + where / when */
+  int32_t  sv, subframe;
+  uint32_t word_buff[12];
+  int32_t  chan, ms;       /* channel index and 1-ms call index within the launch   */
+} gnsscorr_sdr_subframe;
+
+/* Channel::Clear + Channel::Start (channel.cpp:71-170): corr_len 1 or 20. */
+int gnsscorr_sdr_channel_start(gnsscorr_sdr_channel *ch, int chan, int sv, int acq_doppler,
+                               int corr_len);
+/* n_ms calls of Channel::Accum for each of n_ch channels: d_corr[m*n_ch + c]
+ * is channel c's Correlation_S of call m (E, P, L); d_fb[m*n_ch + c] gets the
+ * NCO_Command_S it fills (d_fb NULL: only the last call's, in d_fb_last).
+ * Valid subframes are appended to d_events (up to max_events; *d_n_events
+ * counts them all, order = call, then channel).  Async on the context stream. */
+int gnsscorr_sdr_channel_accum_dev(gnsscorr_sdr_corr_ctx *ctx, int n_ch, int n_ms,
+                                   const gnsscorr_sdr_corr *d_corr, gnsscorr_sdr_channel *d_ch,
+                                   gnsscorr_sdr_feedback *d_fb, gnsscorr_sdr_feedback *d_fb_last,
+                                   gnsscorr_sdr_subframe *d_events, int max_events,
+                                   int32_t *d_n_events);
+
+/* ======================================================================
  * GPS-SDR sample front end, bit-exact with
  *   GPS_Source::Read_GN3S   objects/gps_source.cpp:684-767 (2-bit LUT {-3,-1,1,3},
  *                           1024-entry table NCO mix, products truncated to int16)

@@ -364,3 +364,69 @@ class OracleSdrCorr:
         packet = np.ascontiguousarray(packet, np.int16)
         self.L.sdrc_correlate(C.byref(self._t), _p(packet), len(states), _p(states), _p(corr),
                               self.saturate, cb if cb is not None else self.test_loop, user)
+
+
+# ---------------------------------------------------------------- GPS-SDR Channel
+REF_CHAN_SO = os.path.join(HERE, "_ref", "libsdr_chan_ref.so")
+
+
+def have_ref_chan() -> bool:
+    return os.path.exists(REF_CHAN_SO)
+
+
+class RefSdrChannel:
+    """The reference Channel object itself (objects/channel.cpp built with
+    -DNO_SIMD, oracle/sdr_chan_ref.cpp): Start, Accum per 1-ms correlation,
+    state read-back and the subframes it writes to the ephemeris pipe."""
+
+    FB = np.dtype([("carrier_nco", "<f8"), ("code_nco", "<f8"), ("kill", "<u4"),
+                   ("reset_1ms", "<u4"), ("reset_20ms", "<u4"), ("set_z_count", "<u4"),
+                   ("z_count", "<u4"), ("length", "<u4"), ("navigate", "<u4"), ("pad", "<u4")])
+    SUB = np.dtype([("sv", "<i4"), ("subframe", "<i4"), ("word_buff", "<u4", (12,))])
+
+    def __init__(self, chan=0):
+        L = C.CDLL(REF_CHAN_SO)
+        P, I = C.c_void_p, C.c_int
+        L.ref_chan_new.restype = P
+        L.ref_chan_new.argtypes = [I]
+        L.ref_chan_free.argtypes = [P]
+        L.ref_chan_start.argtypes = [P, I, I, I]
+        L.ref_chan_accum.argtypes = [P, P, P]
+        L.ref_chan_state.argtypes = [P, P]
+        L.ref_chan_read_subframes.argtypes = [P, I]
+        L.ref_chan_read_subframes.restype = I
+        L.ref_chan_parity.argtypes = [C.c_uint32]
+        L.ref_chan_parity.restype = I
+        self.L = L
+        self.h = L.ref_chan_new(chan)
+        self.ssize = L.ref_chan_state_size()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.ref_chan_free(self.h)
+            self.h = None
+
+    def start(self, sv, doppler, corr_len=1):
+        self.L.ref_chan_start(self.h, int(sv), int(doppler), int(corr_len))
+
+    def state(self) -> np.ndarray:
+        out = np.zeros(self.ssize, np.uint8)
+        self.L.ref_chan_state(self.h, _p(out))
+        return out
+
+    def run(self, corr):
+        """Accum over corr (n_ms, 6) int32; returns (feedback FB[n_ms], subframes as
+        (ms, SUB record) pairs, final state bytes)."""
+        corr = np.ascontiguousarray(corr, np.int32)
+        fb = np.zeros(len(corr), self.FB)
+        subs = []
+        buf = np.zeros(64, self.SUB)
+        for m in range(len(corr)):
+            row = np.ascontiguousarray(corr[m])
+            self.L.ref_chan_accum(self.h, _p(row), fb[m:m + 1].ctypes.data)
+            n = self.L.ref_chan_read_subframes(_p(buf), 64)
+            subs.extend((m, buf[k].copy()) for k in range(n))
+        return fb, subs, self.state()
+
+    def parity(self, word: int) -> bool:
+        return bool(self.L.ref_chan_parity(word & 0xFFFFFFFF))

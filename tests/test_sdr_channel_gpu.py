@@ -1,0 +1,111 @@
+"""GPU parity: the GPS-SDR Channel object batched on the GPU (sdr_channel.hip),
+SURVEY 8(f) ranks 2 and 4: bit lock, bit stuffing, frame sync, ICD-200 parity,
+subframe validation, C/N0, FrequencyLock / PLL / DLL, Error / Kill, and the
+NCO_Command_S feedback of every Channel::Accum call (objects/channel.cpp:182-993).
+
+Against the reference Channel itself: its committed outputs
+(tests/golden/sdr_channel.npz) and, where the reference build travelled with
+the tree (oracle/_ref/libsdr_chan_ref.so), a live run on other streams.
+Integers, flags, bit decisions, word buffers and subframes exact; float /
+double loop state within rtol 1e-6 (atan / log10 may differ in the last bit).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import make_sdr_chan_golden as G
+import sdr_nav_scenarios as N
+import sdr_oracle as S
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FLOATS = ("carrier_nco", "code_nco", "I_avg", "Q_var", "P_avg", "cn0", "pll", "dll")
+
+
+def _start(gpu, scen):
+    ch = np.zeros(len(scen), gpu.SDR_CHANNEL)
+    for k, sc in enumerate(scen):
+        ch[k] = gpu.SdrCorrCtx.channel_start(k, int(sc[0]), int(sc[1]), int(sc[2]))
+    return ch
+
+
+def _cmp_state(got, want_bytes, gpu):
+    want = np.frombuffer(want_bytes.tobytes()[:gpu.SDR_CHANNEL_CORE.itemsize],
+                         gpu.SDR_CHANNEL_CORE)[0]
+    for f in gpu.SDR_CHANNEL_CORE.names:
+        a, b = np.asarray(got[f]), np.asarray(want[f])
+        if f in FLOATS:
+            if f == "pll":   # [15] fll_lock reads an uninitialised local in the reference
+                a, b = np.delete(a, 15), np.delete(b, 15)
+            assert np.allclose(a, b, rtol=1e-6, atol=1e-9), (f, a, b)
+        else:
+            assert (a == b).all(), (f, a, b)
+
+
+def test_golden_scenarios(gpu):
+    g = np.load(os.path.join(GOLD, "sdr_channel.npz"))
+    n_ms = int(g["n_ms"])
+    corr = np.stack([G.scenario_corr(sc, n_ms) for sc in N.SCENARIOS], 1)   # (n_ms, n_ch, 6)
+    ch = _start(gpu, N.SCENARIOS)
+    ctx = gpu.SdrCorrCtx()
+    fb, ev, n_ev = ctx.channel_accum(corr, ch)
+    e = int(g["nco_every"])
+    for k in range(len(N.SCENARIOS)):
+        assert (G.flags_of(fb[:, k]) == g["flags"][k]).all(), k
+        zc = np.where(fb[:, k]["set_z_count"] != 0, fb[:, k]["z_count"], 0)
+        assert (zc == g["z_count"][k]).all()
+        assert np.allclose(fb[::e, k]["carrier_nco"], g["nco"][k][:, 0], rtol=1e-9)
+        assert np.allclose(fb[::e, k]["code_nco"], g["nco"][k][:, 1], rtol=1e-9)
+        _cmp_state(ch[k], g["state"][k], gpu)
+    rows, words = g["sub_rows"], g["sub_words"]
+    order = np.lexsort((rows[:, 0], rows[:, 1]))
+    assert n_ev == len(rows)
+    assert (ev["chan"] == rows[order, 0]).all() and (ev["ms"] == rows[order, 1]).all()
+    assert (ev["sv"] == rows[order, 2]).all() and (ev["subframe"] == rows[order, 3]).all()
+    assert (ev["word_buff"] == words[order]).all()
+
+
+def test_split_launches_equal_one(gpu):
+    """State carries across launches: 3 launches of 5000 calls == one of 15000."""
+    corr = np.stack([G.scenario_corr(sc, 15000) for sc in N.SCENARIOS], 1)
+    ctx = gpu.SdrCorrCtx()
+    a = _start(gpu, N.SCENARIOS)
+    fa, ea, _ = ctx.channel_accum(corr, a)
+    b = _start(gpu, N.SCENARIOS)
+    parts = [ctx.channel_accum(corr[i:i + 5000], b) for i in range(0, 15000, 5000)]
+    assert a.tobytes() == b.tobytes()
+    assert np.concatenate([p[0] for p in parts]).tobytes() == fa.tobytes()
+    assert sum(p[2] for p in parts) == len(ea)
+
+
+@pytest.mark.skipif(not S.have_ref_chan(), reason="reference build (oracle/_ref) absent")
+def test_live_reference_random_streams(gpu):
+    rng = np.random.default_rng(17)
+    scen = [(int(rng.integers(0, 32)), int(rng.integers(-9000, 9000)), int(rng.choice([1, 20])),
+             int(rng.integers(0, 20)), float(rng.uniform(2500, 5000)),
+             float(rng.uniform(300, 1500)), float(rng.uniform(-0.1, 0.1)), -1)
+            for _ in range(6)]
+    n_ms = 22000
+    corr = np.stack([N.correlations(n_ms, N.nav_bits(8, seed=100 + k), sc[3], sc[4], sc[5],
+                                    seed=200 + k, q_bias=sc[6]) for k, sc in enumerate(scen)], 1)
+    ch = _start(gpu, scen)
+    fb, ev, _ = gpu.SdrCorrCtx().channel_accum(corr, ch)
+    for k, sc in enumerate(scen):
+        ref = S.RefSdrChannel(k)
+        ref.start(sc[0], sc[1], sc[2])
+        rfb, subs, st = ref.run(corr[:, k])
+        assert (G.flags_of(fb[:, k]) == G.flags_of(rfb)).all()
+        assert np.allclose(fb[:, k]["carrier_nco"], rfb["carrier_nco"], rtol=1e-9)
+        assert np.allclose(fb[:, k]["code_nco"], rfb["code_nco"], rtol=1e-9)
+        _cmp_state(ch[k], st, gpu)
+        mine = ev[ev["chan"] == k]
+        assert list(mine["ms"]) == [m for m, _ in subs]
+        for (m, s), e in zip(subs, mine):
+            assert (e["word_buff"] == s["word_buff"]).all() and e["subframe"] == s["subframe"]
+
+
+def test_bad_args(gpu):
+    ctx = gpu.SdrCorrCtx()
+    with pytest.raises(gpu.GnssCorrError):
+        ctx.channel_accum_dev(0, 10, None, None, None, None, None, 0, None)
