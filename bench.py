@@ -288,6 +288,7 @@ def run_fullsky(dist, dev, steps, warmup):
 SDR_REC, SDR_SV, SDR_ROWS, SDR_N = 64, 32, 120, 2048
 SDR_CORR_CH = 4096
 SDR_FE_BLOCKS = 2000         # GN3S 5-ms reads per front-end launch (10 s of 4 Msps 2-bit samples)
+SDR_CHAN_N, SDR_CHAN_MS = 8192, 1000   # Channel objects x 1-ms Channel::Accum calls per launch
 
 
 def run_sdr(dist, dev, steps, warmup):
@@ -378,8 +379,41 @@ def run_sdr(dist, dev, steps, warmup):
         acq.sync()
         mw[kind] = dict(dt=dist.max(time.perf_counter() - t0), ms=e0.elapsed_ms(e1) / k_steps,
                         steps=k_steps)
+    # Channel objects (bit lock, frame sync, parity, C/N0, loops): SDR_CHAN_N channels x
+    # SDR_CHAN_MS 1-ms Channel::Accum calls per launch on synthetic navigation streams
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import sdr_nav_scenarios as nav
+    corr1 = nav.correlations(SDR_CHAN_MS, nav.nav_bits(2, seed=3 + dist.rank), 7, 4000.0, 900.0,
+                             seed=5 + dist.rank, q_bias=0.02)
+    shift = np.arange(SDR_CHAN_N) % 20                     # different bit phases per channel
+    corr = np.stack([np.roll(corr1, int(k), 0) for k in shift], 1)
+    chans0 = np.zeros(SDR_CHAN_N, gc.SDR_CHANNEL)
+    for k in range(SDR_CHAN_N):
+        chans0[k] = gc.SdrCorrCtx.channel_start(k, k % 32, 1000 + 10 * (k % 50), 1)
+    d_cc = gc.DevBuf.from_array(corr, dev)
+    d_ch = gc.DevBuf.from_array(chans0, dev)
+    d_last = gc.DevBuf(SDR_CHAN_N * gc.SDR_FEEDBACK.itemsize, dev)
+    d_ev = gc.DevBuf(4096 * gc.SDR_SUBFRAME.itemsize, dev)
+    d_ne = gc.DevBuf.from_array(np.zeros(1, np.int32), dev)
+    ch_steps = max(steps // 10, 3)
+    corr_ctx_k = gc.SdrCorrCtx(device=dev)
+    corr_ctx_k.channel_accum_dev(SDR_CHAN_N, SDR_CHAN_MS, d_cc.ptr, d_ch.ptr, None, d_last.ptr,
+                                 d_ev.ptr, 4096, d_ne.ptr)
+    corr_ctx_k.sync()
+    d_ch.upload(chans0)
+    dist.barrier()
+    t0 = time.perf_counter()
+    e0.record(corr_ctx_k.stream)
+    for _ in range(ch_steps):   # consecutive launches continue the same channels
+        corr_ctx_k.channel_accum_dev(SDR_CHAN_N, SDR_CHAN_MS, d_cc.ptr, d_ch.ptr, None,
+                                     d_last.ptr, d_ev.ptr, 4096, d_ne.ptr)
+    e1.record(corr_ctx_k.stream)
+    corr_ctx_k.sync()
+    dt_ch = dist.max(time.perf_counter() - t0)
+    ms_ch = e0.elapsed_ms(e1) / ch_steps
     return dict(dt_acq=dt_acq, ms_acq=ms_acq, dt_corr=dt_corr, ms_corr=ms_corr, steps=steps,
-                bufs=bufs, dt_fe=dt_fe, ms_fe=ms_fe, mw=mw, long=long)
+                bufs=bufs, dt_fe=dt_fe, ms_fe=ms_fe, mw=mw, long=long, dt_ch=dt_ch, ms_ch=ms_ch,
+                ch_steps=ch_steps, ch_corr=corr1)
 
 
 def cpu_baseline_sdr(bufs, budget_s=5.0):
@@ -424,6 +458,28 @@ def cpu_baseline_sdr_mw(long, kind, budget_s=4.0):
                 sample=f"{rows_done} doAcq{kind.capitalize()} rows (one sv x one 1-kHz step per "
                        f"call) of the scalar C restatement (oracle/sdr_acq.c, bit-exact with the "
                        f"reference -DNO_SIMD primitives), {dt:.1f} s")
+
+
+def cpu_baseline_sdr_channel(corr, budget_s=3.0):
+    """The reference Channel class itself (oracle/_ref, when it travelled with the tree)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sdr_oracle
+    if not sdr_oracle.have_ref_chan():
+        return None
+    r = sdr_oracle.RefSdrChannel(0)
+    r.start(0, 1000, 1)
+    n, t0 = 0, time.perf_counter()
+    row = np.zeros(6, np.int32)
+    fb = np.zeros(1, r.FB)
+    while time.perf_counter() - t0 < budget_s:
+        row[:] = corr[n % len(corr)]
+        r.L.ref_chan_accum(r.h, row.ctypes.data, fb.ctypes.data)
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="channel-ms/s", cores=1, kind="reference",
+                sample=f"{n} Channel::Accum calls of the reference Channel class built from "
+                       f"objects/channel.cpp (oracle/_ref/libsdr_chan_ref.so; includes ctypes "
+                       f"call overhead), {dt:.1f} s")
 
 
 def cpu_baseline_sgt(budget_s=6.0):
@@ -648,6 +704,15 @@ def main():
                                  "unit": "Tops/s (int32 op model, DESIGN.md)",
                                  "frac": ops / (m["ms"] * 1e-3) / 1e12 / PEAK_INT_TOPS},
                 }
+            out["sdr_channel"] = {
+                "metric": "Channel::Accum calls/sec (GPS-SDR channel: bit lock, frame sync, "
+                          "parity, C/N0, FLL/PLL/DLL; exact vs the reference Channel)",
+                "value": SDR_CHAN_N * SDR_CHAN_MS * sdr["ch_steps"] * W / sdr["dt_ch"],
+                "unit": "channel-ms/s",
+                "config": f"{SDR_CHAN_N} channels x {SDR_CHAN_MS} consecutive 1-ms calls per "
+                          "launch (one thread per channel), synthetic 50 bps navigation streams",
+                "kernel_ms_per_launch": sdr["ms_ch"],
+            }
             fe_in = SDR_FE_BLOCKS * gc.GN3S_BLOCK_IN
             fe_bytes = fe_in // 4 + SDR_FE_BLOCKS * gc.GN3S_BLOCK_OUT * 4
             out["sdr_frontend"] = {
@@ -676,6 +741,9 @@ def main():
                 for kind in sdr["mw"]:
                     out[f"sdr_acquisition_{kind}"]["cpu_baseline"] = \
                         cpu_baseline_sdr_mw(sdr["long"], kind)
+                cb = cpu_baseline_sdr_channel(sdr["ch_corr"])
+                if cb:
+                    out["sdr_channel"]["cpu_baseline"] = cb
         print(json.dumps(out))
     dist.close()
 
