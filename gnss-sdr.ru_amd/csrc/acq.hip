@@ -311,12 +311,19 @@ __device__ __forceinline__ int out_base(int t) {
 //   K2: the 16 independent 1023-point (3 x 11 x 31) sub-transforms of a row,
 //       one wavefront each, written straight to the correlation layout (sigma).
 // mode 0: IF row = (freq_id, block); x[n] = IF[block][n] * exp(i f ((n*2)*pi)*ts)
+//         with coh > 1 a block is coh code periods and x[n] = sum over p < coh of
+//         the wiped-off sample n + p*N (phase index n + p*N): the coh*N-point
+//         spectrum of acquisition.sci's settings.acqCohIntegration-ms blocks
+//         against repmat(code, coh) is nonzero only at multiples of coh, where it
+//         equals this folded N-point spectrum times coh x the 1-ms code spectrum,
+//         and its inverse is the same N-periodic power row (GLONASS
+//         acquisition.sci:52-72, 113-135: "The rest are copies of the first 1msec")
 // mode 1: code row c; x[n] = code[c][n]
 constexpr int kFwd1Threads = 256;
 __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
     const int8_t* __restrict__ src, int iq, int n_blocks, const double* __restrict__ freqs,
     double ts, int mode, float2* __restrict__ stage, const double* __restrict__ cfreqs,
-    const int* __restrict__ n_rows_dev) {
+    const int* __restrict__ n_rows_dev, int coh) {
   const int row = blockIdx.x >> 2;
   const int g = (blockIdx.x & 3) * kFwd1Threads + threadIdx.x;
   if (g >= M16) return;
@@ -325,17 +332,23 @@ __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
   if (mode == 0) {
     const int cls = row / n_blocks, blk = row % n_blocks;
     const double f = cfreqs[cls];
-    const int8_t* s = src + (long)blk * N * (iq ? 2 : 1);
+    const int8_t* s = src + (long)blk * coh * N * (iq ? 2 : 1);
 #pragma unroll
     for (int a = 0; a < 16; a++) {
-      const int n = in_index(a * M16 + g);
-      const double I = iq ? (double)s[2 * n] : (double)s[n];
-      const double Q = iq ? (double)s[2 * n + 1] : 0.0;
-      // acquisition.sci:61-62, 107: phasePoints = (0:N-1)*2*%pi*ts; exp(i f pp)
-      const double th = f * ((((double)n * 2.0) * M_PI) * ts);
-      double sn, cs;
-      sincos(th, &sn, &cs);
-      x[a] = (v2f){(float)(I * cs - Q * sn), (float)(I * sn + Q * cs)};
+      const int n0 = in_index(a * M16 + g);
+      double re = 0.0, im = 0.0;
+      for (int p = 0; p < coh; p++) {
+        const int n = n0 + p * N;
+        const double I = iq ? (double)s[2 * n] : (double)s[n];
+        const double Q = iq ? (double)s[2 * n + 1] : 0.0;
+        // acquisition.sci:61-62, 107: phasePoints = (0:coh*N-1)*2*%pi*ts; exp(i f pp)
+        const double th = f * ((((double)n * 2.0) * M_PI) * ts);
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        re += I * cs - Q * sn;
+        im += I * sn + Q * cs;
+      }
+      x[a] = (v2f){(float)re, (float)im};
     }
   } else {
     const int8_t* s = src + (long)row * N;
@@ -1204,6 +1217,7 @@ struct gnsscorr_acq_ctx {
   int* d_nclass = nullptr;
   int n_cu = 256;                       // persistent grid of the pipelined kernel
   int pipe = 1;                         // GNSSCORR_ACQ_PIPE=0: one-unit-per-workgroup kernel
+  int coh = 1;                          // code periods per coherent block (set_coherent)
   float2* d_stage = nullptr;            // forward-FFT staging rows
   size_t cap_stage = 0;
   gnsscorr_acq_row* d_stats = nullptr;  // per (row, block) statistics
@@ -1393,7 +1407,7 @@ static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_
   if (rc) return rc;
   hipLaunchKernelGGL(acq_fwd16_kernel, dim3(n_rows * 4), dim3(kFwd1Threads), 0, c->stream, src, iq,
                      n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, mode, c->d_stage, d_cfreq,
-                     d_nrows);
+                     d_nrows, mode == 0 ? c->coh : 1);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(acq_fwd1023_kernel, dim3(n_rows * 16), dim3(64), 0, c->stream, c->d_stage,
                      c->d_sigma, dst, n_blocks, d_nrows);
@@ -1402,8 +1416,8 @@ static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_
 }
 
 static int check_search(gnsscorr_acq_ctx* c, int n_blocks, int n_freqs, int mode) {
-  if (n_blocks < 1 || n_blocks > c->cfg.max_blocks || n_freqs < 1 || n_freqs > c->cfg.max_freqs ||
-      c->n_codes < 1 ||
+  if (n_blocks < 1 || n_blocks * c->coh > c->cfg.max_blocks || n_freqs < 1 ||
+      n_freqs > c->cfg.max_freqs || c->n_codes < 1 ||
       (mode != GNSSCORR_ACQ_BEST_OF_BLOCKS && mode != GNSSCORR_ACQ_NONCOHERENT)) {
     gnsscorr_set_error("gnsscorr_acq: bad arguments (blocks %d/%d, freqs %d/%d, codes %d)",
                        n_blocks, c->cfg.max_blocks, n_freqs, c->cfg.max_freqs, c->n_codes);
@@ -1548,8 +1562,10 @@ extern "C" int gnsscorr_acq_search_dev(gnsscorr_acq_ctx* c, const int8_t* d_if, 
 static int stage_host(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blocks, int n_freqs,
                       const double* h_freqs, int n_groups, int n_bins, const int32_t* h_gcode,
                       const int32_t* h_gfreq) {
-  if (n_blocks < 1 || n_blocks > c->cfg.max_blocks || n_freqs < 1 || n_freqs > c->cfg.max_freqs) {
-    gnsscorr_set_error("gnsscorr_acq_search: n_blocks/n_freqs outside the context capacity");
+  if (n_blocks < 1 || n_blocks * c->coh > c->cfg.max_blocks || n_freqs < 1 ||
+      n_freqs > c->cfg.max_freqs) {
+    gnsscorr_set_error("gnsscorr_acq_search: n_blocks (x coherent ms) / n_freqs outside the "
+                       "context capacity");
     return GNSSCORR_EINVAL;
   }
   for (int g = 0; g < n_groups; g++) {
@@ -1571,7 +1587,7 @@ static int stage_host(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blo
   if ((rc = grow((void**)&c->d_res, &c->cap_res, n_groups, sizeof(gnsscorr_acq_result)))) return rc;
   if ((rc = grow((void**)&c->d_gcode, &c->cap_gcode, n_groups, sizeof(int)))) return rc;
   if ((rc = grow((void**)&c->d_gfreq, &c->cap_gfreq, R, sizeof(int)))) return rc;
-  HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)n_blocks * N * (iq ? 2 : 1),
+  HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)n_blocks * c->coh * N * (iq ? 2 : 1),
                          hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_freqs, h_freqs, sizeof(double) * n_freqs, hipMemcpyHostToDevice,
                          c->stream));
@@ -1625,6 +1641,16 @@ extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, i
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(h_power, c->d_dump, sizeof(float) * N, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_set_coherent(gnsscorr_acq_ctx* c, int coh_ms) {
+  if (!c || coh_ms < 1 || coh_ms > c->cfg.max_blocks) {
+    gnsscorr_set_error("gnsscorr_acq_set_coherent: need 1 <= coh_ms <= max_blocks");
+    return GNSSCORR_EINVAL;
+  }
+  c->coh = coh_ms;
+  c->spec_blocks = 0;   // resident spectra were made with the previous setting
   return GNSSCORR_OK;
 }
 

@@ -153,7 +153,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_acq_create", "gnsscorr_acq_destroy", "gnsscorr_acq_set_codes",
     "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
     "gnsscorr_acq_spectra_dev", "gnsscorr_acq_correlate_dev", "gnsscorr_acq_select_dev",
-    "gnsscorr_acq_sync", "gnsscorr_acq_stream",
+    "gnsscorr_acq_sync", "gnsscorr_acq_stream", "gnsscorr_acq_set_coherent",
     "gnsscorr_sgt_loop_coefs", "gnsscorr_sgt_init_chan", "gnsscorr_sgt_create",
     "gnsscorr_sgt_destroy", "gnsscorr_sgt_track_dev", "gnsscorr_sgt_track", "gnsscorr_sgt_sync",
     "gnsscorr_sgt_stream",
@@ -221,6 +221,7 @@ def lib() -> C.CDLL:
         "gnsscorr_acq_correlate_dev": (I, [P, I, I, P, I, I, P, P, I, P, P]),
         "gnsscorr_acq_select_dev": (I, [P, I, I, P, P, P, P]),
         "gnsscorr_acq_sync": (I, [P]),
+        "gnsscorr_acq_set_coherent": (I, [P, I]),
         "gnsscorr_acq_stream": (P, [P]),
         "gnsscorr_sgt_loop_coefs": (None, [C.POINTER(SgtCfg)] + [C.POINTER(D)] * 5),
         "gnsscorr_sgt_init_chan": (I, [C.POINTER(SgtCfg), I, I, I64, I64, D, P]),
@@ -524,6 +525,10 @@ class AcqCtx:
                                          _ptr(group_freq), spc, _ptr(rows), _ptr(res)),
                "gnsscorr_acq_search")
         return res, rows.reshape(G, B)
+
+    def set_coherent(self, coh_ms: int):
+        """settings.acqCohIntegration: code periods per coherent block (default 1)."""
+        _check(lib().gnsscorr_acq_set_coherent(self.h, int(coh_ms)), "gnsscorr_acq_set_coherent")
 
     def search_dev(self, d_if, n_blocks, n_freqs, d_freqs, n_groups, n_bins, d_group_code,
                    d_group_freq, d_rows, d_res, spc=16, iq=True, mode=ACQ_BEST_OF_BLOCKS):

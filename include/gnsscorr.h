@@ -287,6 +287,13 @@ int gnsscorr_acq_select_dev(gnsscorr_acq_ctx *ctx, int n_groups, int n_bins, con
                             const int32_t *d_group_freq, gnsscorr_acq_row *d_rows,
                             gnsscorr_acq_result *d_res);
 
+/* Coherent integration of settings.acqCohIntegration code periods per block
+ * (GLONASS acquisition.sci:52-72, default 5): every block of the following
+ * searches is coh_ms x n_samples samples, wiped off with one continuous phase
+ * ramp and correlated against the code repeated coh_ms times; rows hold the
+ * first code period of |ifft|^2 as acquisition.sci keeps them.  Needs
+ * n_blocks * coh_ms <= max_blocks.  Default 1. */
+int gnsscorr_acq_set_coherent(gnsscorr_acq_ctx *ctx, int coh_ms);
 /* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples floats. */
 int gnsscorr_acq_power_row(gnsscorr_acq_ctx *ctx, const int8_t *h_if, int iq, int n_blocks,
                            int block, double freq, int code, float *h_power);

@@ -114,26 +114,30 @@ def _second_peak(row: np.ndarray, code_phase_1b: int, spc: int) -> float:
 
 
 def acquire(IF, fs, codes, freqs, group_freq, group_code=None, spc=16, n_blocks=2, iq=True,
-            noncoherent=False, return_rows=False):
+            noncoherent=False, return_rows=False, coh=1):
     """Search groups (PRN/FCH) over their frequency bins.
 
     codes: (n_codes, N) +-1; freqs: frequency table; group_freq: (G, B) indices
-    into freqs; group_code: (G,) code index per group (default arange)."""
+    into freqs; group_code: (G,) code index per group (default arange).
+    coh: settings.acqCohIntegration (GLONASS acquisition.sci:52-72, 113-135):
+    blocks of coh*N samples, phase points over coh*N, the code repeated coh
+    times (repmat), coh*N-point transforms; rows keep the first N powers."""
     codes = np.asarray(codes)
     group_freq = np.asarray(group_freq)
     G, B = group_freq.shape
     if group_code is None:
         group_code = np.arange(G)
     N = codes.shape[1]
+    L = coh * N
     sig = _signal(IF, iq)
     ts = 1.0 / fs
-    phase_points = np.arange(N) * 2 * np.pi * ts
-    blocks = [sig[b * N:(b + 1) * N] for b in range(n_blocks)]
+    phase_points = np.arange(L) * 2 * np.pi * ts
+    blocks = [sig[b * L:(b + 1) * L] for b in range(n_blocks)]
     spec = {}
     out = []
     rows_out = []
     for g in range(G):
-        cf = np.conj(np.fft.fft(codes[group_code[g]].astype(np.float64)))
+        cf = np.conj(np.fft.fft(np.tile(codes[group_code[g]].astype(np.float64), coh)))
         results = np.zeros((B, N))
         rows = []
         for b in range(B):
@@ -141,7 +145,20 @@ def acquire(IF, fs, codes, freqs, group_freq, group_code=None, spc=16, n_blocks=
             if fi not in spec:
                 sc = np.exp(1j * freqs[fi] * phase_points)
                 spec[fi] = [np.fft.fft(sc * blk) for blk in blocks]
-            acq = [np.abs(np.fft.ifft(X * cf)) ** 2 for X in spec[fi]]
+            full = [np.abs(np.fft.ifft(X * cf)) ** 2 for X in spec[fi]]
+            # the max picks the block over all coh*N values (:128-134), the
+            # row keeps the first code period
+            acq = [a[:N] for a in full]
+            if coh > 1 and not noncoherent:
+                chosen = 0
+                for k in range(1, n_blocks):
+                    if not (full[chosen].max() > full[k].max()):
+                        chosen = k
+                results[b] = acq[chosen]
+                am = int(np.argmax(results[b]))
+                rows.append(dict(peak=results[b].max(), argmax=am, block=chosen,
+                                 second=_second_peak(results[b], am + 1, spc)))
+                continue
             if noncoherent:
                 results[b] = np.sum(acq, axis=0)
                 chosen = 0
