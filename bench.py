@@ -285,6 +285,53 @@ def run_fullsky(dist, dev, steps, warmup):
                 cells=46 * N_BINS * N * 10)
 
 
+GLO_COH, GLO_BAND_KHZ = 5, 12.0   # GLONASS initSettings.sci: acqCohIntegration 5, acqSearchBand 12
+
+
+def run_glo_coherent(dist, dev, steps, warmup):
+    """The GLONASS receiver's default acquisition (initSettings.sci:88-96): 14 FCH x 121 bins
+    (12 kHz at 100 Hz) x 2 blocks of 5 ms coherent, resident IF, one search per step."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import acq_oracle
+    rng = np.random.default_rng(0x5EED0009 + dist.rank)
+    glo = rng.choice(np.arange(-7, 7), 4, replace=False)
+    sl = [dict(system=1, fch=int(k), code_phase=float(rng.uniform(0, 511)),
+               doppler=float(rng.uniform(-5000, 5000)), cn0=39.0) for k in glo]
+    IF = gc.ifgen(2 * GLO_COH * N, sl, fs=FS, if_glo=1.0e6, seed=0x5EED000A + dist.rank)
+    nb = int(round(GLO_BAND_KHZ * 2 * GLO_COH)) + 1
+    freqs, gf = [], []
+    for k in range(-7, 7):                                # acquisition.sci:105-108
+        c0 = 1.0e6 + k * 0.5625e6
+        gf.append(np.arange(len(freqs), len(freqs) + nb))
+        freqs.extend(c0 - (GLO_BAND_KHZ / 2) * 1000 + (1000 / (2 * GLO_COH)) * np.arange(nb))
+    freqs, gf = np.array(freqs), np.array(gf, np.int32)
+    ctx = gc.AcqCtx(FS, N, device=dev, max_freqs=len(freqs), max_blocks=2 * GLO_COH, max_codes=1)
+    ctx.set_codes(acq_oracle.make_st_table_row(FS)[None])
+    ctx.set_coherent(GLO_COH)
+    d_if = gc.DevBuf.from_array(IF, dev)
+    d_f = gc.DevBuf.from_array(freqs, dev)
+    d_gc = gc.DevBuf.from_array(np.zeros(14, np.int32), dev)
+    d_gf = gc.DevBuf.from_array(gf, dev)
+    d_rows = gc.DevBuf(14 * nb * gc.ACQ_ROW.itemsize, dev)
+    d_res = gc.DevBuf(14 * gc.ACQ_RESULT.itemsize, dev)
+
+    def step():
+        ctx.search_dev(d_if.ptr, 2, len(freqs), d_f.ptr, 14, nb, d_gc.ptr, d_gf.ptr, d_rows.ptr,
+                       d_res.ptr, spc=32)
+    for _ in range(warmup):
+        step()
+    ctx.sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.sync()
+    dt = dist.max(time.perf_counter() - t0)
+    res = d_res.download(np.uint8).view(gc.ACQ_RESULT)
+    found = int(sum(res[int(k) + 7]["metric"] > 2.5 for k in glo))
+    return dict(dt=dt, steps=steps, nb=nb, found=found, n_planted=len(glo))
+
+
 SDR_REC, SDR_SV, SDR_ROWS, SDR_N = 64, 32, 120, 2048
 SDR_CORR_CH = 4096
 SDR_FE_BLOCKS = 2000         # GN3S 5-ms reads per front-end launch (10 s of 4 Msps 2-bit samples)
@@ -577,6 +624,7 @@ def main():
     sgt = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup)
     sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps // 5, 5), 2)
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
+    gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps // 5, 5), 2)
 
     if dist.rank == 0:
         W = dist.world
@@ -668,6 +716,17 @@ def main():
                           f"x 10 ms non-coherent = {sky['cells']} cell-ms per search; groups "
                           f"sharded round-robin over {W} GPU(s), results gathered over gloo",
                 "planted_found": f"{sky['found']}/{sky['n_planted']}",
+            }
+        if gco:
+            cells = 14 * gco["nb"] * N
+            out["glonass_acquisition_5ms"] = {
+                "metric": "acquisition cells/sec (GLONASS, 5 ms coherent, acquisition.sci)",
+                "value": cells * gco["steps"] * W / gco["dt"], "unit": "cells/s",
+                "ms_per_search": gco["dt"] / gco["steps"] * 1e3,
+                "config": f"GLONASS initSettings.sci defaults: 14 FCH x {gco['nb']} bins (12 kHz "
+                          f"at 100 Hz) x 16368 code phases, 2 blocks of {GLO_COH} ms coherent, "
+                          "16.368 Msps, IF resident in HBM; one search per GPU per step",
+                "planted_found": f"{gco['found']}/{gco['n_planted']}",
             }
         if sdr:
             cells = SDR_REC * SDR_SV * SDR_ROWS * SDR_N
