@@ -319,23 +319,78 @@ __device__ __forceinline__ int out_base(int t) {
 //         and its inverse is the same N-periodic power row (GLONASS
 //         acquisition.sci:52-72, 113-135: "The rest are copies of the first 1msec")
 // mode 1: code row c; x[n] = code[c][n]
+__device__ __forceinline__ double grid_residue(double f, double delta) {
+  double r = fmod(f, delta);
+  return r < 0 ? r + delta : r;
+}
+
+constexpr int kFuseClass = 64;   // frequency tables this short are classified inside fwd16
 constexpr int kFwd1Threads = 256;
+constexpr int kFwd1G = kFwd1Threads / 16;   // radix-16 columns g per workgroup
+// One workgroup = 16 columns g of one row: every thread makes ONE input sample
+// (a, g) -- the wipe-off's fp64 sincos spread over 64 workgroups per row, not
+// 16 per thread -- then 16 threads run the radix-16 of their column.
 __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
     const int8_t* __restrict__ src, int iq, int n_blocks, const double* __restrict__ freqs,
     double ts, int mode, float2* __restrict__ stage, const double* __restrict__ cfreqs,
-    const int* __restrict__ n_rows_dev, int coh) {
-  const int row = blockIdx.x >> 2;
-  const int g = (blockIdx.x & 3) * kFwd1Threads + threadIdx.x;
-  if (g >= M16) return;
-  if (n_rows_dev && row >= *n_rows_dev * n_blocks) return;   // only the spectrum classes
-  v2f x[16];
-  if (mode == 0) {
-    const int cls = row / n_blocks, blk = row % n_blocks;
-    const double f = cfreqs[cls];
-    const int8_t* s = src + (long)blk * coh * N * (iq ? 2 : 1);
-#pragma unroll
-    for (int a = 0; a < 16; a++) {
-      const int n0 = in_index(a * M16 + g);
+    const int* __restrict__ n_rows_dev, int coh, int n_rows, int fuse_n, double delta,
+    int4* __restrict__ fmap_out, double* __restrict__ cfreq_out, int* __restrict__ nclass_out) {
+  __shared__ float2 xs[kFwd1G][17];
+  __shared__ double s_r[kFuseClass], s_cf[kFuseClass];
+  __shared__ int s_l[kFuseClass], s_nc;
+  const int chunks = (M16 + kFwd1G - 1) / kFwd1G;
+  int n_cls_rows = n_rows_dev ? -1 : n_rows;
+  if (fuse_n > 0) {
+    // acq_classify_kernel folded in for short frequency tables: every workgroup
+    // classifies the table in LDS (fuse_n <= kFuseClass lanes), workgroup 0
+    // publishes the map for the later kernels
+    const int t = threadIdx.x;
+    if (t < fuse_n) s_r[t] = grid_residue(freqs[t], delta);
+    __syncthreads();
+    if (t < fuse_n) {
+      int l = t;
+      for (int j = 0; j < t; j++)
+        if (s_r[j] == s_r[t]) { l = j; break; }
+      s_l[t] = l;
+    }
+    __syncthreads();
+    if (t < fuse_n) {
+      const int l = s_l[t];
+      int cls = 0;
+      for (int k = 0; k < l; k++) cls += s_l[k] == k;
+      if (l == t) s_cf[cls] = s_r[t];
+      if (blockIdx.x == 0) {
+        const double q = rint((freqs[t] - s_r[t]) / delta);
+        int mN = (fabs(q) < 1e8 ? (int)q : 0) % N;
+        mN += mN < 0 ? N : 0;
+        fmap_out[t] = make_int4(cls, (15 * mN) & 15, (2 * mN) % 3, ((4 * mN) % 11) * 32 + mN % 31);
+        if (l == t) cfreq_out[cls] = s_r[t];
+      }
+    }
+    if (t == 0) {
+      int cnt = 0;
+      for (int k = 0; k < fuse_n; k++) cnt += s_l[k] == k;
+      s_nc = cnt;
+      if (blockIdx.x == 0) *nclass_out = cnt;
+    }
+    __syncthreads();
+    n_cls_rows = s_nc * n_blocks;
+    cfreqs = s_cf;
+  } else if (n_rows_dev) {
+    n_cls_rows = *n_rows_dev * n_blocks;
+  }
+  // grid-stride over (row, chunk): only the spectrum-class rows exist
+  const int total = n_cls_rows * chunks;
+  for (int w = blockIdx.x; w < total; w += gridDim.x) {
+  const int row = w / chunks, g0 = (w % chunks) * kFwd1G;
+  const int a = threadIdx.x >> 4, gl = threadIdx.x & 15, g = g0 + gl;
+  if (g < M16) {
+    const int n0 = in_index(a * M16 + g);
+    float2 v;
+    if (mode == 0) {
+      const int cls = row / n_blocks, blk = row % n_blocks;
+      const double f = cfreqs[cls];
+      const int8_t* s = src + (long)blk * coh * N * (iq ? 2 : 1);
       double re = 0.0, im = 0.0;
       for (int p = 0; p < coh; p++) {
         const int n = n0 + p * N;
@@ -348,55 +403,106 @@ __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
         re += I * cs - Q * sn;
         im += I * sn + Q * cs;
       }
-      x[a] = (v2f){(float)re, (float)im};
+      v = make_float2((float)re, (float)im);
+    } else {
+      v = make_float2((float)src[(long)row * N + n0], 0.f);
     }
-  } else {
-    const int8_t* s = src + (long)row * N;
-#pragma unroll
-    for (int a = 0; a < 16; a++) x[a] = (v2f){(float)s[in_index(a * M16 + g)], 0.f};
+    xs[gl][a] = v;
   }
-  dft16(x);
-  float2* o = stage + (long)row * NPAD + g;
+  __syncthreads();
+  if (threadIdx.x < kFwd1G && g0 + threadIdx.x < M16) {
+    const int gg = g0 + threadIdx.x;
+    v2f x[16];
 #pragma unroll
-  for (int a = 0; a < 16; a++) o[a * kPlane] = st2(x[a]);
+    for (int k = 0; k < 16; k++) x[k] = ld2(xs[threadIdx.x][k]);
+    dft16(x);
+    float2* o = stage + (long)row * NPAD + gg;
+#pragma unroll
+    for (int k = 0; k < 16; k++) o[k * kPlane] = st2(x[k]);
+  }
+  __syncthreads();   // xs is rewritten by the next item
+  }
 }
 
-__global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restrict__ stage,
-                                                        const int* __restrict__ sigma,
-                                                        float2* __restrict__ out, int n_blocks,
-                                                        const int* __restrict__ n_rows_dev) {
+// The 1023-point (3 x 11 x 31) sub-transform of plane a of a row, 512 threads:
+// dft3 over b for the 341 (c, d) columns, dft11 over c for the 93 (b, d)
+// columns, then the 33 radix-31 groups split into their 16 output pairs
+// (X_0 and X_m / X_{31-m} of the symmetric form): 528 tasks, one round.  The
+// scatter targets (sigma) are fetched before the first barrier.
+constexpr int kFwd2Threads = 512;
+__global__ __launch_bounds__(kFwd2Threads) void acq_fwd1023_kernel(
+    const float2* __restrict__ stage, const int* __restrict__ sigma, float2* __restrict__ out,
+    int n_blocks, const int* __restrict__ n_rows_dev, int n_rows) {
   __shared__ float2 sub[M16 + 1];
-  const int row = blockIdx.x >> 4, a = blockIdx.x & 15;
-  if (n_rows_dev && row >= *n_rows_dev * n_blocks) return;
-  const int lane = threadIdx.x;
-  const float2* in = stage + (long)row * NPAD + a * kPlane;
-  for (int i = lane; i < M16; i += 64) sub[i] = in[i];
-  __syncthreads();
-  if (lane < 31) {  // 3 x 11 over (b, c) for fixed d = lane
-    v2f v[3][11];
+  const int total = (n_rows_dev ? *n_rows_dev * n_blocks : n_rows) * 16;
+  const int t = threadIdx.x;
+  for (int w = blockIdx.x; w < total; w += gridDim.x) {
+    const int row = w >> 4, a = w & 15;
+    // radix-31 tasks of this thread: k = t and t + 512 (k < 528)
+    int dst0[2], dst1[2];
 #pragma unroll
-    for (int b = 0; b < 3; b++)
+    for (int r = 0; r < 2; r++) {
+      const int k = t + r * kFwd2Threads;
+      dst0[r] = dst1[r] = 0;
+      if (k < 33 * 16) {
+        const int grp = k >> 4, m = k & 15, p0 = a * M16 + grp * 31;
+        dst0[r] = sigma[p0 + m];
+        dst1[r] = m ? sigma[p0 + 31 - m] : 0;
+      }
+    }
+    const float2* in = stage + (long)row * NPAD + a * kPlane;
+    for (int i = t; i < M16; i += kFwd2Threads) sub[i] = in[i];
+    __syncthreads();
+    if (t < 11 * 31) {   // radix 3 over b, column (c, d)
+      const int c = t / 31, d = t % 31;
+      v2f x0 = ld2(sub[c * 31 + d]), x1 = ld2(sub[(11 + c) * 31 + d]),
+          x2 = ld2(sub[(22 + c) * 31 + d]);
+      dft3(x0, x1, x2);
+      sub[c * 31 + d] = st2(x0);
+      sub[(11 + c) * 31 + d] = st2(x1);
+      sub[(22 + c) * 31 + d] = st2(x2);
+    }
+    __syncthreads();
+    if (t < 3 * 31) {    // radix 11 over c, column (b, d)
+      const int b = t / 31, d = t % 31;
+      v2f v[11];
 #pragma unroll
-      for (int c = 0; c < 11; c++) v[b][c] = ld2(sub[(b * 11 + c) * 31 + lane]);
+      for (int c = 0; c < 11; c++) v[c] = ld2(sub[(b * 11 + c) * 31 + d]);
+      dftp<11>(v);
 #pragma unroll
-    for (int c = 0; c < 11; c++) dft3(v[0][c], v[1][c], v[2][c]);
-#pragma unroll
-    for (int b = 0; b < 3; b++) dftp<11>(v[b]);
-#pragma unroll
-    for (int b = 0; b < 3; b++)
-#pragma unroll
-      for (int c = 0; c < 11; c++) sub[(b * 11 + c) * 31 + lane] = st2(v[b][c]);
-  }
-  __syncthreads();
-  if (lane < 33) {  // radix 31 over d for fixed (b, c) = lane
-    v2f x[31];
-#pragma unroll
-    for (int d = 0; d < 31; d++) x[d] = ld2(sub[lane * 31 + d]);
-    dftp<31>(x);
+      for (int c = 0; c < 11; c++) sub[(b * 11 + c) * 31 + d] = st2(v[c]);
+    }
+    __syncthreads();
     float2* o = out + (long)row * NPAD;
-    const int p0 = a * M16 + lane * 31;
 #pragma unroll
-    for (int d = 0; d < 31; d++) o[sigma[p0 + d]] = st2(x[d]);
+    for (int r = 0; r < 2; r++) {   // radix 31: (group, output pair m)
+      const int k = t + r * kFwd2Threads;
+      if (k >= 33 * 16) break;
+      const int grp = k >> 4, m = k & 15;
+      const float2* x = &sub[grp * 31];
+      const v2f x0 = ld2(x[0]);
+      if (m == 0) {
+        v2f X0 = x0;
+#pragma unroll
+        for (int j = 1; j <= 15; j++) X0 += ld2(x[j]) + ld2(x[31 - j]);
+        o[dst0[r]] = st2(X0);
+      } else {
+        v2f A = x0, B = (v2f){0.f, 0.f};
+        int q = m;
+#pragma unroll
+        for (int j = 1; j <= 15; j++) {   // q = j*m mod 31
+          const v2f xj = ld2(x[j]), xn = ld2(x[31 - j]);
+          A += bc(kCos31[q]) * (xj + xn);
+          B += bc(kSin31[q]) * (xj - xn);
+          q += m;
+          if (q >= 31) q -= 31;
+        }
+        const v2f sb = swp(B);
+        o[dst0[r]] = st2(__builtin_elementwise_fma(sb, (v2f){1.f, -1.f}, A));   // A - i B
+        o[dst1[r]] = st2(__builtin_elementwise_fma(sb, (v2f){-1.f, 1.f}, A));   // A + i B
+      }
+    }
+    __syncthreads();   // sub is reloaded by the next item
   }
 }
 
@@ -407,46 +513,51 @@ __global__ __launch_bounds__(64) void acq_fwd1023_kernel(const float2* __restric
 // frequencies are in the list (sharding / ordering invariant).
 // fmap[i] = {class, 15m mod 16, 2m mod 3, (4m mod 11) * 32 + m mod 31};
 // cfreq[class] = r.
-__device__ __forceinline__ double grid_residue(double f, double delta) {
-  double r = fmod(f, delta);
-  return r < 0 ? r + delta : r;
-}
 
+constexpr int kClassLds = 2048;   // frequencies classified in LDS (larger tables: global scratch)
 __global__ __launch_bounds__(1024) void acq_classify_kernel(const double* __restrict__ freqs,
                                                             int n, double delta,
                                                             int4* __restrict__ fmap,
                                                             double* __restrict__ cfreq,
-                                                            int* __restrict__ n_classes) {
+                                                            int* __restrict__ n_classes,
+                                                            double* __restrict__ resid) {
+  extern __shared__ double s_cls[];   // [n] residues, then [n] int4 (n <= kClassLds)
+  const bool lds = n <= kClassLds;
+  double* R = lds ? s_cls : resid;
+  int4* F = lds ? reinterpret_cast<int4*>(s_cls + ((n + 1) & ~1)) : fmap;
+  // pass 0: every residue once (fmod is a long fp64 sequence)
+  for (int i = threadIdx.x; i < n; i += blockDim.x) R[i] = grid_residue(freqs[i], delta);
+  __syncthreads();
   // pass 1: leader = first j with the same residue; shift m = (f - r) / delta
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const double f = freqs[i], r = grid_residue(f, delta);
+    const double f = freqs[i], r = R[i];
     int l = i;
     for (int j = 0; j < i; j++)
-      if (grid_residue(freqs[j], delta) == r) { l = j; break; }
+      if (R[j] == r) { l = j; break; }
     const double q = rint((f - r) / delta);
-    fmap[i] = make_int4(l, fabs(q) < 1e8 ? (int)q : 0, 0, 0);
+    F[i] = make_int4(l, fabs(q) < 1e8 ? (int)q : 0, 0, 0);
   }
   __syncthreads();
   // pass 2: class id = number of leaders before the leader
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int4 v = fmap[i];
+    const int4 v = F[i];
     int cls = 0;
-    for (int k = 0; k < v.x; k++) cls += fmap[k].x == k;
+    for (int k = 0; k < v.x; k++) cls += F[k].x == k;
     int mN = v.y % N;
     mN += mN < 0 ? N : 0;
-    fmap[i].z = cls;
-    fmap[i].w = mN;
+    F[i].z = cls;
+    F[i].w = mN;
   }
   if (threadIdx.x == 0) {
     int cnt = 0;
-    for (int k = 0; k < n; k++) cnt += fmap[k].x == k;
+    for (int k = 0; k < n; k++) cnt += F[k].x == k;
     *n_classes = cnt;
   }
   __syncthreads();
   // pass 3: class frequencies and the packed shift coordinates
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int4 v = fmap[i];
-    if (v.x == i) cfreq[v.z] = grid_residue(freqs[i], delta);
+    const int4 v = F[i];
+    if (v.x == i) cfreq[v.z] = R[i];
     const int mN = v.w;
     fmap[i] = make_int4(v.z, (15 * mN) & 15, (2 * mN) % 3, ((4 * mN) % 11) * 32 + mN % 31);
   }
@@ -1010,6 +1121,67 @@ __device__ __forceinline__ void write_stats(gnsscorr_acq_row* stats, const UnitI
   stats[(long)uc.rowid * n_blocks + uc.blk] = o;
 }
 
+__device__ __forceinline__ gnsscorr_acq_row combine_blocks(const gnsscorr_acq_row* st,
+                                                          int n_blocks, int mode) {
+  gnsscorr_acq_row r = st[0];
+  if (mode != GNSSCORR_ACQ_NONCOHERENT)
+    for (int k = 1; k < n_blocks; k++)
+      if (!(r.peak > st[k].peak)) r = st[k];
+  return r;
+}
+
+// one wavefront per group (lane = 0..63); see acq_select_kernel
+__device__ void select_group(int g, int lane, const gnsscorr_acq_row* __restrict__ stats,
+                             int n_bins, int n_blocks, int mode,
+                             const int* __restrict__ group_freq,
+                             const double* __restrict__ freqs, gnsscorr_acq_row* __restrict__ rows,
+                             gnsscorr_acq_result* __restrict__ res) {
+  const gnsscorr_acq_row* st = stats + (long)g * n_bins * n_blocks;
+  float pk = -1.f;
+  int bin = 0x7fffffff;
+  for (int b = lane; b < n_bins; b += 64) {
+    const gnsscorr_acq_row r = combine_blocks(st + (long)b * n_blocks, n_blocks, mode);
+    rows[(long)g * n_bins + b] = r;
+    if (r.peak > pk) { pk = r.peak; bin = b; }
+  }
+  if (!res) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(pk, o, 64);
+    const int b2 = __shfl_xor(bin, o, 64);
+    if (v2 > pk || (v2 == pk && b2 < bin)) { pk = v2; bin = b2; }
+  }
+  int cp = 0x7fffffff;
+  for (int b = lane; b < n_bins; b += 64) {
+    const gnsscorr_acq_row r = combine_blocks(st + (long)b * n_blocks, n_blocks, mode);
+    if (r.peak == pk) cp = min(cp, r.argmax);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cp = min(cp, __shfl_xor(cp, o, 64));
+  if (lane == 0) {
+    const gnsscorr_acq_row rb = combine_blocks(st + (long)bin * n_blocks, n_blocks, mode);
+    gnsscorr_acq_result o;
+    o.peak = pk;
+    o.second = rb.second;
+    o.metric = pk / rb.second;
+    o.bin = bin;
+    o.code_phase = cp + 1;
+    // 1 if an exact tie put the global first column in another row than the
+    // winning row's own argmax (second peak then centred on the row's argmax)
+    o.pad = cp != rb.argmax;
+    o.carr_freq = freqs[group_freq[(long)g * n_bins + bin]];
+    res[g] = o;
+  }
+}
+
+__global__ __launch_bounds__(64) void acq_select_kernel(
+    const gnsscorr_acq_row* __restrict__ stats, int n_groups, int n_bins, int n_blocks, int mode,
+    const int* __restrict__ group_freq, const double* __restrict__ freqs,
+    gnsscorr_acq_row* __restrict__ rows, gnsscorr_acq_result* __restrict__ res) {
+  select_group(blockIdx.x, threadIdx.x, stats, n_bins, n_blocks, mode, group_freq, freqs, rows,
+               res);
+}
+
 // BEST_OF_BLOCKS statistics only (unit = (row, block)); launched with at most
 // one workgroup per CU, each looping over units u = blockIdx.x + k * gridDim.x.
 // Three barriers per unit:
@@ -1133,59 +1305,6 @@ __global__ __launch_bounds__(kPipeThreads) void acq_corr_pipe_kernel(
 //  select    acquisition.sci:141-186 -- frequencyBinIndex = first row with the
 //            largest max, codePhase = first column holding it, metric =
 //            peak / second.
-__device__ __forceinline__ gnsscorr_acq_row combine_blocks(const gnsscorr_acq_row* st,
-                                                          int n_blocks, int mode) {
-  gnsscorr_acq_row r = st[0];
-  if (mode != GNSSCORR_ACQ_NONCOHERENT)
-    for (int k = 1; k < n_blocks; k++)
-      if (!(r.peak > st[k].peak)) r = st[k];
-  return r;
-}
-
-__global__ __launch_bounds__(64) void acq_select_kernel(
-    const gnsscorr_acq_row* __restrict__ stats, int n_groups, int n_bins, int n_blocks, int mode,
-    const int* __restrict__ group_freq, const double* __restrict__ freqs,
-    gnsscorr_acq_row* __restrict__ rows, gnsscorr_acq_result* __restrict__ res) {
-  const int g = blockIdx.x;
-  const int lane = threadIdx.x;
-  const gnsscorr_acq_row* st = stats + (long)g * n_bins * n_blocks;
-  float pk = -1.f;
-  int bin = 0x7fffffff;
-  for (int b = lane; b < n_bins; b += 64) {
-    const gnsscorr_acq_row r = combine_blocks(st + (long)b * n_blocks, n_blocks, mode);
-    rows[(long)g * n_bins + b] = r;
-    if (r.peak > pk) { pk = r.peak; bin = b; }
-  }
-  if (!res) return;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float v2 = __shfl_xor(pk, o, 64);
-    const int b2 = __shfl_xor(bin, o, 64);
-    if (v2 > pk || (v2 == pk && b2 < bin)) { pk = v2; bin = b2; }
-  }
-  int cp = 0x7fffffff;
-  for (int b = lane; b < n_bins; b += 64) {
-    const gnsscorr_acq_row r = combine_blocks(st + (long)b * n_blocks, n_blocks, mode);
-    if (r.peak == pk) cp = min(cp, r.argmax);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) cp = min(cp, __shfl_xor(cp, o, 64));
-  if (lane == 0) {
-    const gnsscorr_acq_row rb = combine_blocks(st + (long)bin * n_blocks, n_blocks, mode);
-    gnsscorr_acq_result o;
-    o.peak = pk;
-    o.second = rb.second;
-    o.metric = pk / rb.second;
-    o.bin = bin;
-    o.code_phase = cp + 1;
-    // 1 if an exact tie put the global first column in another row than the
-    // winning row's own argmax (second peak then centred on the row's argmax)
-    o.pad = cp != rb.argmax;
-    o.carr_freq = freqs[group_freq[(long)g * n_bins + bin]];
-    res[g] = o;
-  }
-}
-
 // ---- host-side index tables ---------------------------------------------------
 static int host_in_index(int p) {
   const int d = p % 31, c = (p / 31) % 11, b = (p / 341) % 3, a = p / 1023;
@@ -1214,6 +1333,7 @@ struct gnsscorr_acq_ctx {
   size_t cap_order = 0;
   int4* d_fmap = nullptr;               // per frequency: spectrum class + shift coordinates
   double* d_cfreq = nullptr;            // per class: the residue frequency whose spectrum is computed
+  double* d_resid = nullptr;            // per frequency: its fs/N-grid residue (classify scratch)
   int* d_nclass = nullptr;
   int n_cu = 256;                       // persistent grid of the pipelined kernel
   int pipe = 1;                         // GNSSCORR_ACQ_PIPE=0: one-unit-per-workgroup kernel
@@ -1236,7 +1356,7 @@ struct gnsscorr_acq_ctx {
 
 static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
                           const double* d_freqs, int mode, int n_rows, float2* dst,
-                          const double* d_cfreq, const int* d_nrows);
+                          const double* d_cfreq, const int* d_nrows, int fuse_n = 0);
 
 static int grow(void** p, size_t* cap, size_t need, size_t elem) {
   if (need <= *cap) return GNSSCORR_OK;
@@ -1297,6 +1417,7 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
       hipMalloc(&c->d_freqs, sizeof(double) * cfg->max_freqs) != hipSuccess ||
       hipMalloc(&c->d_fmap, sizeof(int4) * cfg->max_freqs) != hipSuccess ||
       hipMalloc(&c->d_cfreq, sizeof(double) * cfg->max_freqs) != hipSuccess ||
+      hipMalloc(&c->d_resid, sizeof(double) * cfg->max_freqs) != hipSuccess ||
       hipMalloc(&c->d_nclass, sizeof(int)) != hipSuccess) {
     gnsscorr_set_error("gnsscorr_acq_create: device allocation failed");
     return fail(GNSSCORR_ENOMEM);
@@ -1327,7 +1448,7 @@ extern "C" int gnsscorr_acq_destroy(gnsscorr_acq_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_sigma, c->d_F, c->d_X, c->d_if, c->d_freqs, c->d_gcode, c->d_gfreq,
                   c->d_rows, c->d_res, c->d_dump, c->d_order, c->d_stage, c->d_stats,
-                  c->d_fmap, c->d_cfreq, c->d_nclass};
+                  c->d_fmap, c->d_cfreq, c->d_resid, c->d_nclass};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1402,15 +1523,22 @@ static int ensure_order(gnsscorr_acq_ctx* c, int n_groups, int n_bins, int units
 // forward transform of n_rows rows into dst (padded correlation layout)
 static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
                           const double* d_freqs, int mode, int n_rows, float2* dst,
-                          const double* d_cfreq, const int* d_nrows) {
+                          const double* d_cfreq, const int* d_nrows, int fuse_n) {
   int rc = grow((void**)&c->d_stage, &c->cap_stage, (size_t)n_rows * NPAD, sizeof(float2));
   if (rc) return rc;
-  hipLaunchKernelGGL(acq_fwd16_kernel, dim3(n_rows * 4), dim3(kFwd1Threads), 0, c->stream, src, iq,
+  // grid-stride kernels: the device-side class count bounds the work, the grid
+  // only the parallelism (n_rows is an upper bound of the rows)
+  const int g16 = min(n_rows * ((M16 + kFwd1G - 1) / kFwd1G), 4096);
+  const int g1023 = min(n_rows * 16, 1024);
+  hipLaunchKernelGGL(acq_fwd16_kernel, dim3(g16),
+                     dim3(kFwd1Threads), 0, c->stream, src, iq,
                      n_blocks, d_freqs, 1.0 / c->cfg.samp_rate, mode, c->d_stage, d_cfreq,
-                     d_nrows, mode == 0 ? c->coh : 1);
+                     d_nrows, mode == 0 ? c->coh : 1, n_rows, fuse_n, c->cfg.samp_rate / N,
+                     c->d_fmap, c->d_cfreq, c->d_nclass);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(acq_fwd1023_kernel, dim3(n_rows * 16), dim3(64), 0, c->stream, c->d_stage,
-                     c->d_sigma, dst, n_blocks, d_nrows);
+  hipLaunchKernelGGL(acq_fwd1023_kernel, dim3(g1023), dim3(kFwd2Threads), 0, c->stream,
+                     c->d_stage,
+                     c->d_sigma, dst, n_blocks, d_nrows, n_rows);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
@@ -1431,11 +1559,17 @@ static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n
   int rc = check_search(c, n_blocks, n_freqs, GNSSCORR_ACQ_BEST_OF_BLOCKS);
   if (rc) return rc;
   // spectrum classes on the fs/N grid (one forward FFT per class and block)
-  hipLaunchKernelGGL(acq_classify_kernel, dim3(1), dim3(1024), 0, c->stream, d_freqs, n_freqs,
-                     c->cfg.samp_rate / N, c->d_fmap, c->d_cfreq, c->d_nclass);
-  HIP_TRY(hipGetLastError());
+  const int fuse = n_freqs <= kFuseClass ? n_freqs : 0;
+  if (!fuse) {
+    const size_t cls_lds =
+        n_freqs <= kClassLds ? (size_t)((n_freqs + 1) & ~1) * 8 + (size_t)n_freqs * 16 : 0;
+    hipLaunchKernelGGL(acq_classify_kernel, dim3(1), dim3(1024), cls_lds, c->stream, d_freqs,
+                       n_freqs, c->cfg.samp_rate / N, c->d_fmap, c->d_cfreq, c->d_nclass,
+                       c->d_resid);
+    HIP_TRY(hipGetLastError());
+  }
   rc = forward_launch(c, d_if, iq, n_blocks, d_freqs, 0, n_freqs * n_blocks, c->d_X, c->d_cfreq,
-                      c->d_nclass);
+                      c->d_nclass, fuse);
   if (rc) return rc;
   c->spec_blocks = n_blocks;
   c->spec_freqs = n_freqs;
@@ -1468,11 +1602,11 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
   else if (mode == GNSSCORR_ACQ_NONCOHERENT)
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_NONCOHERENT, false);
-  else if (c->pipe)
+  else if (c->pipe) {
     hipLaunchKernelGGL(acq_corr_pipe_kernel, dim3(n_units < c->n_cu ? n_units : c->n_cu),
                        dim3(kPipeThreads), 0, c->stream, c->d_X, c->d_F, n_blocks, d_gcode,
                        d_gfreq, n_bins, spc, c->d_stats, c->d_order, c->d_fmap, n_units);
-  else
+  } else
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, false);
 #undef ACQ_CORR_LAUNCH
   HIP_TRY(hipGetLastError());
