@@ -778,45 +778,71 @@ __device__ __forceinline__ void dft16_r(v2f (&r)[33]) {
 // r[16..31] (8-byte loads: consecutive lanes read consecutive columns, and the
 // LDS writes of store16_r are bank-conflict free).  g1 = 1023 (tl = 511) is the
 // zero pad column of the HBM rows; it is loaded but never stored.
+// Column pairs of the stream role.  A code is real, so its spectrum is
+// conjugate-symmetric: F[-k] = conj(F[k]).  Negation acts on the PFA slot
+// coordinates one by one ((a, b, c, d) -> (-a, -b, -c, -d), the input map is
+// linear), so stream thread tl owns group g = pair_group(tl) and its negative
+// neg_group(g): 511 such pairs plus group 0 (self-paired, tl = 511, written
+// twice with the same values) cover the 1023 groups, and only the 16 code
+// values of g are loaded (acq_symmetrize_kernel makes the stored F exactly
+// symmetric, so the derived half equals the stored one bit for bit).
+__device__ __forceinline__ int pair_group(int tl) {
+  if (tl < 495) return (tl / 15) * 31 + 1 + tl % 15;   // d = 1..15, every (b, c)
+  if (tl < 510) {                                      // d = 0, c = 1..5, every b
+    const int j = tl - 495;
+    return ((j / 5) * 11 + 1 + j % 5) * 31;
+  }
+  return tl == 510 ? 341 : 0;                          // (1, 0, 0), then group 0
+}
+
+__device__ __forceinline__ int neg_group(int g) {
+  const int d = g % 31, bc = g / 31, c = bc % 11, b = bc / 11;
+  return (((3 - b) % 3) * 11 + (11 - c) % 11) * 31 + (31 - d) % 31;
+}
+
 __device__ __forceinline__ void load_mul_r(const float2* __restrict__ Xb,
                                            const float2* __restrict__ Fc, int tl,
                                            const Shift& sh, v2f (&r)[33]) {
   const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)Xb, 0, NPAD * 8, 0x00020000);
   const auto rf = __builtin_amdgcn_make_buffer_rsrc((void*)Fc, 0, NPAD * 8, 0x00020000);
-  // tl is made opaque so that the (b, c, d) decomposition of its groups is
-  // recomputed per unit instead of being hoisted out of the unit loop
-  int g0 = tl;
-  asm volatile("" : "+v"(g0));
-  const int f0off = g0 * 8, f1off = (g0 + kRole) * 8;
+  // tl is made opaque so that the group arithmetic is recomputed per unit
+  // instead of being hoisted out of the unit loop
+  int t0 = tl;
+  asm volatile("" : "+v"(t0));
+  const int ga = pair_group(t0), gb = neg_group(ga);
+  const int foff = ga * 8;
   // Planes in groups of kLdGroup: all loads of a group are issued before any
   // of its products (sched_group_barrier pins the VMEM reads first), so a
   // unit costs 16 / kLdGroup L2 round trips instead of one per plane.
+  // Column ga takes plane a with F[a]; column gb takes plane -a with conj(F[a]).
   constexpr int kLdGroup = ACQ_LDGROUP;
-  int x0off = f0off, x1off = f1off;
+  int x0off = foff, x1off = gb * 8;
   int pa_shift = 0;
   if (!(sh.a == 0 && sh.b == 0 && sh.c == 0 && sh.d == 0)) {   // uniform branch
-    x0off = shift_group(g0, sh) * 8;
-    x1off = shift_group(g0 + kRole < M16 ? g0 + kRole : 0, sh) * 8;
+    x0off = shift_group(ga, sh) * 8;
+    x1off = shift_group(gb, sh) * 8;
     pa_shift = sh.a;
   }
 #pragma unroll
   for (int a0 = 0; a0 < 16; a0 += kLdGroup) {
-    f2v U0[kLdGroup], U1[kLdGroup], F0[kLdGroup], F1[kLdGroup];
+    f2v U0[kLdGroup], U1[kLdGroup], F0[kLdGroup];
 #pragma unroll
     for (int a = 0; a < kLdGroup; a++) {
+      const int an = (16 - (a0 + a)) & 15;
       const int pa = ((a0 + a - pa_shift) & 15) * kPlane * 8;
+      const int pn = ((an - pa_shift) & 15) * kPlane * 8;
       const int pf = (a0 + a) * kPlane * 8;
       U0[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, x0off, pa, 0));
-      U1[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, x1off, pa, 0));
-      F0[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rf, f0off, pf, 0));
-      F1[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rf, f1off, pf, 0));
+      U1[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rx, x1off, pn, 0));
+      F0[a] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rf, foff, pf, 0));
     }
-    __builtin_amdgcn_sched_group_barrier(0x020, 4 * kLdGroup, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 3 * kLdGroup, 0);
 #pragma unroll
     for (int a = 0; a < kLdGroup; a++) {
-      const v2f f0 = (v2f){F0[a].x, F0[a].y}, f1 = (v2f){F1[a].x, F1[a].y};
+      const int an = (16 - (a0 + a)) & 15;
+      const v2f f0 = (v2f){F0[a].x, F0[a].y}, f1 = (v2f){F0[a].x, -F0[a].y};
       r[a0 + a] = bc(U0[a].x) * f0 + bc(U0[a].y) * mul_mi(f0);
-      r[16 + a0 + a] = bc(U1[a].x) * f1 + bc(U1[a].y) * mul_mi(f1);
+      r[16 + an] = bc(U1[a].x) * f1 + bc(U1[a].y) * mul_mi(f1);
     }
   }
   dft16_r<0>(r);
@@ -828,13 +854,13 @@ __device__ __forceinline__ void load_mul_r(const float2* __restrict__ Xb,
 }
 
 __device__ __forceinline__ void store16_r(float2* lds, int tl, const v2f (&r)[33]) {
-  int g0 = tl;
-  asm volatile("" : "+v"(g0));   // per-unit address arithmetic, not hoisted VGPRs
-  const bool two = g0 + kRole < M16;
+  int t0 = tl;
+  asm volatile("" : "+v"(t0));   // per-unit address arithmetic, not hoisted VGPRs
+  const int ga = pair_group(t0), gb = neg_group(ga);
 #pragma unroll
   for (int a = 0; a < 16; a++) {
-    lds[a * M16 + g0] = st2(r[a]);
-    if (two) lds[a * M16 + g0 + kRole] = st2(r[16 + a]);
+    lds[a * M16 + ga] = st2(r[a]);
+    lds[a * M16 + gb] = st2(r[16 + a]);
   }
 }
 
@@ -1456,6 +1482,25 @@ extern "C" int gnsscorr_acq_destroy(gnsscorr_acq_ctx* c) {
   return GNSSCORR_OK;
 }
 
+// Code spectra are spectra of real sequences; make them exactly
+// conjugate-symmetric (F[-k] = conj(F[k]), F real at k = 0 and N/2) so the
+// pipelined kernel may derive half of them (pair_group).  Slot s = a*M16 + g
+// keeps its value when it precedes its negative and writes the negative.
+__global__ __launch_bounds__(256) void acq_symmetrize_kernel(float2* __restrict__ F,
+                                                             int n_codes) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)n_codes * N) return;
+  const int code = (int)(i / N), sl = (int)(i % N);
+  const int a = sl / M16, g = sl % M16;
+  const int sn = ((16 - a) & 15) * M16 + neg_group(g);
+  float2* Fc = F + (long)code * NPAD;
+  const float2 v = Fc[a * kPlane + g];
+  if (sl == sn)
+    Fc[a * kPlane + g] = make_float2(v.x, 0.f);
+  else if (sl < sn)
+    Fc[(sn / M16) * kPlane + sn % M16] = make_float2(v.x, -v.y);
+}
+
 extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const int8_t* h_codes) {
   if (!c || !h_codes || n_codes < 1 || n_codes > c->cfg.max_codes) {
     gnsscorr_set_error("gnsscorr_acq_set_codes: bad arguments (n_codes %d, max %d)", n_codes,
@@ -1468,6 +1513,9 @@ extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const in
   HIP_TRY(hipMemcpyAsync(d, h_codes, (size_t)n_codes * N, hipMemcpyHostToDevice, c->stream));
   int rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F, nullptr, nullptr);
   if (rc) return rc;
+  hipLaunchKernelGGL(acq_symmetrize_kernel, dim3((n_codes * N + 255) / 256), dim3(256), 0,
+                     c->stream, c->d_F, n_codes);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipFree(d));
   c->n_codes = n_codes;
