@@ -927,11 +927,13 @@ __device__ __forceinline__ void dft31_top2(v2f (&r)[33], float scale, float& m1,
       A += bc(kCos31[q]) * r[j];
       B += bc(kSin31[q]) * r[P - j];
     }
-    const v2f sb = swp(B);
-    const v2f lo = __builtin_elementwise_fma(sb, (v2f){1.f, -1.f}, A);    // X_m = A - i B
-    const v2f hi = __builtin_elementwise_fma(sb, (v2f){-1.f, 1.f}, A);    // X_{P-m} = A + i B
-    top2_push((lo.x * lo.x + lo.y * lo.y) * scale, m, m1, m2, d1);
-    top2_push((hi.x * hi.x + hi.y * hi.y) * scale, P - m, m1, m2, d1);
+    // X_m = A - i B and X_{P-m} = A + i B, held as (re_m, re_{P-m}), (im_m, im_{P-m})
+    // so that both powers come out of three packed instructions
+    const v2f re = __builtin_elementwise_fma(bc(B.y), (v2f){1.f, -1.f}, bc(A.x));
+    const v2f im = __builtin_elementwise_fma(bc(B.x), (v2f){-1.f, 1.f}, bc(A.y));
+    const v2f pw = __builtin_elementwise_fma(im, im, re * re) * bc(scale);
+    top2_push(pw.x, m, m1, m2, d1);
+    top2_push(pw.y, P - m, m1, m2, d1);
   }
 }
 
