@@ -56,7 +56,7 @@
 #define ACQ_STAMP(i)
 #endif
 #ifndef ACQ_LDGROUP         // pipelined kernel: planes per group of row loads
-#define ACQ_LDGROUP 8
+#define ACQ_LDGROUP 16
 #endif
 #ifndef ACQ_PSTAMP          // pipelined kernel: (unit iteration, stamp id), tools/acq_pstamps.hip
 #define ACQ_PSTAMP(it, i)

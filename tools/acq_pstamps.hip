@@ -1,6 +1,7 @@
 // tools/acq_pstamps.hip -- diagnostic build of the pipelined acquisition
 // correlation kernel with s_memtime stamps at its phase boundaries, taken by
-// thread 0 (compute role) and thread 512 (stream role) of every workgroup.
+// lane 0 of every wavefront of every workgroup (role summaries use waves 0
+// and 8, the first of each role; the per-wave table shows the slowest).
 // Not part of the library; run on the GPU box (tools/pstamps.sh).  Read the
 // SHARES, never the run time (stamps serialise the kernel).
 #include <hip/hip_runtime.h>
@@ -10,10 +11,10 @@
 __device__ unsigned long long* g_stamps;
 #define ACQ_PSTAMP(it, i)                                                         \
   do {                                                                            \
-    if ((threadIdx.x & 511) == 0 && (it) < 16) {                                  \
+    if ((threadIdx.x & 63) == 0 && (it) < 16) {                                  \
       unsigned long long _t;                                                      \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");   \
-      g_stamps[((blockIdx.x * 16 + (it)) * 2 + (threadIdx.x >> 9)) * 8 + (i)] = _t; \
+      g_stamps[((blockIdx.x * 16 + (it)) * 16 + (threadIdx.x >> 6)) * 8 + (i)] = _t; \
     }                                                                             \
   } while (0)
 #include "../gnss-sdr.ru_amd/csrc/acq.hip"
@@ -49,7 +50,7 @@ int main() {
   (void)hipMemcpy(dord, ord.data(), U * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(dfm, fm.data(), B * sizeof(int4), hipMemcpyHostToDevice);
   (void)hipMalloc(&drows, U * sizeof(gnsscorr_acq_row));
-  const size_t NS = (size_t)GRID * 16 * 2 * 8;
+  const size_t NS = (size_t)GRID * 16 * 16 * 8;
   (void)hipMalloc(&dst, NS * 8);
   (void)hipMemset(dst, 0, NS * 8);
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst));
@@ -71,7 +72,7 @@ int main() {
     int n = 0;
     for (int b = 0; b < GRID; b++)
       for (int it = 1; it < 10; it++) {   // steady state, skip the prologue iteration
-        const unsigned long long* s = &st[((b * 16 + it) * 2 + role) * 8];
+        const unsigned long long* s = &st[((b * 16 + it) * 16 + role * 8) * 8];
         if (!s[NI]) continue;
         for (int i = 0; i < NI; i++) tot[i] += (double)(s[i + 1] - s[i]);
         n++;
@@ -86,9 +87,24 @@ int main() {
   int np = 0;
   for (int b = 0; b < GRID; b++)
     for (int it = 1; it < 9; it++) {
-      const unsigned long long a = st[((b * 16 + it) * 2) * 8], c = st[((b * 16 + it + 1) * 2) * 8];
+      const unsigned long long a = st[((b * 16 + it) * 16) * 8], c = st[((b * 16 + it + 1) * 16) * 8];
       if (a && c) { per += (double)(c - a); np++; }
     }
   printf("period %.0f cycles per unit\n", per / np);
+  // per wave: work of P1 and P3 (stamp 0 -> 1 and 4 -> 5), steady state
+  printf("wave  P1work  P3work\n");
+  for (int w = 0; w < 16; w++) {
+    double p1 = 0, p3 = 0;
+    int n = 0;
+    for (int b = 0; b < GRID; b++)
+      for (int it = 1; it < 10; it++) {
+        const unsigned long long* s = &st[((b * 16 + it) * 16 + w) * 8];
+        if (!s[6]) continue;
+        p1 += (double)(s[1] - s[0]);
+        p3 += (double)(s[5] - s[4]);
+        n++;
+      }
+    printf("%4d %7.0f %7.0f\n", w, p1 / n, p3 / n);
+  }
   return 0;
 }
