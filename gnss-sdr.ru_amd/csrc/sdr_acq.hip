@@ -76,58 +76,176 @@ __device__ __forceinline__ uint32_t cmulsc(uint32_t a, uint32_t b, int shift, bo
   return sat ? pack(sat16(ti), sat16(tq)) : pack((int16_t)ti, (int16_t)tq);
 }
 
-__device__ __forceinline__ int brev11(int k) { return (int)(__brev((uint32_t)k) >> 21); }
 
 // one radix-2 DIT butterfly of rank r with the reference's wrap points
-// (fft.cpp:403-441: optional >>1 pre-scaling, (b*w + 8192) >> 14, int16 sums)
-__device__ __forceinline__ void bfly(uint32_t* x, int a, int b, int32_t wi, int32_t wq, bool scale) {
-  const uint32_t A = x[a], B = x[b];
+// (fft.cpp:403-441: optional >>1 pre-scaling, (b*w + 8192) >> 14, int16 sums),
+// on registers: A is the top element x[a], B the bottom x[a + 2^r]
+__device__ __forceinline__ void bfly(uint32_t& A, uint32_t& B, uint32_t w, bool scale) {
+  const int32_t wi = lo16(w), wq = hi16(w);
   int16_t ai = lo16(A), aq = hi16(A), bi0 = lo16(B), bq0 = hi16(B);
   if (scale) { ai >>= 1; aq >>= 1; bi0 >>= 1; bq0 >>= 1; }
   int32_t bi = (int32_t)bi0 * wi - (int32_t)bq0 * wq;
   int32_t bq = (int32_t)bi0 * wq + (int32_t)bq0 * wi;
   bi = (bi + 8192) >> 14;
   bq = (bq + 8192) >> 14;
-  x[b] = pack((int16_t)(ai - (int16_t)bi), (int16_t)(aq - (int16_t)bq));
-  x[a] = pack((int16_t)(ai + (int16_t)bi), (int16_t)(aq + (int16_t)bq));
+  B = pack((int16_t)(ai - (int16_t)bi), (int16_t)(aq - (int16_t)bq));
+  A = pack((int16_t)(ai + (int16_t)bi), (int16_t)(aq + (int16_t)bq));
 }
 
-// 11 radix-2 DIT ranks in LDS (fft.cpp:156-180 with the rank/bfly loops of
-// :314-334) over F independent transforms at x + f*kN, T threads; each thread
-// applies its butterflies to all F transforms (one twiddle load per F).
-// tw: packed (c, s) Q14 twiddles, 1024 entries, forward or inverse
-template <int T, int F>
-__device__ void dit_ranks(uint32_t* x, const uint32_t* tw, uint32_t scale_mask) {
-  for (int r = 0; r < kM; r++) {
-    const bool scale = (scale_mask >> r) & 1u;
+// ---------------------------------------------------------------------------
+// The reference's 11-rank radix-2 DIT (fft.cpp:156-180, rank/bfly loops
+// :314-334) run as radix-8 passes in registers.  The butterflies of rank r
+// pair positions a and a + 2^r and use twiddle (a mod 2^r) << (10 - r); the
+// 2^R positions b + m*2^R0 (b with zero bits R0..R0+R-1) are closed under
+// ranks R0..R0+R-1, so one thread can run those R ranks on them in registers
+// with exactly the reference's butterflies and rounding.  11 ranks = passes
+// at R0 = 0, 3, 6 (radix 8) and 9 (radix 4): four LDS round trips and
+// barriers instead of eleven.
+//   LDS layout: bit-reversed positions, padded by 8 words per 64 so that the
+//   R0 = 3 pass (positions 64 apart) is bank-conflict free.
+//   The R0 = 0 pass reads the natural-order input straight from global
+//   memory: position 8g + m holds sample k = brev8(g) + 256 * brev3(m).
+// ---------------------------------------------------------------------------
+constexpr int kNP = kN + kN / 8;     // padded transform stride in LDS (words)
+__device__ __forceinline__ int pad(int a) { return a + ((a >> 6) << 3); }
+__device__ __forceinline__ int brev8(int g) { return (int)(__brev((uint32_t)g) >> 24); }
+__device__ __forceinline__ int nat_k(int g, int m) {
+  constexpr int kBrev3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+  return brev8(g) + 256 * kBrev3[m];
+}
+
+// the 2^R - 1 twiddles of one group: tws[2^s - 1 + i] for rank R0 + s, i < 2^s
+template <int R0, int R>
+__device__ __forceinline__ void group_twiddles(uint32_t* tws, int lo, const uint32_t* tw) {
 #pragma unroll
-    for (int u = 0; u < (kN / 2) / T; u++) {
-      const int t = threadIdx.x + u * T;
-      const int j = t & ((1 << r) - 1);
-      const int a = ((t >> r) << (r + 1)) + j;
-      const uint32_t w = tw[j << (kM - 1 - r)];
+  for (int s = 0; s < R; s++)
 #pragma unroll
-      for (int f = 0; f < F; f++) bfly(x + f * kN, a, a + (1 << r), lo16(w), hi16(w), scale);
-    }
-    __syncthreads();
+    for (int i = 0; i < (1 << s); i++)
+      tws[(1 << s) - 1 + i] = tw[(lo + (i << R0)) << (kM - 1 - R0 - s)];
+}
+
+// ranks R0 .. R0+R-1 on v[m] = x[b + m*2^R0]
+template <int R0, int R, uint32_t MASK>
+__device__ __forceinline__ void dit_group(uint32_t* v, const uint32_t* tws) {
+#pragma unroll
+  for (int s = 0; s < R; s++) {
+    const bool scale = (MASK >> (R0 + s)) & 1u;
+#pragma unroll
+    for (int m = 0; m < (1 << R); m++)
+      if (!(m & (1 << s))) bfly(v[m], v[m + (1 << s)], tws[(1 << s) - 1 + (m & ((1 << s) - 1))], scale);
   }
+}
+
+__device__ __forceinline__ void st_group8(uint32_t* x, int g, const uint32_t* v) {
+  uint4* p = reinterpret_cast<uint4*>(x + pad(8 * g));
+  p[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  p[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+
+// pass R0 = 0 on group g of one transform: in[m] = natural-order samples
+// nat_k(g, m), already wiped off; result to LDS
+template <uint32_t MASK>
+__device__ __forceinline__ void dit_first(uint32_t* x, int g, uint32_t* v, const uint32_t* tw) {
+  uint32_t tws[7];
+  group_twiddles<0, 3>(tws, 0, tw);
+  dit_group<0, 3, MASK>(v, tws);
+  st_group8(x, g, v);
+}
+
+// one in-LDS pass over F transforms (stride kNP) with T threads
+template <int T, int F, int R0, int R, uint32_t MASK>
+__device__ __forceinline__ void dit_pass(uint32_t* x, const uint32_t* tw) {
+  constexpr int E = 1 << R, G = kN >> R;
+  static_assert(T % G == 0 || G % T == 0, "thread / group mapping");
+  if constexpr (T % G == 0) {
+    // fixed group per thread: twiddles loaded once, transforms f strided.
+    // The empty asm keeps the per-group addresses and twiddles from being
+    // hoisted out of an enclosing pass loop (they would stay live and spill).
+    int g = threadIdx.x % G;
+    asm volatile("" : "+v"(g));
+    const int lo = g & ((1 << R0) - 1);
+    const int b = lo | ((g >> R0) << (R0 + R));
+    uint32_t tws[E - 1];
+    group_twiddles<R0, R>(tws, lo, tw);
+#pragma unroll 1
+    for (int f = threadIdx.x / G; f < F; f += T / G) {
+      uint32_t* xf = x + f * kNP;
+      uint32_t v[E];
+#pragma unroll
+      for (int m = 0; m < E; m++) v[m] = xf[pad(b + (m << R0))];
+      dit_group<R0, R, MASK>(v, tws);
+#pragma unroll
+      for (int m = 0; m < E; m++) xf[pad(b + (m << R0))] = v[m];
+    }
+  } else {
+    for (int f = 0; f < F; f++)
+#pragma unroll
+      for (int u = 0; u < G / T; u++) {
+        const int g = threadIdx.x + u * T, lo = g & ((1 << R0) - 1);
+        const int b = lo | ((g >> R0) << (R0 + R));
+        uint32_t tws[E - 1];
+        group_twiddles<R0, R>(tws, lo, tw);
+        uint32_t* xf = x + f * kNP;
+        uint32_t v[E];
+#pragma unroll
+        for (int m = 0; m < E; m++) v[m] = xf[pad(b + (m << R0))];
+        dit_group<R0, R, MASK>(v, tws);
+#pragma unroll
+        for (int m = 0; m < E; m++) xf[pad(b + (m << R0))] = v[m];
+      }
+  }
+}
+
+// the last pass (R0 = 9, radix 4) of a single transform into registers:
+// v[m] = output position g + 512 m
+template <uint32_t MASK>
+__device__ __forceinline__ void dit_last_regs(const uint32_t* x, int g, uint32_t* v, const uint32_t* tw) {
+  uint32_t tws[3];
+  group_twiddles<9, 2>(tws, g, tw);
+#pragma unroll
+  for (int m = 0; m < 4; m++) v[m] = x[pad(g + 512 * m)];
+  dit_group<9, 2, MASK>(v, tws);
+}
+
+// whole transform of one row, T = 256 threads: first pass from the wiped-off
+// natural-order samples produced by load(k), passes 3 and 6 in LDS; returns
+// after the barrier that precedes the last pass
+template <uint32_t MASK, class Load>
+__device__ __forceinline__ void dit_row_256(uint32_t* x, const uint32_t* tw, Load load) {
+  static_assert(kThreads == 256, "one radix-8 group per thread");
+  const int g = threadIdx.x;
+  uint32_t v[8];
+#pragma unroll
+  for (int m = 0; m < 8; m++) v[m] = load(nat_k(g, m));
+  dit_first<MASK>(x, g, v, tw);
+  __syncthreads();
+  dit_pass<kThreads, 1, 3, 3, MASK>(x, tw);
+  __syncthreads();
+  dit_pass<kThreads, 1, 6, 3, MASK>(x, tw);
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(kThreads) void sdr_prep_kernel(
     const uint32_t* __restrict__ buff, const uint32_t* __restrict__ wipe,
     const uint32_t* __restrict__ tw_fwd, uint32_t* __restrict__ X, int saturate) {
-  __shared__ uint32_t x[kN];
+  __shared__ uint32_t x[kNP];
   __shared__ uint32_t tw[kN / 2];
   const int rec = blockIdx.x >> 2, j = blockIdx.x & 3;
   const uint32_t* src = buff + (size_t)rec * kN;
   const uint32_t* wp = wipe + (size_t)j * kN;
   for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_fwd[k];
-  for (int k = threadIdx.x; k < kN; k += kThreads)
-    x[brev11(k)] = cmulsc(src[k], wp[k], 14, saturate != 0);   // + doShuffle
   __syncthreads();
-  dit_ranks<kThreads, 1>(x, tw, 0u);                                         // R1: no scaling
+  const bool sat = saturate != 0;
+  dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });   // R1: no scaling
   uint32_t* dst = X + ((size_t)rec * 4 + j) * kN;
-  for (int k = threadIdx.x; k < kN; k += kThreads) dst[k] = x[k];
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int g = threadIdx.x + u * kThreads;
+    uint32_t v[4];
+    dit_last_regs<0u>(x, g, v, tw);
+#pragma unroll
+    for (int m = 0; m < 4; m++) dst[g + 512 * m] = v[m];
+  }
 }
 
 // per-row result: (magnitude, index) of x86_cmag + x86_max
@@ -135,7 +253,7 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
     const uint32_t* __restrict__ X, const uint32_t* __restrict__ codes,
     const uint32_t* __restrict__ tw_inv, const int32_t* __restrict__ svs, int n_sv, int lmin,
     int n_rows, int saturate, int2* __restrict__ row_out) {
-  __shared__ uint32_t x[kN];
+  __shared__ uint32_t x[kNP];
   __shared__ uint32_t tw[kN / 2];
   __shared__ int2 red[kThreads / 64];
   const int row = blockIdx.x % n_rows;
@@ -145,17 +263,23 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
   const uint32_t* xr = X + ((size_t)rec * 4 + lcv2) * kN;
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
   for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_inv[k];
-  for (int k = threadIdx.x; k < kN; k += kThreads)
-    x[brev11(k)] = cmulsc(xr[(k + lcv) & (kN - 1)], cr[k], 10, saturate != 0);
   __syncthreads();
-  dit_ranks<kThreads, 1>(x, tw, kR2);
-  // x86_cmag (int32 wrap) + x86_max (first index of the strict maximum, > 0)
+  const bool sat = saturate != 0;
+  dit_row_256<kR2>(x, tw, [&](int k) { return cmulsc(xr[(k + lcv) & (kN - 1)], cr[k], 10, sat); });
+  // last pass in registers, then x86_cmag (int32 wrap) + x86_max (first index
+  // of the strict maximum, > 0): ties go to the smaller index
   int32_t best = 0, idx = 0;
-  for (int k = threadIdx.x; k < kN; k += kThreads) {
-    const uint32_t v = x[k];
-    const int32_t i = lo16(v), q = hi16(v);
-    const int32_t p = (int32_t)((uint32_t)(i * i) + (uint32_t)(q * q));
-    if (p > best) { best = p; idx = k; }
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int g = threadIdx.x + u * kThreads;
+    uint32_t v[4];
+    dit_last_regs<kR2>(x, g, v, tw);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int32_t i = lo16(v[m]), q = hi16(v[m]);
+      const int32_t p = (int32_t)((uint32_t)(i * i) + (uint32_t)(q * q));
+      if (p > best || (p == best && g + 512 * m < idx)) { best = p; idx = g + 512 * m; }
+    }
   }
   // reduce: larger magnitude wins, equal magnitude -> smaller index
 #pragma unroll
@@ -220,19 +344,25 @@ __device__ __forceinline__ int32_t dot2(uint32_t a, uint32_t b, int32_t c) {
 __global__ __launch_bounds__(kThreads) void sdr_prep_rows_kernel(
     const uint32_t* __restrict__ buff, int ms, const uint32_t* __restrict__ wipe10,
     const uint32_t* __restrict__ tw_fwd, uint32_t* __restrict__ store, int saturate) {
-  __shared__ uint32_t x[kN];
+  __shared__ uint32_t x[kNP];
   __shared__ uint32_t tw[kN / 2];
   const int nr = 4 * ms;
   const int rec = blockIdx.x / nr, r = blockIdx.x % nr, j = r / ms, m = r % ms;
   const uint32_t* src = buff + ((size_t)rec * ms + m) * kN;
   const uint32_t* wp = wipe10 + (size_t)j * kWipe + (size_t)(m % 10) * kN;
   for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_fwd[k];
-  for (int k = threadIdx.x; k < kN; k += kThreads)
-    x[brev11(k)] = cmulsc(src[k], wp[k], 14, saturate != 0);
   __syncthreads();
-  dit_ranks<kThreads, 1>(x, tw, 0u);
+  const bool sat = saturate != 0;
+  dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });
   uint32_t* dst = store + ((size_t)rec * kStoreRows + r) * kN;
-  for (int k = threadIdx.x; k < kN; k += kThreads) dst[k] = x[k];
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int g = threadIdx.x + u * kThreads;
+    uint32_t v[4];
+    dit_last_regs<0u>(x, g, v, tw);
+#pragma unroll
+    for (int q = 0; q < 4; q++) dst[g + 512 * q] = v[q];
+  }
 }
 
 __device__ __forceinline__ int weak_shift(int i, int lcv, int lcv2) {
@@ -265,9 +395,8 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
     const uint32_t* __restrict__ tw_inv, const uint32_t* __restrict__ dft,
     const int32_t* __restrict__ svs, int n_sv, int lmin, int n_rows, int saturate,
     int2* __restrict__ row_out) {
-  __shared__ uint32_t coh[10 * kN];
+  __shared__ uint32_t coh[10 * kNP];
   __shared__ uint32_t tw[kN / 2];
-  __shared__ uint32_t dw[200];
   __shared__ int2 red[kCoh / 64];
   const int row = blockIdx.x % n_rows;
   const int s = (blockIdx.x / n_rows) % n_sv;
@@ -276,10 +405,16 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
   const int lcv2 = WEAK ? (row >> 1) & 3 : row & 3;
   const int kk = WEAK ? row & 1 : 0;
   for (int k = threadIdx.x; k < kN / 2; k += kCoh) tw[k] = tw_inv[k];
-  if (threadIdx.x < 200) dw[threadIdx.x] = dft[threadIdx.x];
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
   const uint32_t* rb = store + (size_t)rec * kStoreRows * kN;
   const bool sat = saturate != 0;
+  // first radix-8 pass: thread t owns group g = t % 256 of the 1-ms rows
+  // f = t / 256 + 4u (u < 3, f < 10); the eight PRN-spectrum samples it
+  // multiplies are the same in every row and pass (re-read from L1/L2 rather
+  // than held: the weak kernel is at the 128-VGPR limit of 1024 threads)
+  const int g0 = threadIdx.x & 255, f0 = threadIdx.x >> 8;
+  const int src0 = brev8(g0) + lcv;   // source column of sample k: (k + lcv) mod 2048
+  __syncthreads();
   uint32_t acc[2][10];
 #pragma unroll
   for (int q = 0; q < 2; q++)
@@ -289,18 +424,26 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
   constexpr int kPasses = WEAK ? 15 : 1;
   for (int i = 0; i < kPasses; i++) {
     const int row0 = WEAK ? lcv2 * 310 + i * 20 + kk * 10 : lcv2 * 20;
+#pragma unroll 1
+    for (int u = 0; u < 3; u++) {
+      int f = f0 + 4 * u;
+      asm volatile("" : "+v"(f));   // per-pass addresses, not hoisted (see dit_pass)
+      if (f < 10) {
+        const uint32_t* rr = rb + (size_t)(row0 + f) * kN;
+        uint32_t v[8];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const int k = threadIdx.x + q * kCoh;
-      const uint32_t cv = cr[k];
-      const int src = (k + lcv) & (kN - 1);
-      const int dst = brev11(k);
-#pragma unroll
-      for (int m = 0; m < 10; m++)
-        coh[m * kN + dst] = cmulsc(rb[(size_t)(row0 + m) * kN + src], cv, WEAK ? 9 : 10, sat);
+        for (int m = 0; m < 8; m++)
+          v[m] = cmulsc(rr[(nat_k(g0, m) - brev8(g0) + src0) & (kN - 1)], cr[nat_k(g0, m)], WEAK ? 9 : 10, sat);
+        dit_first<kR2>(coh + f * kNP, g0, v, tw);
+      }
     }
     __syncthreads();
-    dit_ranks<kCoh, 10>(coh, tw, kR2);
+    dit_pass<kCoh, 10, 3, 3, kR2>(coh, tw);
+    __syncthreads();
+    dit_pass<kCoh, 10, 6, 3, kR2>(coh, tw);
+    __syncthreads();
+    dit_pass<kCoh, 10, 9, 2, kR2>(coh, tw);
+    __syncthreads();
     const int shift = WEAK ? weak_shift(i, lcv, lcv2) : 0;
 #pragma unroll
     for (int q = 0; q < 2; q++) {
@@ -308,14 +451,14 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
       const int c_in = (c_out - shift) & (kN - 1);
       uint32_t d[10];
 #pragma unroll
-      for (int m = 0; m < 10; m++) d[m] = coh[m * kN + c_in];
+      for (int m = 0; m < 10; m++) d[m] = coh[m * kNP + pad(c_in)];
 #pragma unroll 2
       for (int j = 0; j < 10; j++) {
         int32_t ia = 0, qa = 0;
 #pragma unroll
         for (int m = 0; m < 10; m++) {
-          ia = dot2(d[m], dw[(j * 10 + m) * 2], ia);
-          qa = dot2(d[m], dw[(j * 10 + m) * 2 + 1], qa);
+          ia = dot2(d[m], dft[(j * 10 + m) * 2], ia);   // uniform: scalar loads
+          qa = dot2(d[m], dft[(j * 10 + m) * 2 + 1], qa);
         }
         const int32_t ti = (int16_t)(ia >> 16), tq = (int16_t)(qa >> 16);
         const uint32_t p = (uint32_t)(ti * ti) + (uint32_t)(tq * tq);
