@@ -77,19 +77,36 @@ __device__ __forceinline__ uint32_t cmulsc(uint32_t a, uint32_t b, int shift, bo
 }
 
 
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
 // one radix-2 DIT butterfly of rank r with the reference's wrap points
-// (fft.cpp:403-441: optional >>1 pre-scaling, (b*w + 8192) >> 14, int16 sums),
-// on registers: A is the top element x[a], B the bottom x[a + 2^r]
-__device__ __forceinline__ void bfly(uint32_t& A, uint32_t& B, uint32_t w, bool scale) {
-  const int32_t wi = lo16(w), wq = hi16(w);
-  int16_t ai = lo16(A), aq = hi16(A), bi0 = lo16(B), bq0 = hi16(B);
-  if (scale) { ai >>= 1; aq >>= 1; bi0 >>= 1; bq0 >>= 1; }
-  int32_t bi = (int32_t)bi0 * wi - (int32_t)bq0 * wq;
-  int32_t bq = (int32_t)bi0 * wq + (int32_t)bq0 * wi;
-  bi = (bi + 8192) >> 14;
-  bq = (bq + 8192) >> 14;
-  B = pack((int16_t)(ai - (int16_t)bi), (int16_t)(aq - (int16_t)bq));
-  A = pack((int16_t)(ai + (int16_t)bi), (int16_t)(aq + (int16_t)bq));
+// (fft.cpp:403-441: optional >>1 pre-scaling of both inputs, (b*w + 8192) >> 14
+// in int32, int16 sum and difference), on packed {i, q} registers: A is the top
+// element x[a], B the bottom x[a + 2^r].  w = {pack(wi, -wq), pack(wq, wi)}:
+// the complex product's two components are v_dot2_i32_i16 with the rounding
+// constant as the accumulator (exact: |b*w| <= 2^30 since |w| <= 2^14), and the
+// int16 sum / difference are v_pk_add_u16 / v_pk_sub_u16 (wrapping, as the
+// reference's int16 stores).
+__device__ __forceinline__ void bfly(uint32_t& A, uint32_t& B, uint2 w, bool scale) {
+  short2_t a = __builtin_bit_cast(short2_t, A), b = __builtin_bit_cast(short2_t, B);
+  if (scale) { a = a >> (short)1; b = b >> (short)1; }
+  // VOP3P v_dot2 with the rounding constant in an SGPR: the compiler's
+  // v_dot2c form needs a v_mov into the accumulator per product
+  int32_t rnd, bi, bq;
+  asm("s_mov_b32 %0, 0x2000" : "=s"(rnd));
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(bi) : "v"(b), "v"(w.x), "s"(rnd));
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(bq) : "v"(b), "v"(w.y), "s"(rnd));
+  bi >>= 14;
+  bq >>= 14;
+  const short2_t t = __builtin_bit_cast(short2_t, pack((int16_t)bi, (int16_t)bq));
+  B = __builtin_bit_cast(uint32_t, a - t);
+  A = __builtin_bit_cast(uint32_t, a + t);
+}
+
+// LDS twiddle entry for bfly from the packed (c, s) Q14 table
+__device__ __forceinline__ uint2 tw_entry(uint32_t w) {
+  const int16_t wi = lo16(w), wq = hi16(w);
+  return make_uint2(pack(wi, (int16_t)-wq), pack(wq, wi));
 }
 
 // ---------------------------------------------------------------------------
@@ -116,7 +133,7 @@ __device__ __forceinline__ int nat_k(int g, int m) {
 
 // the 2^R - 1 twiddles of one group: tws[2^s - 1 + i] for rank R0 + s, i < 2^s
 template <int R0, int R>
-__device__ __forceinline__ void group_twiddles(uint32_t* tws, int lo, const uint32_t* tw) {
+__device__ __forceinline__ void group_twiddles(uint2* tws, int lo, const uint2* tw) {
 #pragma unroll
   for (int s = 0; s < R; s++)
 #pragma unroll
@@ -126,7 +143,7 @@ __device__ __forceinline__ void group_twiddles(uint32_t* tws, int lo, const uint
 
 // ranks R0 .. R0+R-1 on v[m] = x[b + m*2^R0]
 template <int R0, int R, uint32_t MASK>
-__device__ __forceinline__ void dit_group(uint32_t* v, const uint32_t* tws) {
+__device__ __forceinline__ void dit_group(uint32_t* v, const uint2* tws) {
 #pragma unroll
   for (int s = 0; s < R; s++) {
     const bool scale = (MASK >> (R0 + s)) & 1u;
@@ -145,8 +162,8 @@ __device__ __forceinline__ void st_group8(uint32_t* x, int g, const uint32_t* v)
 // pass R0 = 0 on group g of one transform: in[m] = natural-order samples
 // nat_k(g, m), already wiped off; result to LDS
 template <uint32_t MASK>
-__device__ __forceinline__ void dit_first(uint32_t* x, int g, uint32_t* v, const uint32_t* tw) {
-  uint32_t tws[7];
+__device__ __forceinline__ void dit_first(uint32_t* x, int g, uint32_t* v, const uint2* tw) {
+  uint2 tws[7];
   group_twiddles<0, 3>(tws, 0, tw);
   dit_group<0, 3, MASK>(v, tws);
   st_group8(x, g, v);
@@ -154,7 +171,7 @@ __device__ __forceinline__ void dit_first(uint32_t* x, int g, uint32_t* v, const
 
 // one in-LDS pass over F transforms (stride kNP) with T threads
 template <int T, int F, int R0, int R, uint32_t MASK>
-__device__ __forceinline__ void dit_pass(uint32_t* x, const uint32_t* tw) {
+__device__ __forceinline__ void dit_pass(uint32_t* x, const uint2* tw) {
   constexpr int E = 1 << R, G = kN >> R;
   static_assert(T % G == 0 || G % T == 0, "thread / group mapping");
   if constexpr (T % G == 0) {
@@ -165,7 +182,7 @@ __device__ __forceinline__ void dit_pass(uint32_t* x, const uint32_t* tw) {
     asm volatile("" : "+v"(g));
     const int lo = g & ((1 << R0) - 1);
     const int b = lo | ((g >> R0) << (R0 + R));
-    uint32_t tws[E - 1];
+    uint2 tws[E - 1];
     group_twiddles<R0, R>(tws, lo, tw);
 #pragma unroll 1
     for (int f = threadIdx.x / G; f < F; f += T / G) {
@@ -183,7 +200,7 @@ __device__ __forceinline__ void dit_pass(uint32_t* x, const uint32_t* tw) {
       for (int u = 0; u < G / T; u++) {
         const int g = threadIdx.x + u * T, lo = g & ((1 << R0) - 1);
         const int b = lo | ((g >> R0) << (R0 + R));
-        uint32_t tws[E - 1];
+        uint2 tws[E - 1];
         group_twiddles<R0, R>(tws, lo, tw);
         uint32_t* xf = x + f * kNP;
         uint32_t v[E];
@@ -199,8 +216,8 @@ __device__ __forceinline__ void dit_pass(uint32_t* x, const uint32_t* tw) {
 // the last pass (R0 = 9, radix 4) of a single transform into registers:
 // v[m] = output position g + 512 m
 template <uint32_t MASK>
-__device__ __forceinline__ void dit_last_regs(const uint32_t* x, int g, uint32_t* v, const uint32_t* tw) {
-  uint32_t tws[3];
+__device__ __forceinline__ void dit_last_regs(const uint32_t* x, int g, uint32_t* v, const uint2* tw) {
+  uint2 tws[3];
   group_twiddles<9, 2>(tws, g, tw);
 #pragma unroll
   for (int m = 0; m < 4; m++) v[m] = x[pad(g + 512 * m)];
@@ -211,7 +228,7 @@ __device__ __forceinline__ void dit_last_regs(const uint32_t* x, int g, uint32_t
 // natural-order samples produced by load(k), passes 3 and 6 in LDS; returns
 // after the barrier that precedes the last pass
 template <uint32_t MASK, class Load>
-__device__ __forceinline__ void dit_row_256(uint32_t* x, const uint32_t* tw, Load load) {
+__device__ __forceinline__ void dit_row_256(uint32_t* x, const uint2* tw, Load load) {
   static_assert(kThreads == 256, "one radix-8 group per thread");
   const int g = threadIdx.x;
   uint32_t v[8];
@@ -229,11 +246,11 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_kernel(
     const uint32_t* __restrict__ buff, const uint32_t* __restrict__ wipe,
     const uint32_t* __restrict__ tw_fwd, uint32_t* __restrict__ X, int saturate) {
   __shared__ uint32_t x[kNP];
-  __shared__ uint32_t tw[kN / 2];
+  __shared__ uint2 tw[kN / 2];
   const int rec = blockIdx.x >> 2, j = blockIdx.x & 3;
   const uint32_t* src = buff + (size_t)rec * kN;
   const uint32_t* wp = wipe + (size_t)j * kN;
-  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_fwd[k];
+  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_entry(tw_fwd[k]);
   __syncthreads();
   const bool sat = saturate != 0;
   dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });   // R1: no scaling
@@ -254,7 +271,7 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
     const uint32_t* __restrict__ tw_inv, const int32_t* __restrict__ svs, int n_sv, int lmin,
     int n_rows, int saturate, int2* __restrict__ row_out) {
   __shared__ uint32_t x[kNP];
-  __shared__ uint32_t tw[kN / 2];
+  __shared__ uint2 tw[kN / 2];
   __shared__ int2 red[kThreads / 64];
   const int row = blockIdx.x % n_rows;
   const int s = (blockIdx.x / n_rows) % n_sv;
@@ -262,7 +279,7 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
   const int lcv = lmin + (row >> 2), lcv2 = row & 3;
   const uint32_t* xr = X + ((size_t)rec * 4 + lcv2) * kN;
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
-  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_inv[k];
+  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_entry(tw_inv[k]);
   __syncthreads();
   const bool sat = saturate != 0;
   dit_row_256<kR2>(x, tw, [&](int k) { return cmulsc(xr[(k + lcv) & (kN - 1)], cr[k], 10, sat); });
@@ -330,7 +347,6 @@ constexpr int kStoreRows = 1240;      // baseband_rows (acquisition.cpp:107-110)
 constexpr int kWipe = 10 * kN;        // 10-ms wipe-off tables, repeated (:123-137)
 constexpr int kCoh = 1024;            // threads of the coherent kernels
 
-typedef short short2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int32_t dot2(uint32_t a, uint32_t b, int32_t c) {
   // a.i*b.lo + a.q*b.hi + c in int32 (wrap): one pmaddwd half of sse_cacc
   return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a), __builtin_bit_cast(short2_t, b),
@@ -345,12 +361,12 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_rows_kernel(
     const uint32_t* __restrict__ buff, int ms, const uint32_t* __restrict__ wipe10,
     const uint32_t* __restrict__ tw_fwd, uint32_t* __restrict__ store, int saturate) {
   __shared__ uint32_t x[kNP];
-  __shared__ uint32_t tw[kN / 2];
+  __shared__ uint2 tw[kN / 2];
   const int nr = 4 * ms;
   const int rec = blockIdx.x / nr, r = blockIdx.x % nr, j = r / ms, m = r % ms;
   const uint32_t* src = buff + ((size_t)rec * ms + m) * kN;
   const uint32_t* wp = wipe10 + (size_t)j * kWipe + (size_t)(m % 10) * kN;
-  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_fwd[k];
+  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_entry(tw_fwd[k]);
   __syncthreads();
   const bool sat = saturate != 0;
   dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });
@@ -396,7 +412,7 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
     const int32_t* __restrict__ svs, int n_sv, int lmin, int n_rows, int saturate,
     int2* __restrict__ row_out) {
   __shared__ uint32_t coh[10 * kNP];
-  __shared__ uint32_t tw[kN / 2];
+  __shared__ uint2 tw[kN / 2];
   __shared__ int2 red[kCoh / 64];
   const int row = blockIdx.x % n_rows;
   const int s = (blockIdx.x / n_rows) % n_sv;
@@ -404,7 +420,7 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
   const int lcv = lmin + (WEAK ? row >> 3 : row >> 2);
   const int lcv2 = WEAK ? (row >> 1) & 3 : row & 3;
   const int kk = WEAK ? row & 1 : 0;
-  for (int k = threadIdx.x; k < kN / 2; k += kCoh) tw[k] = tw_inv[k];
+  for (int k = threadIdx.x; k < kN / 2; k += kCoh) tw[k] = tw_entry(tw_inv[k]);
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
   const uint32_t* rb = store + (size_t)rec * kStoreRows * kN;
   const bool sat = saturate != 0;
