@@ -44,24 +44,52 @@ constexpr int kBlkIn = GNSSCORR_GN3S_BLOCK_IN;     // 20000 samples per 5 ms
 constexpr int kBlkOut = GNSSCORR_GN3S_BLOCK_OUT;   // 10240 = 5 x 2048
 constexpr int kThreads = 256;
 
-// out[b][i] (int16 I, Q packed in one uint32, I in the low half like CPX)
+// out[b][i] (int16 I, Q packed in one uint32, I in the low half like CPX).
+// A thread writes four consecutive outputs of one block as one 16-byte store.
+// The product lookups are random in the 1024-entry phase, so the table sits in
+// LDS (an L1 gather touches one cache line per lane).  Only codes 2, 3 (LUT
+// +1, +3) are staged: (int16)(-x) == -(int16)(x) for the truncating cast, so
+// codes 1, 0 are their packed negations (exact).  grid = (kBlkOut / 4 /
+// kThreads) x min(n_blocks, kGridY); each workgroup loops over blocks b =
+// blockIdx.y + k * gridDim.y, amortising the 8 KiB staging.
+constexpr int kQuads = kBlkOut / 4;   // 2560 16-byte stores per block
+constexpr int kGridY = 192;           // 10 x 192 workgroups: ~8 per CU
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t gn3s_sample(const uint8_t* __restrict__ in, int fmt, uint32_t s0,
+                                                int i, uint32_t phase0, uint32_t step,
+                                                const uint32_t* tab) {
+  const int n = ((i + 1) * 125) >> 6;   // floor((i+1)*4000/2048)
+  if (n >= kBlkIn) return 0u;           // output 10239 reads the zero past the block
+  const uint32_t s = s0 + (uint32_t)n;  // < 2^31 (checked on the host)
+  const uint32_t code = fmt == 0 ? (in[s] & 3u) : ((in[s >> 2] >> (2 * (s & 3))) & 3u);
+  const uint32_t ph = phase0 + s * step;
+  const uint32_t v = tab[((code >= 2 ? code : 3u - code) - 2u) * 1024 + (ph >> 22)];
+  if (code >= 2) return v;
+  const short2_t neg = -__builtin_bit_cast(short2_t, v);
+  return __builtin_bit_cast(uint32_t, neg);
+}
+
 __global__ __launch_bounds__(kThreads) void gn3s_kernel(const uint8_t* __restrict__ in, int fmt,
                                                         int n_blocks, uint32_t phase0,
                                                         uint32_t step,
                                                         const uint32_t* __restrict__ prod,
                                                         uint32_t* __restrict__ out) {
-  const long o = (long)blockIdx.x * kThreads + threadIdx.x;
-  if (o >= (long)n_blocks * kBlkOut) return;
-  const int b = (int)(o / kBlkOut), i = (int)(o % kBlkOut);
-  const int n = ((i + 1) * 125) >> 6;   // floor((i+1)*4000/2048)
-  uint32_t v = 0;
-  if (n < kBlkIn) {
-    const long s = (long)b * kBlkIn + n;
-    const uint32_t code = fmt == 0 ? (in[s] & 3u) : ((in[s >> 2] >> (2 * (s & 3))) & 3u);
-    const uint32_t ph = phase0 + (uint32_t)s * step;   // (uint32)s: s < 2^31 checked on the host
-    v = prod[code * 1024 + (ph >> 22)];
+  __shared__ uint32_t tab[2 * 1024];
+  for (int k = threadIdx.x; k < 2 * 1024; k += kThreads) tab[k] = prod[2 * 1024 + k];
+  __syncthreads();
+  const int q = blockIdx.x * kThreads + threadIdx.x;   // < kQuads: the grid is exact
+  for (int b = blockIdx.y; b < n_blocks; b += gridDim.y) {
+    const int i = 4 * q;
+    const uint32_t s0 = (uint32_t)b * kBlkIn;
+    uint4 v;
+    v.x = gn3s_sample(in, fmt, s0, i, phase0, step, tab);
+    v.y = gn3s_sample(in, fmt, s0, i + 1, phase0, step, tab);
+    v.z = gn3s_sample(in, fmt, s0, i + 2, phase0, step, tab);
+    v.w = gn3s_sample(in, fmt, s0, i + 3, phase0, step, tab);
+    *reinterpret_cast<uint4*>(out + (size_t)b * kBlkOut + i) = v;
   }
-  out[o] = v;
 }
 
 __global__ __launch_bounds__(kThreads) void downsample_kernel(const uint32_t* __restrict__ src,
@@ -140,9 +168,14 @@ extern "C" int gnsscorr_sdr_gn3s_dev(gnsscorr_sdr_fe_ctx* c, const uint8_t* d_in
     gnsscorr_set_error("gnsscorr_sdr_gn3s: bad arguments (fmt %d, blocks %d)", fmt, n_blocks);
     return GNSSCORR_EINVAL;
   }
+  if ((uintptr_t)d_out & 15u) {
+    gnsscorr_set_error("gnsscorr_sdr_gn3s_dev: d_out must be 16-byte aligned");
+    return GNSSCORR_EINVAL;
+  }
   HIP_TRY(hipSetDevice(c->device));
-  const long n_out = (long)n_blocks * kBlkOut;
-  hipLaunchKernelGGL(gn3s_kernel, dim3((unsigned)((n_out + kThreads - 1) / kThreads)),
+  static_assert(kQuads % kThreads == 0, "exact grid of 16-byte output stores");
+  hipLaunchKernelGGL(gn3s_kernel, dim3(kQuads / kThreads,
+                                       (unsigned)(n_blocks < kGridY ? n_blocks : kGridY)),
                      dim3(kThreads), 0, c->stream, d_in, fmt, n_blocks, *phase, step, c->d_prod,
                      (uint32_t*)d_out);
   HIP_TRY(hipGetLastError());

@@ -595,7 +595,8 @@ int gnsscorr_sdr_fe_destroy(gnsscorr_sdr_fe_ctx *ctx);
  * the reference's gbuff); fmt 1: packed, 4 samples per byte, sample j of a byte
  * in bits 2j..2j+1.  *phase: the NCO phase before the first sample (0 after
  * construction in the reference), advanced by n_blocks * 20000 * step.
- * d_out: n_blocks * 10240 CPX (int16 I, Q).  Asynchronous on the context stream. */
+ * d_out: n_blocks * 10240 CPX (int16 I, Q), 16-byte aligned (GNSSCORR_EINVAL
+ * otherwise).  Asynchronous on the context stream. */
 int gnsscorr_sdr_gn3s_dev(gnsscorr_sdr_fe_ctx *ctx, const uint8_t *d_in, int fmt, int n_blocks,
                           uint32_t *phase, uint32_t step, int16_t *d_out);
 int gnsscorr_sdr_gn3s(gnsscorr_sdr_fe_ctx *ctx, const uint8_t *h_in, int fmt, int n_blocks,
