@@ -68,18 +68,40 @@ __global__ __launch_bounds__(kThreads) void sdr_accum_kernel(
 #pragma unroll
   for (int k = 0; k < 3; k++) cb[k] = ((size_t)j.sv * kCBins + j.cbin[k]) * kRow + j.coff[k];
   uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-  for (int n = threadIdx.x; n < j.samps; n += kThreads) {
-    const uint32_t a = d[n], b = sn[n];
+  // Wave w covers the contiguous samples [1024 w, 1024 w + 1024) of the job,
+  // 64 per step.  The code bits it needs per arm lie in the 33 words from
+  // (cb + 1024 w) >> 5: lane l holds word l of that range (one coalesced load
+  // per arm for the whole job), and each sample's bit comes from its word's
+  // lane by ds_bpermute.
+  static_assert(kThreads == 128 && kN == 2048, "two waves of 1024 samples");
+  const int lane = threadIdx.x & 63, wave0 = (threadIdx.x >> 6) * 1024;
+  const int nend = min(j.samps, wave0 + 1024);
+  uint32_t cw[3];
+  uint32_t sh[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const size_t bit0 = cb[k] + (size_t)wave0;
+    sh[k] = (uint32_t)bit0 & 31u;
+    // words 0..32 cover bits up to sh + 1023; an idle wave loads nothing
+    cw[k] = (lane <= 32 && wave0 < nend) ? codebits[(bit0 >> 5) + lane] : 0u;
+  }
+  for (int n0 = wave0; n0 < nend; n0 += 64) {
+    const int n = n0 + lane;
+    const bool live = n < nend;
+    const uint32_t a = live ? d[n] : 0u, b = live ? sn[n] : 0u;
     const int32_t ai = lo16(a), aq = hi16(a), bi = lo16(b), bq = hi16(b);
     const int32_t ti = (ai * bi - aq * bq + 8192) >> 14, tq = (ai * bq + aq * bi + 8192) >> 14;
-    const int32_t wi = saturate ? sat16(ti) : (int32_t)(int16_t)ti;
-    const int32_t wq = saturate ? sat16(tq) : (int32_t)(int16_t)tq;
+    int32_t wi = saturate ? sat16(ti) : (int32_t)(int16_t)ti;
+    int32_t wq = saturate ? sat16(tq) : (int32_t)(int16_t)tq;
+    if (!live) wi = wq = 0;
+    const uint32_t rel = (uint32_t)(n - wave0);   // < 1024
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      const size_t bit = cb[k] + n;
-      const bool one = (codebits[bit >> 5] >> (bit & 31)) & 1u;
-      acc[2 * k] += (uint32_t)(one ? wi : -wi);       // A.i * code  (+-1)
-      acc[2 * k + 1] += (uint32_t)(one ? wq : -wq);   // A.q * code
+      const uint32_t r = rel + sh[k];
+      const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r >> 5) << 2), (int)cw[k]);
+      const int32_t m = (int32_t)((word >> (r & 31u)) & 1u) - 1;   // 0: +code, -1: -code
+      acc[2 * k] += (uint32_t)((wi ^ m) - m);       // A.i * code  (+-1)
+      acc[2 * k + 1] += (uint32_t)((wq ^ m) - m);   // A.q * code
     }
   }
 #pragma unroll
@@ -232,7 +254,8 @@ extern "C" int gnsscorr_sdr_corr_create(gnsscorr_sdr_corr_ctx** out,
   auto* c = new gnsscorr_sdr_corr_ctx();
   c->cfg = *cfg;
   const size_t ncar = (size_t)kSBins * kRow;
-  const size_t nbits = (size_t)kSV * kCBins * kRow, nwords = nbits / 32;
+  // + 4 words: the kernel's word window may end one word past a row's last bit
+  const size_t nbits = (size_t)kSV * kCBins * kRow, nwords = nbits / 32 + 4;
   std::vector<uint32_t> car(ncar), bits(nwords, 0u);
   // carrier rows: sine_gen(row, -IF_FREQUENCY - (float)k*CARRIER_SPACING, fs, 4096)
   for (int k = -kCarrBins; k <= kCarrBins; k++) {
