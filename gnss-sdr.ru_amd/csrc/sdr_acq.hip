@@ -131,14 +131,49 @@ __device__ __forceinline__ int nat_k(int g, int m) {
   return brev8(g) + 256 * kBrev3[m];
 }
 
+// LDS twiddles: the 1024 entries of the reference table (tw_entry form), then
+// per-pass copies for the R0 = 3 and R0 = 6 passes laid out [e][lo] (e = the
+// group's twiddle slot, lo = b mod 2^R0).  Read from the main table, those two
+// passes' lanes would hit one bank at power-of-two strides (8- to 16-way
+// conflicts); from the [e][lo] copies consecutive lanes read consecutive
+// entries.  The R0 = 0 pass reads broadcast entries, R0 = 9 stride 1 or 2.
+constexpr int kTw3 = kN / 2;              // 7 x 8 entries
+constexpr int kTw6 = kTw3 + 7 * 8;        // 7 x 64 entries
+constexpr int kTwLds = kTw6 + 7 * 64;     // 1528 entries, 12 KiB
+
 // the 2^R - 1 twiddles of one group: tws[2^s - 1 + i] for rank R0 + s, i < 2^s
-template <int R0, int R>
+template <int R0, int R, bool PT = false>
 __device__ __forceinline__ void group_twiddles(uint2* tws, int lo, const uint2* tw) {
+  if constexpr (PT && (R0 == 3 || R0 == 6)) {
+    static_assert(R == 3, "per-pass tables are radix 8");
+    const uint2* t = tw + (R0 == 3 ? kTw3 : kTw6);
 #pragma unroll
-  for (int s = 0; s < R; s++)
+    for (int e = 0; e < 7; e++) tws[e] = t[e * (1 << R0) + lo];
+  } else {
 #pragma unroll
-    for (int i = 0; i < (1 << s); i++)
-      tws[(1 << s) - 1 + i] = tw[(lo + (i << R0)) << (kM - 1 - R0 - s)];
+    for (int s = 0; s < R; s++)
+#pragma unroll
+      for (int i = 0; i < (1 << s); i++)
+        tws[(1 << s) - 1 + i] = tw[(lo + (i << R0)) << (kM - 1 - R0 - s)];
+  }
+}
+
+// fill the LDS twiddles from the packed (c, s) Q14 table; T threads, caller
+// syncs.  PT: also the per-pass copies.  They pay off only when a workgroup
+// runs many transforms (sdr_coh_kernel: 10 per pass, 15 passes); for one
+// transform per workgroup the extra staging costs more than the conflicts.
+template <int T, bool PT>
+__device__ __forceinline__ void stage_twiddles(uint2* tw, const uint32_t* __restrict__ glob) {
+  for (int k = threadIdx.x; k < (PT ? kTwLds : kTw3); k += T) {
+    int j = k;
+    if (k >= kTw3) {
+      const int r0 = k >= kTw6 ? 6 : 3, rel = k - (k >= kTw6 ? kTw6 : kTw3);
+      const int e = rel >> r0, lo = rel & ((1 << r0) - 1);
+      const int sl = e >= 3 ? 2 : (e >= 1 ? 1 : 0), i = e - ((1 << sl) - 1);
+      j = (lo + (i << r0)) << (kM - 1 - r0 - sl);
+    }
+    tw[k] = tw_entry(glob[j]);
+  }
 }
 
 // ranks R0 .. R0+R-1 on v[m] = x[b + m*2^R0]
@@ -170,7 +205,7 @@ __device__ __forceinline__ void dit_first(uint32_t* x, int g, uint32_t* v, const
 }
 
 // one in-LDS pass over F transforms (stride kNP) with T threads
-template <int T, int F, int R0, int R, uint32_t MASK>
+template <int T, int F, int R0, int R, uint32_t MASK, bool PT = false>
 __device__ __forceinline__ void dit_pass(uint32_t* x, const uint2* tw) {
   constexpr int E = 1 << R, G = kN >> R;
   static_assert(T % G == 0 || G % T == 0, "thread / group mapping");
@@ -183,7 +218,7 @@ __device__ __forceinline__ void dit_pass(uint32_t* x, const uint2* tw) {
     const int lo = g & ((1 << R0) - 1);
     const int b = lo | ((g >> R0) << (R0 + R));
     uint2 tws[E - 1];
-    group_twiddles<R0, R>(tws, lo, tw);
+    group_twiddles<R0, R, PT>(tws, lo, tw);
 #pragma unroll 1
     for (int f = threadIdx.x / G; f < F; f += T / G) {
       uint32_t* xf = x + f * kNP;
@@ -201,7 +236,7 @@ __device__ __forceinline__ void dit_pass(uint32_t* x, const uint2* tw) {
         const int g = threadIdx.x + u * T, lo = g & ((1 << R0) - 1);
         const int b = lo | ((g >> R0) << (R0 + R));
         uint2 tws[E - 1];
-        group_twiddles<R0, R>(tws, lo, tw);
+        group_twiddles<R0, R, PT>(tws, lo, tw);
         uint32_t* xf = x + f * kNP;
         uint32_t v[E];
 #pragma unroll
@@ -246,11 +281,11 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_kernel(
     const uint32_t* __restrict__ buff, const uint32_t* __restrict__ wipe,
     const uint32_t* __restrict__ tw_fwd, uint32_t* __restrict__ X, int saturate) {
   __shared__ uint32_t x[kNP];
-  __shared__ uint2 tw[kN / 2];
+  __shared__ uint2 tw[kTwLds];
   const int rec = blockIdx.x >> 2, j = blockIdx.x & 3;
   const uint32_t* src = buff + (size_t)rec * kN;
   const uint32_t* wp = wipe + (size_t)j * kN;
-  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_entry(tw_fwd[k]);
+  stage_twiddles<kThreads, false>(tw, tw_fwd);
   __syncthreads();
   const bool sat = saturate != 0;
   dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });   // R1: no scaling
@@ -271,7 +306,7 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
     const uint32_t* __restrict__ tw_inv, const int32_t* __restrict__ svs, int n_sv, int lmin,
     int n_rows, int saturate, int2* __restrict__ row_out) {
   __shared__ uint32_t x[kNP];
-  __shared__ uint2 tw[kN / 2];
+  __shared__ uint2 tw[kTwLds];
   __shared__ int2 red[kThreads / 64];
   const int row = blockIdx.x % n_rows;
   const int s = (blockIdx.x / n_rows) % n_sv;
@@ -279,7 +314,7 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
   const int lcv = lmin + (row >> 2), lcv2 = row & 3;
   const uint32_t* xr = X + ((size_t)rec * 4 + lcv2) * kN;
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
-  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_entry(tw_inv[k]);
+  stage_twiddles<kThreads, false>(tw, tw_inv);
   __syncthreads();
   const bool sat = saturate != 0;
   dit_row_256<kR2>(x, tw, [&](int k) { return cmulsc(xr[(k + lcv) & (kN - 1)], cr[k], 10, sat); });
@@ -361,12 +396,12 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_rows_kernel(
     const uint32_t* __restrict__ buff, int ms, const uint32_t* __restrict__ wipe10,
     const uint32_t* __restrict__ tw_fwd, uint32_t* __restrict__ store, int saturate) {
   __shared__ uint32_t x[kNP];
-  __shared__ uint2 tw[kN / 2];
+  __shared__ uint2 tw[kTwLds];
   const int nr = 4 * ms;
   const int rec = blockIdx.x / nr, r = blockIdx.x % nr, j = r / ms, m = r % ms;
   const uint32_t* src = buff + ((size_t)rec * ms + m) * kN;
   const uint32_t* wp = wipe10 + (size_t)j * kWipe + (size_t)(m % 10) * kN;
-  for (int k = threadIdx.x; k < kN / 2; k += kThreads) tw[k] = tw_entry(tw_fwd[k]);
+  stage_twiddles<kThreads, false>(tw, tw_fwd);
   __syncthreads();
   const bool sat = saturate != 0;
   dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });
@@ -412,7 +447,7 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
     const int32_t* __restrict__ svs, int n_sv, int lmin, int n_rows, int saturate,
     int2* __restrict__ row_out) {
   __shared__ uint32_t coh[10 * kNP];
-  __shared__ uint2 tw[kN / 2];
+  __shared__ uint2 tw[kTwLds];
   __shared__ int2 red[kCoh / 64];
   const int row = blockIdx.x % n_rows;
   const int s = (blockIdx.x / n_rows) % n_sv;
@@ -420,7 +455,7 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
   const int lcv = lmin + (WEAK ? row >> 3 : row >> 2);
   const int lcv2 = WEAK ? (row >> 1) & 3 : row & 3;
   const int kk = WEAK ? row & 1 : 0;
-  for (int k = threadIdx.x; k < kN / 2; k += kCoh) tw[k] = tw_entry(tw_inv[k]);
+  stage_twiddles<kCoh, true>(tw, tw_inv);
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
   const uint32_t* rb = store + (size_t)rec * kStoreRows * kN;
   const bool sat = saturate != 0;
@@ -454,9 +489,9 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
       }
     }
     __syncthreads();
-    dit_pass<kCoh, 10, 3, 3, kR2>(coh, tw);
+    dit_pass<kCoh, 10, 3, 3, kR2, true>(coh, tw);
     __syncthreads();
-    dit_pass<kCoh, 10, 6, 3, kR2>(coh, tw);
+    dit_pass<kCoh, 10, 6, 3, kR2, true>(coh, tw);
     __syncthreads();
     dit_pass<kCoh, 10, 9, 2, kR2>(coh, tw);
     __syncthreads();
