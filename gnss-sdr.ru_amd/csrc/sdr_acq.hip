@@ -12,7 +12,7 @@
 //                      wipe-off (cmulsc, shift 14) written straight into
 //                      bit-reversed LDS positions, 11 unscaled DIT ranks,
 //                      spectrum row X[rec][j][2048] to HBM (natural order).
-//   sdr_strong_kernel  one workgroup per (record, sv, row) with row =
+//   sdr_strong_kernel  one workgroup per (record, sv, lcv), rows lcv2 = 0..3 in turn; row =
 //                      (lcv - lmin)*4 + lcv2: reads X[rec][lcv2] circularly
 //                      from offset lcv (the reference's baseband_rows[...]
 //                      [100+lcv] rotation), cmulsc by the PRN spectrum (shift
@@ -262,18 +262,19 @@ __device__ __forceinline__ void dit_last_regs(const uint32_t* x, int g, uint32_t
 // whole transform of one row, T = 256 threads: first pass from the wiped-off
 // natural-order samples produced by load(k), passes 3 and 6 in LDS; returns
 // after the barrier that precedes the last pass
-template <uint32_t MASK, class Load>
+// load(k, m): the wiped-off natural-order sample k, the thread's m-th
+template <uint32_t MASK, bool PT, class Load>
 __device__ __forceinline__ void dit_row_256(uint32_t* x, const uint2* tw, Load load) {
   static_assert(kThreads == 256, "one radix-8 group per thread");
   const int g = threadIdx.x;
   uint32_t v[8];
 #pragma unroll
-  for (int m = 0; m < 8; m++) v[m] = load(nat_k(g, m));
+  for (int m = 0; m < 8; m++) v[m] = load(nat_k(g, m), m);
   dit_first<MASK>(x, g, v, tw);
   __syncthreads();
-  dit_pass<kThreads, 1, 3, 3, MASK>(x, tw);
+  dit_pass<kThreads, 1, 3, 3, MASK, PT>(x, tw);
   __syncthreads();
-  dit_pass<kThreads, 1, 6, 3, MASK>(x, tw);
+  dit_pass<kThreads, 1, 6, 3, MASK, PT>(x, tw);
   __syncthreads();
 }
 
@@ -288,7 +289,7 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_kernel(
   stage_twiddles<kThreads, false>(tw, tw_fwd);
   __syncthreads();
   const bool sat = saturate != 0;
-  dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });   // R1: no scaling
+  dit_row_256<0u, false>(x, tw, [&](int k, int) { return cmulsc(src[k], wp[k], 14, sat); });   // R1: no scaling
   uint32_t* dst = X + ((size_t)rec * 4 + j) * kN;
 #pragma unroll
   for (int u = 0; u < 2; u++) {
@@ -301,6 +302,11 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_kernel(
 }
 
 // per-row result: (magnitude, index) of x86_cmag + x86_max
+// One workgroup per (record, sv, lcv): the four 250-Hz sub-bins lcv2 of the
+// 1-kHz shift run back to back, sharing the staged twiddles (with the per-pass
+// copies) and the thread's eight PRN-spectrum samples.  Per-row result:
+// (magnitude, index) of x86_cmag + x86_max at row_out[(rec, sv, row)], row =
+// (lcv - lmin)*4 + lcv2.
 __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
     const uint32_t* __restrict__ X, const uint32_t* __restrict__ codes,
     const uint32_t* __restrict__ tw_inv, const int32_t* __restrict__ svs, int n_sv, int lmin,
@@ -308,47 +314,55 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
   __shared__ uint32_t x[kNP];
   __shared__ uint2 tw[kTwLds];
   __shared__ int2 red[kThreads / 64];
-  const int row = blockIdx.x % n_rows;
-  const int s = (blockIdx.x / n_rows) % n_sv;
-  const int rec = blockIdx.x / (n_rows * n_sv);
-  const int lcv = lmin + (row >> 2), lcv2 = row & 3;
-  const uint32_t* xr = X + ((size_t)rec * 4 + lcv2) * kN;
+  const int n_lcv = n_rows >> 2;
+  const int l = blockIdx.x % n_lcv;
+  const int s = (blockIdx.x / n_lcv) % n_sv;
+  const int rec = blockIdx.x / (n_lcv * n_sv);
+  const int lcv = lmin + l;
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
-  stage_twiddles<kThreads, false>(tw, tw_inv);
-  __syncthreads();
+  uint32_t cv[8];
+#pragma unroll
+  for (int m = 0; m < 8; m++) cv[m] = cr[nat_k(threadIdx.x, m)];
+  stage_twiddles<kThreads, true>(tw, tw_inv);
   const bool sat = saturate != 0;
-  dit_row_256<kR2>(x, tw, [&](int k) { return cmulsc(xr[(k + lcv) & (kN - 1)], cr[k], 10, sat); });
-  // last pass in registers, then x86_cmag (int32 wrap) + x86_max (first index
-  // of the strict maximum, > 0): ties go to the smaller index
-  int32_t best = 0, idx = 0;
+  for (int lcv2 = 0; lcv2 < 4; lcv2++) {
+    __syncthreads();   // twiddles staged / the previous row's last pass has read x
+    const uint32_t* xr = X + ((size_t)rec * 4 + lcv2) * kN;
+    dit_row_256<kR2, true>(x, tw, [&](int k, int m) {
+      return cmulsc(xr[(k + lcv) & (kN - 1)], cv[m], 10, sat);
+    });
+    // last pass in registers, then x86_cmag (int32 wrap) + x86_max (first
+    // index of the strict maximum, > 0): ties go to the smaller index
+    int32_t best = 0, idx = 0;
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
-    const int g = threadIdx.x + u * kThreads;
-    uint32_t v[4];
-    dit_last_regs<kR2>(x, g, v, tw);
+    for (int u = 0; u < 2; u++) {
+      const int g = threadIdx.x + u * kThreads;
+      uint32_t v[4];
+      dit_last_regs<kR2>(x, g, v, tw);
 #pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const int32_t i = lo16(v[m]), q = hi16(v[m]);
-      const int32_t p = (int32_t)((uint32_t)(i * i) + (uint32_t)(q * q));
-      if (p > best || (p == best && g + 512 * m < idx)) { best = p; idx = g + 512 * m; }
+      for (int q = 0; q < 4; q++) {
+        const int32_t i = lo16(v[q]), qq = hi16(v[q]);
+        const int32_t p = (int32_t)((uint32_t)(i * i) + (uint32_t)(qq * qq));
+        if (p > best || (p == best && g + 512 * q < idx)) { best = p; idx = g + 512 * q; }
+      }
     }
-  }
-  // reduce: larger magnitude wins, equal magnitude -> smaller index
+    // reduce: larger magnitude wins, equal magnitude -> smaller index
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const int32_t ob = __shfl_xor(best, o, 64), oi = __shfl_xor(idx, o, 64);
-    if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; }
-  }
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = make_int2(best, idx);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int2 r = red[0];
-    for (int w = 1; w < kThreads / 64; w++) {
-      const int2 o = red[w];
-      if (o.x > r.x || (o.x == r.x && o.y < r.y)) r = o;
+    for (int o = 32; o >= 1; o >>= 1) {
+      const int32_t ob = __shfl_xor(best, o, 64), oi = __shfl_xor(idx, o, 64);
+      if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; }
     }
-    if (r.x <= 0) r = make_int2(0, 0);
-    row_out[blockIdx.x] = r;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = make_int2(best, idx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int2 r = red[0];
+      for (int w = 1; w < kThreads / 64; w++) {
+        const int2 o = red[w];
+        if (o.x > r.x || (o.x == r.x && o.y < r.y)) r = o;
+      }
+      if (r.x <= 0) r = make_int2(0, 0);
+      row_out[((size_t)rec * n_sv + s) * n_rows + l * 4 + lcv2] = r;
+    }
   }
 }
 
@@ -404,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void sdr_prep_rows_kernel(
   stage_twiddles<kThreads, false>(tw, tw_fwd);
   __syncthreads();
   const bool sat = saturate != 0;
-  dit_row_256<0u>(x, tw, [&](int k) { return cmulsc(src[k], wp[k], 14, sat); });
+  dit_row_256<0u, false>(x, tw, [&](int k, int) { return cmulsc(src[k], wp[k], 14, sat); });
   uint32_t* dst = store + ((size_t)rec * kStoreRows + r) * kN;
 #pragma unroll
   for (int u = 0; u < 2; u++) {
@@ -706,7 +720,7 @@ extern "C" int gnsscorr_sdr_acq_strong_dev(gnsscorr_sdr_acq_ctx* c, const int16_
     return rc;
   hipLaunchKernelGGL(sdr_prep_kernel, dim3(4 * n_rec), dim3(kThreads), 0, c->stream,
                      (const uint32_t*)d_buff, c->d_wipe, c->d_twf, c->d_X, c->cfg.saturate);
-  hipLaunchKernelGGL(sdr_strong_kernel, dim3(n_rec * n_sv * n_rows), dim3(kThreads), 0, c->stream,
+  hipLaunchKernelGGL(sdr_strong_kernel, dim3(n_rec * n_sv * (n_rows / 4)), dim3(kThreads), 0, c->stream,
                      c->d_X, c->d_codes, c->d_twi, d_svs, n_sv, lmin, n_rows, c->cfg.saturate,
                      c->d_rows);
   const int G = n_rec * n_sv;
