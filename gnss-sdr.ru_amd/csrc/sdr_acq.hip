@@ -366,24 +366,41 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
   }
 }
 
-__global__ void sdr_select_kernel(const int2* __restrict__ row_out, const int32_t* __restrict__ svs,
-                                  int n_sv, int n_rec, int lmin, int n_rows,
-                                  gnsscorr_sdr_acq_result* __restrict__ res) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+// The reference scans the rows in order with a strict '>' from 0, so it keeps
+// the first row holding the maximum (if the maximum is > 0).  One wave per
+// (record, sv): lane l scans rows l, l + 64, ... the same way, then the wave
+// keeps the larger magnitude, and on equal magnitude the smaller row.
+// Returns (magnitude, row) in every lane; magnitude 0 = no row beats 0.
+__device__ __forceinline__ int2 first_max_row(const int2* __restrict__ rr, int n_rows, int lane) {
+  int32_t mag = 0, row = 0x7fffffff;
+  for (int r = lane; r < n_rows; r += 64) {
+    const int32_t v = rr[r].x;
+    if (v > mag) { mag = v; row = r; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int32_t om = __shfl_xor(mag, o, 64), orow = __shfl_xor(row, o, 64);
+    if (om > mag || (om == mag && orow < row)) { mag = om; row = orow; }
+  }
+  return make_int2(mag, row);
+}
+
+__global__ __launch_bounds__(64) void sdr_select_kernel(
+    const int2* __restrict__ row_out, const int32_t* __restrict__ svs, int n_sv, int n_rec,
+    int lmin, int n_rows, gnsscorr_sdr_acq_result* __restrict__ res) {
+  const int g = blockIdx.x;   // (record, sv); doAcqStrong: lcv outer, lcv2 inner, strict >
   if (g >= n_rec * n_sv) return;
   const int2* rr = row_out + (size_t)g * n_rows;
+  const int2 best = first_max_row(rr, n_rows, threadIdx.x);
+  if (threadIdx.x != 0) return;
   gnsscorr_sdr_acq_result r = {};
   r.sv = svs[g % n_sv];
-  int32_t mag = 0;
-  for (int row = 0; row < n_rows; row++) {   // doAcqStrong: lcv outer, lcv2 inner, strict >
-    const int2 v = rr[row];
-    if (v.x > mag) {
-      mag = v.x;
-      r.code_phase = kN - v.y;
-      r.doppler = (lmin + (row >> 2)) * 1000 + (row & 3) * 250;
-      r.magnitude = (uint32_t)v.x;
-      r.row = row;
-    }
+  if (best.x > 0) {
+    const int row = best.y;
+    r.code_phase = kN - rr[row].y;
+    r.doppler = (lmin + (row >> 2)) * 1000 + (row & 3) * 250;
+    r.magnitude = (uint32_t)best.x;
+    r.row = row;
   }
   r.success = r.magnitude > 0u;   // THRESH_STRONG = 0 (config.h:72)
   res[g] = r;
@@ -560,26 +577,23 @@ __global__ __launch_bounds__(kCoh) void sdr_coh_kernel(
 // per (record, sv): strict-greater scan over the rows in the reference's loop
 // order (lcv, lcv2[, k]); code_phase = index % 2048 and doppler = lcv*1000 +
 // lcv2*250 + (index / 2048)*25 (acquisition.cpp:397-405, :543-551)
-__global__ void sdr_select_mw_kernel(const int2* __restrict__ row_out,
-                                     const int32_t* __restrict__ svs, int n_sv, int n_rec,
-                                     int lmin, int n_rows, int weak,
-                                     gnsscorr_sdr_acq_result* __restrict__ res) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64) void sdr_select_mw_kernel(
+    const int2* __restrict__ row_out, const int32_t* __restrict__ svs, int n_sv, int n_rec,
+    int lmin, int n_rows, int weak, gnsscorr_sdr_acq_result* __restrict__ res) {
+  const int g = blockIdx.x;   // (record, sv)
   if (g >= n_rec * n_sv) return;
   const int2* rr = row_out + (size_t)g * n_rows;
+  const int2 best = first_max_row(rr, n_rows, threadIdx.x);
+  if (threadIdx.x != 0) return;
   gnsscorr_sdr_acq_result r = {};
   r.sv = svs[g % n_sv];
-  int32_t mag = 0;
-  for (int row = 0; row < n_rows; row++) {
-    const int2 v = rr[row];
-    if (v.x > mag) {
-      mag = v.x;
-      const int lcv = lmin + (weak ? row >> 3 : row >> 2), lcv2 = weak ? (row >> 1) & 3 : row & 3;
-      r.code_phase = v.y % kN;
-      r.doppler = lcv * 1000 + lcv2 * 250 + (v.y / kN) * 25;
-      r.magnitude = (uint32_t)v.x;
-      r.row = row;
-    }
+  if (best.x > 0) {
+    const int row = best.y, v = rr[row].y;
+    const int lcv = lmin + (weak ? row >> 3 : row >> 2), lcv2 = weak ? (row >> 1) & 3 : row & 3;
+    r.code_phase = v % kN;
+    r.doppler = lcv * 1000 + lcv2 * 250 + (v / kN) * 25;
+    r.magnitude = (uint32_t)best.x;
+    r.row = row;
   }
   r.success = r.magnitude > 0u;   // THRESH_MEDIUM = THRESH_WEAK = 0 (config.h:73-74)
   res[g] = r;
@@ -724,7 +738,7 @@ extern "C" int gnsscorr_sdr_acq_strong_dev(gnsscorr_sdr_acq_ctx* c, const int16_
                      c->d_X, c->d_codes, c->d_twi, d_svs, n_sv, lmin, n_rows, c->cfg.saturate,
                      c->d_rows);
   const int G = n_rec * n_sv;
-  hipLaunchKernelGGL(sdr_select_kernel, dim3((G + 63) / 64), dim3(64), 0, c->stream, c->d_rows,
+  hipLaunchKernelGGL(sdr_select_kernel, dim3(G), dim3(64), 0, c->stream, c->d_rows,
                      d_svs, n_sv, n_rec, lmin, n_rows, d_res);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
@@ -886,7 +900,7 @@ extern "C" int gnsscorr_sdr_acq_search_dev(gnsscorr_sdr_acq_ctx* c, int type, in
                        c->d_codes, c->d_twi, c->d_dft, d_svs, n_sv, lmin, n_rows,
                        c->cfg.saturate, c->d_rows);
   const int G = n_rec * n_sv;
-  hipLaunchKernelGGL(sdr_select_mw_kernel, dim3((G + 63) / 64), dim3(64), 0, c->stream, c->d_rows,
+  hipLaunchKernelGGL(sdr_select_mw_kernel, dim3(G), dim3(64), 0, c->stream, c->d_rows,
                      d_svs, n_sv, n_rec, lmin, n_rows, type == GNSSCORR_SDR_ACQ_WEAK ? 1 : 0,
                      d_res);
   HIP_TRY(hipGetLastError());
