@@ -59,6 +59,16 @@ def test_gn3s_dev_large(gpu, oracle):
     assert ph == (12345 + nb * 20000 * 2557223528) % (1 << 32)
 
 
+def test_gn3s_dev_misaligned_out(gpu):
+    """The kernel writes 16-byte stores: a misaligned d_out is refused (EINVAL),
+    nothing is launched and the caller's phase is left unchanged."""
+    fe = gpu.SdrFeCtx()
+    d_in = gpu.DevBuf.from_array(np.zeros(20000 // 4, np.uint8))
+    d_out = gpu.DevBuf(10240 * 4 + 16)
+    with pytest.raises(gpu.GnssCorrError, match="16-byte aligned"):
+        fe.gn3s_dev(d_in.ptr, True, 1, 7, d_out.ptr + 4)
+
+
 def test_downsample_golden(gpu):
     f = np.load(os.path.join(GOLD, "sdr_frontend.npz"))
     fe = gpu.SdrFeCtx()
