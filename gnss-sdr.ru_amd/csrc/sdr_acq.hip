@@ -109,6 +109,18 @@ __device__ __forceinline__ uint2 tw_entry(uint32_t w) {
   return make_uint2(pack(wi, (int16_t)-wq), pack(wq, wi));
 }
 
+// cmulsc(a, b, shift) with b given as tw_entry(b): the two products are
+// v_dot2_i32_i16 with the rounding constant as the accumulator.  Exact when
+// -b.q is an int16, i.e. b.q != -32768: the PRN spectra are within +-502
+// (checked at context creation).
+__device__ __forceinline__ uint32_t cmulsc_d2(uint32_t a, uint2 b2, int shift, bool sat) {
+  const short2_t av = __builtin_bit_cast(short2_t, a);
+  const int32_t rnd = 1 << (shift - 1);
+  const int32_t ti = __builtin_amdgcn_sdot2(av, __builtin_bit_cast(short2_t, b2.x), rnd, false) >> shift;
+  const int32_t tq = __builtin_amdgcn_sdot2(av, __builtin_bit_cast(short2_t, b2.y), rnd, false) >> shift;
+  return sat ? pack(sat16(ti), sat16(tq)) : pack((int16_t)ti, (int16_t)tq);
+}
+
 // ---------------------------------------------------------------------------
 // The reference's 11-rank radix-2 DIT (fft.cpp:156-180, rank/bfly loops
 // :314-334) run as radix-8 passes in registers.  The butterflies of rank r
@@ -320,16 +332,16 @@ __global__ __launch_bounds__(kThreads) void sdr_strong_kernel(
   const int rec = blockIdx.x / (n_lcv * n_sv);
   const int lcv = lmin + l;
   const uint32_t* cr = codes + (size_t)svs[s] * kN;
-  uint32_t cv[8];
+  uint2 cv[8];   // the thread's PRN-spectrum samples in dot2 form
 #pragma unroll
-  for (int m = 0; m < 8; m++) cv[m] = cr[nat_k(threadIdx.x, m)];
+  for (int m = 0; m < 8; m++) cv[m] = tw_entry(cr[nat_k(threadIdx.x, m)]);
   stage_twiddles<kThreads, true>(tw, tw_inv);
   const bool sat = saturate != 0;
   for (int lcv2 = 0; lcv2 < 4; lcv2++) {
     __syncthreads();   // twiddles staged / the previous row's last pass has read x
     const uint32_t* xr = X + ((size_t)rec * 4 + lcv2) * kN;
     dit_row_256<kR2, true>(x, tw, [&](int k, int m) {
-      return cmulsc(xr[(k + lcv) & (kN - 1)], cv[m], 10, sat);
+      return cmulsc_d2(xr[(k + lcv) & (kN - 1)], cv[m], 10, sat);
     });
     // last pass in registers, then x86_cmag (int32 wrap) + x86_max (first
     // index of the strict maximum, > 0): ties go to the smaller index
@@ -662,6 +674,9 @@ extern "C" int gnsscorr_sdr_acq_create(gnsscorr_sdr_acq_ctx** out, const gnsscor
     gnsscorr_sdr_post_dft((int16_t*)(w10 + 4 * (size_t)kWipe));
     gnsscorr_sdr_prn_codes(tmp);
     memcpy(h + 4 * kN, tmp, sizeof(uint32_t) * 51 * kN);
+    // cmulsc_d2 negates the code's Q component in int16 (sdr_strong_kernel)
+    for (size_t k = 0; k < (size_t)51 * kN * 2; k++)
+      if (((const int16_t*)tmp)[k] == -32768) rc = GNSSCORR_EINVAL;
     gnsscorr_sdr_twiddles((int16_t*)(h + 55 * kN), (int16_t*)(h + 55 * kN + kN / 2));
   }
   hipError_t e = hipSuccess;
