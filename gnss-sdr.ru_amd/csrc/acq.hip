@@ -30,7 +30,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-#include "gnsscorr_internal.h"
+#include "acq_ctx.h"
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -618,7 +618,7 @@ template <int MODE, bool DUMP>
 __global__ __launch_bounds__(kThreads) void acq_corr_kernel(
     const float2* __restrict__ X, const float2* __restrict__ F, int n_blocks,
     const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins,
-    int spc, gnsscorr_acq_row* __restrict__ stats, float* __restrict__ dump_power,
+    int spc, gnsscorr_acq_row* __restrict__ stats, double* __restrict__ dump_power,
     int dump_block, const int* __restrict__ order, const int4* __restrict__ fmap) {
   __shared__ float2 lds[N];
   __shared__ float2 tw[32];
@@ -1165,7 +1165,7 @@ __device__ void select_group(int g, int lane, const gnsscorr_acq_row* __restrict
                              const double* __restrict__ freqs, gnsscorr_acq_row* __restrict__ rows,
                              gnsscorr_acq_result* __restrict__ res) {
   const gnsscorr_acq_row* st = stats + (long)g * n_bins * n_blocks;
-  float pk = -1.f;
+  double pk = -1.0;
   int bin = 0x7fffffff;
   for (int b = lane; b < n_bins; b += 64) {
     const gnsscorr_acq_row r = combine_blocks(st + (long)b * n_blocks, n_blocks, mode);
@@ -1175,7 +1175,7 @@ __device__ void select_group(int g, int lane, const gnsscorr_acq_row* __restrict
   if (!res) return;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float v2 = __shfl_xor(pk, o, 64);
+    const double v2 = __shfl_xor(pk, o, 64);
     const int b2 = __shfl_xor(bin, o, 64);
     if (v2 > pk || (v2 == pk && b2 < bin)) { pk = v2; bin = b2; }
   }
@@ -1348,45 +1348,12 @@ static int host_out_index(int p) {
 // ============================================================================
 // context / C ABI
 // ============================================================================
-struct gnsscorr_acq_ctx {
-  gnsscorr_acq_cfg cfg;
-  hipStream_t stream = nullptr;
-  int* d_sigma = nullptr;
-  float2* d_F = nullptr;     // code spectra, permuted, [max_codes][N]
-  float2* d_X = nullptr;     // IF spectra, permuted, [max_freqs*max_blocks][N]
-  int n_codes = 0;
-  int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra
-  int* d_order = nullptr;               // workgroup -> work-unit permutation (XCD tiles)
-  int order_groups = 0, order_bins = 0, order_units = 0;
-  size_t cap_order = 0;
-  int4* d_fmap = nullptr;               // per frequency: spectrum class + shift coordinates
-  double* d_cfreq = nullptr;            // per class: the residue frequency whose spectrum is computed
-  double* d_resid = nullptr;            // per frequency: its fs/N-grid residue (classify scratch)
-  int* d_nclass = nullptr;
-  int n_cu = 256;                       // persistent grid of the pipelined kernel
-  int pipe = 1;                         // GNSSCORR_ACQ_PIPE=0: one-unit-per-workgroup kernel
-  int coh = 1;                          // code periods per coherent block (set_coherent)
-  float2* d_stage = nullptr;            // forward-FFT staging rows
-  size_t cap_stage = 0;
-  gnsscorr_acq_row* d_stats = nullptr;  // per (row, block) statistics
-  size_t cap_stats = 0;
-  int stat_groups = 0, stat_bins = 0, stat_blocks = 0, stat_mode = 0;
-  // host-API staging
-  int8_t* d_if = nullptr;
-  double* d_freqs = nullptr;
-  int* d_gcode = nullptr;
-  int* d_gfreq = nullptr;
-  gnsscorr_acq_row* d_rows = nullptr;
-  gnsscorr_acq_result* d_res = nullptr;
-  float* d_dump = nullptr;
-  size_t cap_rows = 0, cap_res = 0, cap_gcode = 0, cap_gfreq = 0;
-};
 
 static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
                           const double* d_freqs, int mode, int n_rows, float2* dst,
                           const double* d_cfreq, const int* d_nrows, int fuse_n = 0);
 
-static int grow(void** p, size_t* cap, size_t need, size_t elem) {
+int acq_grow(void** p, size_t* cap, size_t need, size_t elem) {
   if (need <= *cap) return GNSSCORR_OK;
   if (*p) (void)hipFree(*p);
   *p = nullptr;
@@ -1397,14 +1364,25 @@ static int grow(void** p, size_t* cap, size_t need, size_t elem) {
 }
 
 extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cfg* cfg) {
-  if (!out || !cfg || cfg->n_samples != N || cfg->max_freqs < 1 || cfg->max_blocks < 1 ||
-      cfg->max_codes < 1 || cfg->samp_rate <= 0) {
-    gnsscorr_set_error("gnsscorr_acq_create: bad config (n_samples must be %d)", N);
+  if (!out || !cfg || cfg->max_freqs < 1 || cfg->max_blocks < 1 || cfg->max_codes < 1 ||
+      cfg->samp_rate <= 0 ||
+      (cfg->precision != GNSSCORR_ACQ_F64 && cfg->precision != GNSSCORR_ACQ_F32)) {
+    gnsscorr_set_error("gnsscorr_acq_create: bad config");
+    return GNSSCORR_EINVAL;
+  }
+  if (cfg->precision == GNSSCORR_ACQ_F32 && cfg->n_samples != N) {
+    gnsscorr_set_error("gnsscorr_acq_create: the fp32 path needs n_samples %d (got %d)", N,
+                       cfg->n_samples);
+    return GNSSCORR_EINVAL;
+  }
+  if (cfg->precision == GNSSCORR_ACQ_F64 && !acq64_plan_for(cfg->n_samples)) {
+    gnsscorr_set_error("gnsscorr_acq_create: no fp64 plan for n_samples %d (supported: 16368, "
+                       "16000)", cfg->n_samples);
     return GNSSCORR_EINVAL;
   }
   *out = nullptr;
   // self-check of the prime-factor maps: both must be bijections
-  {
+  if (cfg->precision == GNSSCORR_ACQ_F32) {
     static int checked = 0;
     if (!checked) {
       char* seen = (char*)calloc(2 * N, 1);
@@ -1427,6 +1405,8 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
   HIP_TRY(hipSetDevice(cfg->device));
   auto* c = new gnsscorr_acq_ctx();
   c->cfg = *cfg;
+  c->prec = cfg->precision;
+  const int ns = cfg->n_samples;
   if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device) !=
           hipSuccess || c->n_cu < 1)
     c->n_cu = 256;
@@ -1436,17 +1416,26 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
     return code;
   };
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->d_sigma, sizeof(int) * N) != hipSuccess ||
+      hipMalloc(&c->d_if, (size_t)ns * 2 * cfg->max_blocks) != hipSuccess ||
+      hipMalloc(&c->d_freqs, sizeof(double) * cfg->max_freqs) != hipSuccess ||
+      hipMalloc(&c->d_cfreq, sizeof(double) * cfg->max_freqs) != hipSuccess ||
+      hipMalloc(&c->d_resid, sizeof(double) * cfg->max_freqs) != hipSuccess ||
+      hipMalloc(&c->d_nclass, sizeof(int)) != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_acq_create: device allocation failed");
+    return fail(GNSSCORR_ENOMEM);
+  }
+  if (c->prec == GNSSCORR_ACQ_F64) {
+    const int rc = acq64_init(c);
+    if (rc) return fail(rc);
+    *out = c;
+    return GNSSCORR_OK;
+  }
+  if (hipMalloc(&c->d_sigma, sizeof(int) * N) != hipSuccess ||
       hipMalloc(&c->d_F, sizeof(float2) * NPAD * (size_t)cfg->max_codes) != hipSuccess ||
       hipMalloc(&c->d_X, sizeof(float2) * NPAD * (size_t)cfg->max_freqs * cfg->max_blocks) != hipSuccess ||
       hipMemset(c->d_F, 0, sizeof(float2) * NPAD * (size_t)cfg->max_codes) != hipSuccess ||
       hipMemset(c->d_X, 0, sizeof(float2) * NPAD * (size_t)cfg->max_freqs * cfg->max_blocks) != hipSuccess ||
-      hipMalloc(&c->d_if, (size_t)N * 2 * cfg->max_blocks) != hipSuccess ||
-      hipMalloc(&c->d_freqs, sizeof(double) * cfg->max_freqs) != hipSuccess ||
-      hipMalloc(&c->d_fmap, sizeof(int4) * cfg->max_freqs) != hipSuccess ||
-      hipMalloc(&c->d_cfreq, sizeof(double) * cfg->max_freqs) != hipSuccess ||
-      hipMalloc(&c->d_resid, sizeof(double) * cfg->max_freqs) != hipSuccess ||
-      hipMalloc(&c->d_nclass, sizeof(int)) != hipSuccess) {
+      hipMalloc(&c->d_fmap, sizeof(int4) * cfg->max_freqs) != hipSuccess) {
     gnsscorr_set_error("gnsscorr_acq_create: device allocation failed");
     return fail(GNSSCORR_ENOMEM);
   }
@@ -1474,6 +1463,7 @@ extern "C" int gnsscorr_acq_destroy(gnsscorr_acq_ctx* c) {
   if (!c) return GNSSCORR_OK;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  acq64_free(c);
   void* bufs[] = {c->d_sigma, c->d_F, c->d_X, c->d_if, c->d_freqs, c->d_gcode, c->d_gfreq,
                   c->d_rows, c->d_res, c->d_dump, c->d_order, c->d_stage, c->d_stats,
                   c->d_fmap, c->d_cfreq, c->d_resid, c->d_nclass};
@@ -1510,16 +1500,31 @@ extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const in
     return GNSSCORR_EINVAL;
   }
   HIP_TRY(hipSetDevice(c->cfg.device));
+  const size_t bytes = (size_t)n_codes * c->cfg.n_samples;
   int8_t* d = nullptr;
-  HIP_TRY(hipMalloc(&d, (size_t)n_codes * N));
-  HIP_TRY(hipMemcpyAsync(d, h_codes, (size_t)n_codes * N, hipMemcpyHostToDevice, c->stream));
-  int rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F, nullptr, nullptr);
+  HIP_TRY(hipMalloc(&d, bytes));
+  int rc = GNSSCORR_OK;
+  if (hipMemcpyAsync(d, h_codes, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_acq_set_codes: H2D copy failed");
+    rc = GNSSCORR_EDEVICE;
+  } else if (c->prec == GNSSCORR_ACQ_F64) {
+    rc = acq64_set_codes(c, d, n_codes);
+  } else {
+    rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F, nullptr, nullptr);
+    if (!rc) {
+      hipLaunchKernelGGL(acq_symmetrize_kernel, dim3((n_codes * N + 255) / 256), dim3(256), 0,
+                         c->stream, c->d_F, n_codes);
+      if (hipGetLastError() != hipSuccess) {
+        gnsscorr_set_error("gnsscorr_acq_set_codes: symmetrize launch failed");
+        rc = GNSSCORR_EDEVICE;
+      }
+    }
+  }
+  // the staging buffer is freed on every path, after the stream has used it
+  const hipError_t es = hipStreamSynchronize(c->stream);
+  (void)hipFree(d);
   if (rc) return rc;
-  hipLaunchKernelGGL(acq_symmetrize_kernel, dim3((n_codes * N + 255) / 256), dim3(256), 0,
-                     c->stream, c->d_F, n_codes);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipFree(d));
+  HIP_TRY(es);
   c->n_codes = n_codes;
   return GNSSCORR_OK;
 }
@@ -1555,7 +1560,7 @@ static int ensure_order(gnsscorr_acq_ctx* c, int n_groups, int n_bins, int units
   const int R = n_groups * n_bins * units_per_row;
   int* perm = (int*)malloc(sizeof(int) * R);
   build_tile_order(n_groups, n_bins, units_per_row, perm);
-  int rc = grow((void**)&c->d_order, &c->cap_order, R, sizeof(int));
+  int rc = acq_grow((void**)&c->d_order, &c->cap_order, R, sizeof(int));
   if (rc) { free(perm); return rc; }
   hipError_t e = hipMemcpyAsync(c->d_order, perm, sizeof(int) * R, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1574,7 +1579,7 @@ static int ensure_order(gnsscorr_acq_ctx* c, int n_groups, int n_bins, int units
 static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_blocks,
                           const double* d_freqs, int mode, int n_rows, float2* dst,
                           const double* d_cfreq, const int* d_nrows, int fuse_n) {
-  int rc = grow((void**)&c->d_stage, &c->cap_stage, (size_t)n_rows * NPAD, sizeof(float2));
+  int rc = acq_grow((void**)&c->d_stage, &c->cap_stage, (size_t)n_rows * NPAD, sizeof(float2));
   if (rc) return rc;
   // grid-stride kernels: the device-side class count bounds the work, the grid
   // only the parallelism (n_rows is an upper bound of the rows)
@@ -1608,6 +1613,13 @@ static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n
                           int n_freqs, const double* d_freqs) {
   int rc = check_search(c, n_blocks, n_freqs, GNSSCORR_ACQ_BEST_OF_BLOCKS);
   if (rc) return rc;
+  if (c->prec == GNSSCORR_ACQ_F64) {
+    rc = acq64_spectra(c, d_if, iq, n_blocks, n_freqs, d_freqs);
+    if (rc) return rc;
+    c->spec_blocks = n_blocks;
+    c->spec_freqs = n_freqs;
+    return GNSSCORR_OK;
+  }
   // spectrum classes on the fs/N grid (one forward FFT per class and block)
   const int fuse = n_freqs <= kFuseClass ? n_freqs : 0;
   if (!fuse) {
@@ -1629,10 +1641,11 @@ static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n
 static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
                             const double* d_freqs, const int32_t* d_gcode,
                             const int32_t* d_gfreq, int spc, gnsscorr_acq_row* d_rows,
-                            gnsscorr_acq_result* d_res, float* d_dump, int dump_block) {
+                            gnsscorr_acq_result* d_res, double* d_dump, int dump_block) {
   int rc = check_search(c, n_blocks, c->spec_freqs > 0 ? c->spec_freqs : 1, mode);
   if (rc) return rc;
-  if (n_groups < 1 || n_bins < 1 || spc < 1 || spc > N / 2 || n_blocks != c->spec_blocks) {
+  if (n_groups < 1 || n_bins < 1 || spc < 1 || spc > c->cfg.n_samples / 2 ||
+      n_blocks != c->spec_blocks) {
     gnsscorr_set_error("gnsscorr_acq_correlate: bad arguments (groups %d, bins %d, spc %d, "
                        "blocks %d vs spectra %d)", n_groups, n_bins, spc, n_blocks, c->spec_blocks);
     return GNSSCORR_EINVAL;
@@ -1640,10 +1653,15 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
   const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;  // work units per row
   rc = ensure_order(c, n_groups, n_bins, upr);
   if (rc) return rc;
-  rc = grow((void**)&c->d_stats, &c->cap_stats, (size_t)n_groups * n_bins * n_blocks,
+  rc = acq_grow((void**)&c->d_stats, &c->cap_stats, (size_t)n_groups * n_bins * n_blocks,
             sizeof(gnsscorr_acq_row));
   if (rc) return rc;
   const int n_units = n_groups * n_bins * upr;
+  if (c->prec == GNSSCORR_ACQ_F64) {
+    rc = acq64_correlate(c, n_blocks, mode, n_groups, n_bins, d_gcode, d_gfreq, spc, d_dump,
+                         dump_block);
+    if (rc) return rc;
+  } else {
 #define ACQ_CORR_LAUNCH(M, D)                                                                \
   hipLaunchKernelGGL((acq_corr_kernel<M, D>), dim3(n_units), dim3(kThreads), 0, c->stream,    \
                      c->d_X, c->d_F, n_blocks, d_gcode, d_gfreq, n_bins, spc, c->d_stats,      \
@@ -1660,6 +1678,7 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
     ACQ_CORR_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, false);
 #undef ACQ_CORR_LAUNCH
   HIP_TRY(hipGetLastError());
+  }
   c->stat_groups = n_groups;
   c->stat_bins = n_bins;
   c->stat_blocks = n_blocks;
@@ -1679,7 +1698,7 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
 static int search_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int mode,
                          int n_freqs, const double* d_freqs, int n_groups, int n_bins,
                          const int32_t* d_gcode, const int32_t* d_gfreq, int spc,
-                         gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res, float* d_dump,
+                         gnsscorr_acq_row* d_rows, gnsscorr_acq_result* d_res, double* d_dump,
                          int dump_block) {
   int rc = spectra_launch(c, d_if, iq, n_blocks, n_freqs, d_freqs);
   if (rc) return rc;
@@ -1767,11 +1786,11 @@ static int stage_host(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blo
   }
   const size_t R = (size_t)n_groups * n_bins;
   int rc;
-  if ((rc = grow((void**)&c->d_rows, &c->cap_rows, R, sizeof(gnsscorr_acq_row)))) return rc;
-  if ((rc = grow((void**)&c->d_res, &c->cap_res, n_groups, sizeof(gnsscorr_acq_result)))) return rc;
-  if ((rc = grow((void**)&c->d_gcode, &c->cap_gcode, n_groups, sizeof(int)))) return rc;
-  if ((rc = grow((void**)&c->d_gfreq, &c->cap_gfreq, R, sizeof(int)))) return rc;
-  HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)n_blocks * c->coh * N * (iq ? 2 : 1),
+  if ((rc = acq_grow((void**)&c->d_rows, &c->cap_rows, R, sizeof(gnsscorr_acq_row)))) return rc;
+  if ((rc = acq_grow((void**)&c->d_res, &c->cap_res, n_groups, sizeof(gnsscorr_acq_result)))) return rc;
+  if ((rc = acq_grow((void**)&c->d_gcode, &c->cap_gcode, n_groups, sizeof(int)))) return rc;
+  if ((rc = acq_grow((void**)&c->d_gfreq, &c->cap_gfreq, R, sizeof(int)))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)n_blocks * c->coh * c->cfg.n_samples * (iq ? 2 : 1),
                          hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_freqs, h_freqs, sizeof(double) * n_freqs, hipMemcpyHostToDevice,
                          c->stream));
@@ -1809,7 +1828,7 @@ extern "C" int gnsscorr_acq_search(gnsscorr_acq_ctx* c, const int8_t* h_if, int 
 
 extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq,
                                       int n_blocks, int block, double freq, int code,
-                                      float* h_power) {
+                                      double* h_power) {
   if (!c || !h_if || !h_power || block < 0 || block >= n_blocks || code < 0 ||
       code >= c->n_codes) {
     gnsscorr_set_error("gnsscorr_acq_power_row: bad arguments");
@@ -1819,11 +1838,12 @@ extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, i
   const int32_t gc = code, gf = 0;
   int rc = stage_host(c, h_if, iq, n_blocks, 1, &freq, 1, 1, &gc, &gf);
   if (rc) return rc;
-  if (!c->d_dump) HIP_TRY(hipMalloc(&c->d_dump, sizeof(float) * N));
+  if (!c->d_dump) HIP_TRY(hipMalloc(&c->d_dump, sizeof(double) * c->cfg.n_samples));
   rc = search_launch(c, c->d_if, iq, n_blocks, GNSSCORR_ACQ_BEST_OF_BLOCKS, 1, c->d_freqs, 1, 1,
                      c->d_gcode, c->d_gfreq, 16, c->d_rows, nullptr, c->d_dump, block);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(h_power, c->d_dump, sizeof(float) * N, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(h_power, c->d_dump, sizeof(double) * c->cfg.n_samples,
+                         hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return GNSSCORR_OK;
 }

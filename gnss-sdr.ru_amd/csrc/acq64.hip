@@ -1,0 +1,930 @@
+// acq64.hip -- parallel code-phase acquisition at the reference's precision
+// (fp64), on gfx950.
+//
+// Reference: POSTPROCESSING_SCILAB_RECEIVERS/GPS/L1/acquisition.sci:46-192
+// (GLONASS: GLONASS/L1/acquisition.sci:46-198), which Scilab evaluates in
+// doubles:  X = fft(exp(i f 2 pi t) .* block), |ifft(X .* conj(fft(code)))|^2,
+// keep the block with the larger maximum, then peak / code phase / second
+// peak outside +-1 chip.  This file computes every one of those steps in fp64
+// (wipe-off, forward transforms, products, inverse transform, powers and the
+// comparisons), so rows agree with an fp64 evaluation to ~1e-13 relative.
+//
+// MI355X design
+//  * A 1-ms row of N complex doubles (256 KiB at N = 16368) does not fit the
+//    160 KiB LDS, so it lives in REGISTERS: T threads hold ~N/T complex values
+//    each, and every FFT stage is a batch of small in-register DFTs.  Between
+//    stages the row is exchanged through LDS in two halves -- the real parts
+//    (N doubles = 128 KiB), then the imaginary parts -- so the LDS only ever
+//    holds one fp64 plane of the row.
+//  * Three stages N = R1 * R2 * R3 per plan, two exchanges per transform:
+//      N = 16368 (16.368 Msps, BASELINE config 2): 16 x 33 x 31, Good-Thomas
+//        prime-factor (pairwise coprime): no twiddles at all; the Ruritanian
+//        input map and the CRT output map are folded into addressing, and the
+//        spectra are stored pre-permuted so the hot loads stay coalesced;
+//        512 threads, the 16 radix-31 groups beyond 512 are done as direct
+//        31-term sums from a side copy;
+//      N = 16000 (16 Msps, the Scilab receivers' initSettings.sci:69 default):
+//        40 x 40 x 10 Cooley-Tukey (decimation in frequency), 400 threads,
+//        every stage balanced (40 values per thread); inter-stage twiddles
+//        W^(k m) are generated per group from one table load by a complex
+//        recurrence (error ~1e-15).
+//  * Small DFTs are compile-time compositions: symmetric prime kernels
+//    (X_m = A_m - i B_m, X_{P-m} = A_m + i B_m), Good-Thomas for coprime
+//    splits (33 = 3 x 11, 40 = 8 x 5, 10 = 2 x 5), Cooley-Tukey for prime
+//    powers (16 = 4 x 4, 8 = 2 x 4); twiddle constants are constexpr-evaluated.
+//  * The inverse FFT is a forward FFT of conj(Y): |ifft(Y)|^2 = |fft(conj Y)|^2 / N^2.
+//  * The correlation kernel fuses conj(X)*F (with the bin's circular shift on
+//    the fs/N grid folded into the X load), the three stages, |.|^2, the
+//    non-coherent sum over blocks, and exact row statistics (argmax = first
+//    natural index of the maximum; second peak = max outside the open circular
+//    window (argmax - spc, argmax + spc)) in two register passes.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "acq_ctx.h"
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      gnsscorr_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                         __LINE__);                                                     \
+      return GNSSCORR_EDEVICE;                                                          \
+    }                                                                                   \
+  } while (0)
+
+namespace {
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+// ---- compile-time arithmetic -------------------------------------------------
+constexpr double kPi = 3.14159265358979323846264338327950288;
+
+constexpr double poly_sin(double x) {   // |x| <= pi/4, 1 ulp
+  double x2 = x * x, term = x, sum = x;
+  for (int i = 1; i < 12; i++) {
+    term *= -x2 / (double)((2 * i) * (2 * i + 1));
+    sum += term;
+  }
+  return sum;
+}
+constexpr double poly_cos(double x) {
+  double x2 = x * x, term = 1.0, sum = 1.0;
+  for (int i = 1; i < 12; i++) {
+    term *= -x2 / (double)((2 * i - 1) * (2 * i));
+    sum += term;
+  }
+  return sum;
+}
+struct CS { double c, s; };
+// cos, sin of 2 pi j / R: exact octant reduction in integers, then a series
+constexpr CS cs2pi(long j, long R) {
+  j %= R;
+  if (j < 0) j += R;
+  const long q = (8 * j) / R, rem = 8 * j - q * R;   // angle = (q + rem/R) pi/4
+  double c = 0, s = 0;
+  if ((q & 1) == 0) {
+    const double x = (double)rem / (double)R * (kPi / 4);
+    c = poly_cos(x);
+    s = poly_sin(x);
+  } else {   // phi = pi/4 + x in [pi/4, pi/2): use pi/2 - phi = (R - rem)/R pi/4
+    const double y = (double)(R - rem) / (double)R * (kPi / 4);
+    c = poly_sin(y);
+    s = poly_cos(y);
+  }
+  switch ((q >> 1) & 3) {
+    case 0: return CS{c, s};
+    case 1: return CS{-s, c};
+    case 2: return CS{-c, -s};
+    default: return CS{s, -c};
+  }
+}
+template <int R>
+struct TwTab {
+  double c[R], s[R];
+  constexpr TwTab() : c{}, s{} {
+    for (int j = 0; j < R; j++) {
+      const CS v = cs2pi(j, R);
+      c[j] = v.c;
+      s[j] = v.s;
+    }
+  }
+};
+template <int R>
+constexpr TwTab<R> kTw{};
+
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+constexpr int cinv(int a, int m) {   // a^-1 mod m (gcd(a, m) = 1)
+  a %= m;
+  for (int x = 1; x < m; x++)
+    if ((long)a * x % m == 1) return x;
+  return m == 1 ? 0 : -1;
+}
+constexpr bool is_prime(int r) {
+  if (r < 2) return false;
+  for (int d = 2; d * d <= r; d++)
+    if (r % d == 0) return false;
+  return true;
+}
+constexpr int small_pf(int r) {
+  for (int d = 2; d * d <= r; d++)
+    if (r % d == 0) return d;
+  return r;
+}
+// largest power of the smallest prime factor dividing r
+constexpr int pf_power(int r) {
+  const int p = small_pf(r);
+  int q = 1;
+  while (r % (q * p) == 0) q *= p;
+  return q;
+}
+
+// ---- complex helpers -----------------------------------------------------------
+__device__ __forceinline__ v2d mul_mi(v2d v) { return (v2d){v.y, -v.x}; }   // -i v
+__device__ __forceinline__ v2d mul_pi(v2d v) { return (v2d){-v.y, v.x}; }   // +i v
+__device__ __forceinline__ v2d cmul(v2d a, v2d b) {
+  return (v2d){fma(a.x, b.x, -(a.y * b.y)), fma(a.x, b.y, a.y * b.x)};
+}
+// v * W_R^j, W = exp(-2 pi i / R); j is a compile-time constant after unrolling
+template <int R>
+__device__ __forceinline__ v2d twc(v2d v, int j) {
+  j %= R;
+  if (j == 0) return v;
+  if (4 * j == R) return mul_mi(v);
+  if (2 * j == R) return -v;
+  if (4 * j == 3 * R) return mul_pi(v);
+  const double c = kTw<R>.c[j], s = kTw<R>.s[j];   // W^j = c - i s
+  return (v2d){fma(v.x, c, v.y * s), fma(v.y, c, -(v.x * s))};
+}
+
+// ---- small in-register DFTs (forward, natural order in and out) ---------------
+template <int R>
+__device__ __forceinline__ void dft(v2d (&x)[R]);
+
+__device__ __forceinline__ void dft2(v2d (&x)[2]) {
+  const v2d a = x[0], b = x[1];
+  x[0] = a + b;
+  x[1] = a - b;
+}
+__device__ __forceinline__ void dft4(v2d (&x)[4]) {
+  const v2d t0 = x[0] + x[2], t1 = x[0] - x[2], t2 = x[1] + x[3], t3 = x[1] - x[3];
+  x[0] = t0 + t2;
+  x[2] = t0 - t2;
+  x[1] = t1 + mul_mi(t3);
+  x[3] = t1 + mul_pi(t3);
+}
+// symmetric prime-length DFT
+template <int P>
+__device__ __forceinline__ void dft_prime(v2d (&x)[P]) {
+  constexpr int H = (P - 1) / 2;
+  v2d s[H + 1], d[H + 1];
+#pragma unroll
+  for (int j = 1; j <= H; j++) {
+    s[j] = x[j] + x[P - j];
+    d[j] = x[j] - x[P - j];
+  }
+  const v2d x0 = x[0];
+  v2d X0 = x0;
+#pragma unroll
+  for (int j = 1; j <= H; j++) X0 += s[j];
+#pragma unroll
+  for (int m = 1; m <= H; m++) {
+    v2d A = x0, B = (v2d){0.0, 0.0};
+#pragma unroll
+    for (int j = 1; j <= H; j++) {
+      const int q = (j * m) % P;
+      const double c = kTw<P>.c[q], sn = kTw<P>.s[q];
+      A = (v2d){fma(c, s[j].x, A.x), fma(c, s[j].y, A.y)};
+      B = (v2d){fma(sn, d[j].x, B.x), fma(sn, d[j].y, B.y)};
+    }
+    x[m] = (v2d){A.x + B.y, A.y - B.x};       // A - i B
+    x[P - m] = (v2d){A.x - B.y, A.y + B.x};   // A + i B
+  }
+  x[0] = X0;
+}
+// Good-Thomas R = A * B, gcd(A, B) = 1: n = (a B + b A) mod R, k = CRT(ka, kb)
+template <int A, int B>
+__device__ __forceinline__ void dft_pfa(v2d (&x)[A * B]) {
+  constexpr int R = A * B;
+  constexpr int eA = B * cinv(B % A, A) % R, eB = A * cinv(A % B, B) % R;
+  v2d y[A][B];
+#pragma unroll
+  for (int a = 0; a < A; a++)
+#pragma unroll
+    for (int b = 0; b < B; b++) y[a][b] = x[(a * B + b * A) % R];
+#pragma unroll
+  for (int b = 0; b < B; b++) {
+    v2d t[A];
+#pragma unroll
+    for (int a = 0; a < A; a++) t[a] = y[a][b];
+    dft<A>(t);
+#pragma unroll
+    for (int a = 0; a < A; a++) y[a][b] = t[a];
+  }
+#pragma unroll
+  for (int a = 0; a < A; a++) dft<B>(y[a]);
+#pragma unroll
+  for (int a = 0; a < A; a++)
+#pragma unroll
+    for (int b = 0; b < B; b++) x[(a * eA + b * eB) % R] = y[a][b];
+}
+// Cooley-Tukey R = A * B (decimation in frequency): n = a B + b, k = ka + A kb
+template <int A, int B>
+__device__ __forceinline__ void dft_ct(v2d (&x)[A * B]) {
+  constexpr int R = A * B;
+  v2d y[A][B];
+#pragma unroll
+  for (int b = 0; b < B; b++) {
+    v2d t[A];
+#pragma unroll
+    for (int a = 0; a < A; a++) t[a] = x[a * B + b];
+    dft<A>(t);
+#pragma unroll
+    for (int a = 0; a < A; a++) y[a][b] = twc<R>(t[a], a * b);
+  }
+#pragma unroll
+  for (int a = 0; a < A; a++) dft<B>(y[a]);
+#pragma unroll
+  for (int a = 0; a < A; a++)
+#pragma unroll
+    for (int b = 0; b < B; b++) x[a + A * b] = y[a][b];
+}
+template <int R>
+__device__ __forceinline__ void dft(v2d (&x)[R]) {
+  if constexpr (R == 1) {
+  } else if constexpr (R == 2) {
+    dft2(x);
+  } else if constexpr (R == 4) {
+    dft4(x);
+  } else if constexpr (is_prime(R)) {
+    dft_prime<R>(x);
+  } else if constexpr (pf_power(R) != R) {
+    constexpr int A = pf_power(R);
+    dft_pfa<A, R / A>(x);
+  } else {
+    constexpr int A = (small_pf(R) == 2 && R >= 16) ? 4 : small_pf(R);
+    dft_ct<A, R / A>(x);
+  }
+}
+
+// ---- plans -----------------------------------------------------------------------
+// N = R1 R2 R3.  Positions between stages (same for both kinds):
+//   after stage 1: k1*G1 + g,       g = n2*R3 + n3   (G1 = R2*R3 = stage-1 groups)
+//   after stage 2: (k1*R2 + k2)*R3 + n3
+// stage 2 groups g2 = k1*R3 + n3 (G2 = R1*R3), stage 3 groups g3 = k1*R2 + k2.
+// PFA: input n = (n1 Q1 + n2 Q2 + n3 Q3) mod N, output k = (k1 E1 + k2 E2 + k3 E3) mod N,
+//      spectra stored at n1*G1 + n2*R3 + n3 (digits n_i = (n mod R_i) INV_i mod R_i).
+// CT:  input n = n1*G1 + n2*R3 + n3, output k = k1 + R1 k2 + R1 R2 k3, twiddles
+//      W_N^(k1 g) after stage 1 and W_G1^(k2 n3) after stage 2; natural storage.
+template <int N_, int R1_, int R2_, int R3_, int T_, bool PFA_>
+struct Plan {
+  static constexpr int N = N_, R1 = R1_, R2 = R2_, R3 = R3_, T = T_;
+  static constexpr bool PFA = PFA_;
+  static constexpr int TB = (T + 63) / 64 * 64;   // launched threads (whole waves)
+  static constexpr int NW = TB / 64;
+  static constexpr int G1 = N / R1, G2 = N / R2, G3 = N / R3;
+  static constexpr int K1 = (G1 + T - 1) / T, K2 = (G2 + T - 1) / T;
+  static constexpr int K3 = G3 / T, L = G3 - K3 * T;   // leftover stage-3 groups
+  static constexpr int LS = L * R3 > 0 ? L * R3 : 1;
+  static constexpr int Q1 = N / R1, Q2 = N / R2, Q3 = N / R3;
+  static constexpr int INV1 = PFA ? cinv(Q1 % R1, R1) : 0;
+  static constexpr int INV2 = PFA ? cinv(Q2 % R2, R2) : 0;
+  static constexpr int INV3 = PFA ? cinv(Q3 % R3, R3) : 0;
+  static constexpr int E1 = PFA ? (int)((long)Q1 * INV1 % N) : 0;
+  static constexpr int E2 = PFA ? (int)((long)Q2 * INV2 % N) : 0;
+  static constexpr int E3 = PFA ? (int)((long)Q3 * INV3 % N) : 0;
+  static_assert(R1 * R2 * R3 == N, "plan factors");
+  static_assert(L * R3 <= T, "leftover stage-3 outputs must fit one per thread");
+  static_assert(!PFA || (cgcd(R1, R2) == 1 && cgcd(R1, R3) == 1 && cgcd(R2, R3) == 1),
+                "PFA needs coprime factors");
+  // natural input index of stage-1 element (n1, g)
+  __device__ static __forceinline__ int in_index(int n1, int g) {
+    if constexpr (PFA) {
+      const int n2 = g / R3, n3 = g % R3;
+      return (int)(((long)n1 * Q1 + (long)n2 * Q2 + (long)n3 * Q3) % N);
+    } else {
+      return n1 * G1 + g;
+    }
+  }
+  // natural output index of stage-3 slot k3 of group g3: base + k3*step (mod N)
+  __device__ static __forceinline__ void out_base(int g3, int& base, int& step) {
+    const int k1 = g3 / R2, k2 = g3 % R2;
+    if constexpr (PFA) {
+      base = (int)(((long)k1 * E1 + (long)k2 * E2) % N);
+      step = E3;
+    } else {
+      base = k1 + R1 * k2;
+      step = R1 * R2;
+    }
+  }
+  // storage position of natural index k in a spectrum row
+  __device__ static __forceinline__ int store_index(int k) {
+    if constexpr (PFA) {
+      const int n1 = (k % R1) * INV1 % R1, n2 = (k % R2) * INV2 % R2, n3 = (k % R3) * INV3 % R3;
+      return n1 * G1 + n2 * R3 + n3;
+    } else {
+      return k;
+    }
+  }
+};
+
+typedef Plan<16368, 16, 33, 31, 512, true> PlanA;   // 16.368 Msps
+typedef Plan<16000, 40, 40, 10, 400, false> PlanB;  // 16 Msps
+
+// multiply x[k] (k = 1..R-1) by w^k, w = W_M^m from the table; two interleaved
+// recurrences (odd / even powers) halve the dependency chain
+template <int R>
+__device__ __forceinline__ void twiddle_run(v2d (&x)[R], v2d w) {
+  const v2d w2 = cmul(w, w);
+  v2d po = w, pe = w2;
+#pragma unroll
+  for (int k = 1; k < R; k++) {
+    if (k & 1) {
+      x[k] = cmul(x[k], po);
+      if (k + 2 < R) po = cmul(po, w2);
+    } else {
+      x[k] = cmul(x[k], pe);
+      if (k + 2 < R) pe = cmul(pe, w2);
+    }
+  }
+}
+
+__device__ __forceinline__ double part(v2d v, int p) { return p ? v.y : v.x; }
+__device__ __forceinline__ void set_part(v2d& v, int p, double d) {
+  if (p)
+    v.y = d;
+  else
+    v.x = d;
+}
+
+// The transform from stage-1 inputs v1 (loaded by the caller) to stage-3
+// outputs v3 (main groups g3 = t + j*T) and vl (leftover output t < L*R3:
+// slot t % R3 of group K3*T + t / R3).  lds: N doubles; side: LS complex;
+// tw3: W_R3^q, q < R3 (LDS); twN: W_N^j (global, CT plans only).
+template <class P>
+__device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
+                                         const v2d* __restrict__ twN, int t,
+                                         v2d (&v1)[P::K1][P::R1], v2d (&v3)[P::K3][P::R3],
+                                         v2d& vl) {
+  constexpr int R1 = P::R1, R2 = P::R2, R3 = P::R3, T = P::T, G1 = P::G1, G2 = P::G2;
+  const bool act = t < T;
+  // ---- stage 1
+#pragma unroll
+  for (int j = 0; j < P::K1; j++) {
+    dft<R1>(v1[j]);
+    if constexpr (!P::PFA) {
+      const int g = t + j * T;
+      if (act && g < G1) twiddle_run<R1>(v1[j], twN[g]);
+    }
+  }
+  // ---- exchange 1: re then im
+  v2d v2[P::K2][R2];
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+#pragma unroll
+    for (int j = 0; j < P::K1; j++) {
+      const int g = t + j * T;
+      if (act && g < G1) {
+#pragma unroll
+        for (int k1 = 0; k1 < R1; k1++) lds[k1 * G1 + g] = part(v1[j][k1], p);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < P::K2; j++) {
+      const int g2 = t + j * T;
+      if (act && g2 < G2) {
+        const int base = (g2 / R3) * G1 + g2 % R3;
+#pragma unroll
+        for (int n2 = 0; n2 < R2; n2++) set_part(v2[j][n2], p, lds[base + n2 * R3]);
+      } else {
+#pragma unroll
+        for (int n2 = 0; n2 < R2; n2++) set_part(v2[j][n2], p, 0.0);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- stage 2
+#pragma unroll
+  for (int j = 0; j < P::K2; j++) {
+    dft<R2>(v2[j]);
+    if constexpr (!P::PFA) {
+      const int g2 = t + j * T;
+      if (act && g2 < G2) twiddle_run<R2>(v2[j], twN[(g2 % R3) * R1]);   // W_G1^n3 = W_N^(n3 R1)
+    }
+  }
+  // ---- exchange 2
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+#pragma unroll
+    for (int j = 0; j < P::K2; j++) {
+      const int g2 = t + j * T;
+      if (act && g2 < G2) {
+        const int k1 = g2 / R3, n3 = g2 % R3;
+#pragma unroll
+        for (int k2 = 0; k2 < R2; k2++) lds[(k1 * R2 + k2) * R3 + n3] = part(v2[j][k2], p);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < P::K3; j++) {
+      const int g3 = act ? t + j * T : 0;
+#pragma unroll
+      for (int n3 = 0; n3 < R3; n3++) set_part(v3[j][n3], p, lds[g3 * R3 + n3]);
+    }
+    if constexpr (P::L > 0) {
+      if (t < P::L * R3) set_part(vl, p, lds[P::K3 * T * R3 + t]);
+      if (p == 1 && t < P::L * R3) side[t] = vl;
+    }
+    __syncthreads();
+  }
+  // ---- stage 3
+#pragma unroll
+  for (int j = 0; j < P::K3; j++) dft<R3>(v3[j]);
+  if constexpr (P::L > 0) {
+    if (t < P::L * R3) {
+      const int lg = t / R3, m = t % R3;
+      const v2d* x = side + lg * R3;
+      v2d acc = (v2d){0.0, 0.0};
+      int q = 0;
+#pragma unroll
+      for (int n = 0; n < R3; n++) {
+        acc += cmul(x[n], tw3[q]);
+        q += m;
+        if (q >= R3) q -= R3;
+      }
+      vl = acc;
+    }
+  }
+}
+
+template <class P>
+__device__ __forceinline__ void init_tw3(v2d* tw3) {
+  if (threadIdx.x < P::R3)
+    tw3[threadIdx.x] = (v2d){kTw<P::R3>.c[threadIdx.x], -kTw<P::R3>.s[threadIdx.x]};
+}
+
+// ---- workgroup reductions --------------------------------------------------------
+__device__ __forceinline__ bool better(double v1, int k1, double v0, int k0) {
+  return v1 > v0 || (v1 == v0 && k1 < k0);
+}
+template <int NW>
+__device__ __forceinline__ void block_argmax(double& v, int& k, double* sv, int* sk) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(v, o, 64);
+    const int k2 = __shfl_xor(k, o, 64);
+    if (better(v2, k2, v, k)) { v = v2; k = k2; }
+  }
+  if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; sk[threadIdx.x >> 6] = k; }
+  __syncthreads();
+  v = sv[0];
+  k = sk[0];
+#pragma unroll
+  for (int i = 1; i < NW; i++)
+    if (better(sv[i], sk[i], v, k)) { v = sv[i]; k = sk[i]; }
+}
+template <int NW>
+__device__ __forceinline__ double block_max0(double v, double* sm) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 1; i < NW; i++) v = fmax(v, sm[i]);
+  }
+  return v;
+}
+
+// ---- forward transforms ------------------------------------------------------------
+// IF rows: x[n] = sum_{p<coh} IF[blk][n + pN] * exp(i f ((n+pN)*2)*pi*ts), evaluated as
+// acquisition.sci:61-62,107 does (phasePoints = (0:L-1)*2*%pi*ts; exp(%i*f*phasePoints))
+// at the class frequency f = cfreq[cls]; row = cls * n_blocks + blk.
+__global__ __launch_bounds__(256) void acq64_wipe_kernel(const int8_t* __restrict__ src, int iq,
+                                                         int n_blocks, int coh,
+                                                         const double* __restrict__ cfreq,
+                                                         const int* __restrict__ n_cls_dev,
+                                                         double ts, int N, v2d* __restrict__ out) {
+  const long total = (long)(*n_cls_dev) * n_blocks * N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(i / N), n = (int)(i % N);
+    const int cls = row / n_blocks, blk = row % n_blocks;
+    const double f = cfreq[cls];
+    const int8_t* s = src + (long)blk * coh * N * (iq ? 2 : 1);
+    double re = 0.0, im = 0.0;
+    for (int p = 0; p < coh; p++) {
+      const long m = n + (long)p * N;
+      const double I = iq ? (double)s[2 * m] : (double)s[m];
+      const double Q = iq ? (double)s[2 * m + 1] : 0.0;
+      const double th = f * ((((double)m * 2.0) * M_PI) * ts);
+      double sn, cs;
+      sincos(th, &sn, &cs);
+      re += I * cs - Q * sn;
+      im += I * sn + Q * cs;
+    }
+    out[i] = (v2d){re, im};
+  }
+}
+
+__global__ __launch_bounds__(256) void acq64_codes_kernel(const int8_t* __restrict__ codes,
+                                                          long n, v2d* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (v2d){(double)codes[i], 0.0};
+}
+
+// Natural-order complex rows -> spectra in the plan's storage order.
+template <class P>
+__global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict__ in,
+                                                          const int* __restrict__ n_cls_dev,
+                                                          int per_cls, int n_rows,
+                                                          v2d* __restrict__ out, int rs,
+                                                          const v2d* __restrict__ twN) {
+  __shared__ double lds[P::N];
+  __shared__ v2d side[P::LS];
+  __shared__ v2d tw3[P::R3];
+  const int t = threadIdx.x;
+  init_tw3<P>(tw3);
+  const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
+  for (int w = blockIdx.x; w < rows; w += gridDim.x) {
+    const v2d* src = in + (long)w * P::N;
+    v2d v1[P::K1][P::R1];
+#pragma unroll
+    for (int j = 0; j < P::K1; j++) {
+      const int g = t + j * P::T;
+      const bool ok = t < P::T && g < P::G1;
+#pragma unroll
+      for (int n1 = 0; n1 < P::R1; n1++)
+        v1[j][n1] = ok ? src[P::in_index(n1, g)] : (v2d){0.0, 0.0};
+    }
+    v2d v3[P::K3][P::R3], vl = (v2d){0.0, 0.0};
+    fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl);
+    v2d* o = out + (long)w * rs;
+    if (t < P::T) {
+#pragma unroll
+      for (int j = 0; j < P::K3; j++) {
+        int base, step;
+        P::out_base(t + j * P::T, base, step);
+        int k = base;
+#pragma unroll
+        for (int k3 = 0; k3 < P::R3; k3++) {
+          o[P::store_index(k)] = v3[j][k3];
+          k += step;
+          if (k >= P::N) k -= P::N;
+        }
+      }
+    }
+    if constexpr (P::L > 0) {
+      if (t < P::L * P::R3) {
+        int base, step;
+        P::out_base(P::K3 * P::T + t / P::R3, base, step);
+        const int k = (int)((base + (long)(t % P::R3) * step) % P::N);
+        o[P::store_index(k)] = vl;
+      }
+    }
+  }
+}
+
+// ---- the correlation kernel -------------------------------------------------------
+// One workgroup = one unit: BEST_OF_BLOCKS -> (row, block); NONCOHERENT -> row,
+// |.|^2 summed over the blocks in registers.  fmap[fid] = {class, m}: the bin's
+// spectrum is the class spectrum circularly shifted by m (X_f[k] = X_r[k - m]).
+template <class P, int MODE, bool DUMP>
+__global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
+    const v2d* __restrict__ X, const v2d* __restrict__ F, int rs, int n_blocks,
+    const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins, int spc,
+    gnsscorr_acq_row* __restrict__ stats, double* __restrict__ dump, int dump_block,
+    const int* __restrict__ order, const int2* __restrict__ fmap, const v2d* __restrict__ twN) {
+  constexpr int N = P::N, R1 = P::R1, R3 = P::R3, T = P::T, K3 = P::K3, L = P::L;
+  constexpr bool kNC = MODE == GNSSCORR_ACQ_NONCOHERENT;
+  __shared__ double lds[N];
+  __shared__ v2d side[P::LS];
+  __shared__ v2d tw3[R3];
+  __shared__ double s_v[P::NW], s_m[P::NW];
+  __shared__ int s_k[P::NW];
+  const int t = threadIdx.x;
+  const bool act = t < T;
+  init_tw3<P>(tw3);
+  const int unit = order[blockIdx.x];
+  const int rowid = kNC ? unit : unit / n_blocks;
+  const int blk0 = kNC ? 0 : unit % n_blocks;
+  const int nblk = kNC ? n_blocks : 1;
+  const int g = rowid / n_bins, bin = rowid % n_bins;
+  const int code = group_code[g];
+  const int2 fm = fmap[group_freq[g * n_bins + bin]];
+  const int m = fm.y;
+  const double inv_n2 = 1.0 / ((double)N * (double)N);
+  const v2d* Fc = F + (long)code * rs;
+
+  double pw[K3][R3], pwl = -1.0;
+#pragma unroll
+  for (int j = 0; j < K3; j++)
+#pragma unroll
+    for (int k = 0; k < R3; k++) pw[j][k] = 0.0;
+  if constexpr (kNC) pwl = 0.0;
+
+  for (int i = 0; i < nblk; i++) {
+    const int blk = blk0 + i;
+    const v2d* Xb = X + ((long)fm.x * n_blocks + blk) * rs;
+    // stage-1 inputs: conj(X[k - m]) * F[k]  (= conj(X * conj(F)), acquisition.sci:116)
+    v2d v1[P::K1][R1];
+#pragma unroll
+    for (int j = 0; j < P::K1; j++) {
+      const int gg0 = t + j * T;
+      const bool ok = act && gg0 < P::G1;
+      const int gg = ok ? gg0 : 0;
+      if constexpr (P::PFA) {
+        constexpr int R2 = P::R2;
+        const int m1 = (m % R1) * P::INV1 % R1, m2 = (m % R2) * P::INV2 % R2,
+                  m3 = (m % R3) * P::INV3 % R3;
+        int n2 = gg / R3 - m2, n3 = gg % R3 - m3;
+        n2 += n2 < 0 ? R2 : 0;
+        n3 += n3 < 0 ? R3 : 0;
+        const int gs = n2 * R3 + n3;
+#pragma unroll
+        for (int n1 = 0; n1 < R1; n1++) {
+          int n1s = n1 - m1;
+          n1s += n1s < 0 ? R1 : 0;
+          const v2d x = Xb[n1s * P::G1 + gs], f = Fc[n1 * P::G1 + gg];
+          v1[j][n1] = ok ? (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))}
+                         : (v2d){0.0, 0.0};
+        }
+      } else {
+#pragma unroll
+        for (int n1 = 0; n1 < R1; n1++) {
+          const int n = n1 * P::G1 + gg;
+          int s = n - m;
+          s += s < 0 ? N : 0;
+          const v2d x = Xb[s], f = Fc[n];
+          v1[j][n1] = ok ? (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))}
+                         : (v2d){0.0, 0.0};
+        }
+      }
+    }
+    v2d v3[K3][R3], vl = (v2d){0.0, 0.0};
+    fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl);
+    // |.|^2 / N^2 (|ifft(Y)|^2 = |fft(conj Y)|^2 / N^2)
+#pragma unroll
+    for (int j = 0; j < K3; j++)
+#pragma unroll
+      for (int k3 = 0; k3 < R3; k3++) {
+        const double p = fma(v3[j][k3].x, v3[j][k3].x, v3[j][k3].y * v3[j][k3].y) * inv_n2;
+        pw[j][k3] = kNC ? pw[j][k3] + p : p;
+      }
+    if constexpr (L > 0) {
+      if (t < L * R3) {
+        const double p = fma(vl.x, vl.x, vl.y * vl.y) * inv_n2;
+        pwl = kNC ? pwl + p : p;
+      }
+    }
+    if (DUMP && blk == dump_block && act) {
+#pragma unroll
+      for (int j = 0; j < K3; j++) {
+        int base, step;
+        P::out_base(t + j * T, base, step);
+        int k = base;
+#pragma unroll
+        for (int k3 = 0; k3 < R3; k3++) {
+          dump[(long)rowid * N + k] = pw[j][k3];
+          k += step;
+          if (k >= N) k -= N;
+        }
+      }
+      if constexpr (L > 0) {
+        if (t < L * R3) {
+          int base, step;
+          P::out_base(K3 * T + t / R3, base, step);
+          dump[(long)rowid * N + (int)((base + (long)(t % R3) * step) % N)] = pwl;
+        }
+      }
+    }
+  }
+  // ---- row statistics (exact, two passes over the registers)
+  double bv = -1.0;
+  int bk = INT_MAX;
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < K3; j++) {
+      int base, step;
+      P::out_base(t + j * T, base, step);
+      int k = base;
+#pragma unroll
+      for (int k3 = 0; k3 < R3; k3++) {
+        if (better(pw[j][k3], k, bv, bk)) { bv = pw[j][k3]; bk = k; }
+        k += step;
+        if (k >= N) k -= N;
+      }
+    }
+  }
+  int kl = INT_MAX;
+  if constexpr (L > 0) {
+    if (t < L * R3) {
+      int base, step;
+      P::out_base(K3 * T + t / R3, base, step);
+      kl = (int)((base + (long)(t % R3) * step) % N);
+      if (better(pwl, kl, bv, bk)) { bv = pwl; bk = kl; }
+    }
+  }
+  block_argmax<P::NW>(bv, bk, s_v, s_k);
+  // second peak: max outside the open circular window (bk - spc, bk + spc)
+  auto outside = [&](int k) {
+    int d = k - bk;
+    d += d < 0 ? N : 0;
+    return d >= spc && d <= N - spc;
+  };
+  double sv = -1.0;
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < K3; j++) {
+      int base, step;
+      P::out_base(t + j * T, base, step);
+      int k = base;
+#pragma unroll
+      for (int k3 = 0; k3 < R3; k3++) {
+        if (outside(k)) sv = fmax(sv, pw[j][k3]);
+        k += step;
+        if (k >= N) k -= N;
+      }
+    }
+  }
+  if constexpr (L > 0) {
+    if (t < L * R3 && outside(kl)) sv = fmax(sv, pwl);
+  }
+  sv = block_max0<P::NW>(sv, s_m);
+  if (t == 0) {
+    gnsscorr_acq_row r;
+    r.peak = bv;
+    r.second = sv;
+    r.argmax = bk;
+    r.block = kNC ? -1 : blk0;
+    stats[(long)rowid * n_blocks + blk0] = r;
+  }
+}
+
+// Frequencies -> spectrum classes on the fs/N grid: class = canonical residue
+// r = f mod fs/N (one forward FFT per class and block); bin f = r + m fs/N
+// reads the class spectrum shifted by m.  fmap[i] = {class, m mod N}.
+__device__ __forceinline__ double grid_residue(double f, double delta) {
+  double r = fmod(f, delta);
+  return r < 0 ? r + delta : r;
+}
+__global__ __launch_bounds__(1024) void acq64_classify_kernel(const double* __restrict__ freqs,
+                                                              int n, double delta, int N,
+                                                              int2* __restrict__ fmap,
+                                                              double* __restrict__ cfreq,
+                                                              int* __restrict__ n_classes,
+                                                              double* __restrict__ resid,
+                                                              int* __restrict__ lead) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) resid[i] = grid_residue(freqs[i], delta);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double r = resid[i];
+    int l = i;
+    for (int j = 0; j < i; j++)
+      if (resid[j] == r) { l = j; break; }
+    lead[i] = l;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int l = lead[i];
+    int cls = 0;
+    for (int k = 0; k < l; k++) cls += lead[k] == k;
+    const double q = rint((freqs[i] - resid[i]) / delta);
+    int mN = (fabs(q) < 1e9 ? (int)fmod(q, (double)N) : 0);
+    mN += mN < 0 ? N : 0;
+    fmap[i] = make_int2(cls, mN);
+    if (l == i) cfreq[cls] = resid[i];
+  }
+  if (threadIdx.x == 0) {
+    int cnt = 0;
+    for (int k = 0; k < n; k++) cnt += lead[k] == k;
+    *n_classes = cnt;
+  }
+}
+
+// ---- launch helpers ---------------------------------------------------------------
+template <class P>
+int fwd_launch(gnsscorr_acq_ctx* c, const v2d* in, const int* n_cls_dev, int per_cls,
+               int n_rows, v2d* out) {
+  const int grid = n_rows < 1024 ? n_rows : 1024;
+  hipLaunchKernelGGL((acq64_fwd_kernel<P>), dim3(grid), dim3(P::TB), 0, c->stream, in, n_cls_dev,
+                     per_cls, n_rows, out, c->rs64, (const v2d*)c->d_twN);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+template <class P>
+int corr_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_units, int n_bins,
+                const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
+                int dump_block) {
+#define ACQ64_LAUNCH(M, D)                                                                  \
+  hipLaunchKernelGGL((acq64_corr_kernel<P, M, D>), dim3(n_units), dim3(P::TB), 0, c->stream, \
+                     (const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, d_gcode,   \
+                     d_gfreq, n_bins, spc, c->d_stats, d_dump, dump_block, c->d_order,         \
+                     c->d_fmap64, (const v2d*)c->d_twN)
+  if (d_dump)
+    ACQ64_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
+  else if (mode == GNSSCORR_ACQ_NONCOHERENT)
+    ACQ64_LAUNCH(GNSSCORR_ACQ_NONCOHERENT, false);
+  else
+    ACQ64_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, false);
+#undef ACQ64_LAUNCH
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+}  // namespace
+
+int acq64_plan_for(int n_samples) {
+  if (n_samples == PlanA::N) return 1;
+  if (n_samples == PlanB::N) return 2;
+  return 0;
+}
+
+int acq64_init(gnsscorr_acq_ctx* c) {
+  c->plan64 = acq64_plan_for(c->cfg.n_samples);
+  if (!c->plan64) {
+    gnsscorr_set_error("acq64: no fp64 plan for n_samples %d (supported: %d, %d)",
+                       c->cfg.n_samples, PlanA::N, PlanB::N);
+    return GNSSCORR_EINVAL;
+  }
+  const int N = c->cfg.n_samples;
+  c->rs64 = (N + 63) & ~63;
+  HIP_TRY(hipMalloc(&c->d_F64, sizeof(double2) * (size_t)c->rs64 * c->cfg.max_codes));
+  HIP_TRY(hipMemset(c->d_F64, 0, sizeof(double2) * (size_t)c->rs64 * c->cfg.max_codes));
+  HIP_TRY(hipMalloc(&c->d_fmap64, sizeof(int2) * c->cfg.max_freqs));
+  HIP_TRY(hipMalloc(&c->d_lead64, sizeof(int) * c->cfg.max_freqs));
+  HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
+  double2* tw = (double2*)malloc(sizeof(double2) * N);
+  for (int j = 0; j < N; j++) {
+    // W_N^j = exp(-2 pi i j / N), argument reduced to [0, pi/4]-accurate libm calls
+    const double a = 2.0 * M_PI * ((double)j / (double)N);
+    tw[j] = make_double2(cos(a), -sin(a));
+  }
+  hipError_t e = hipMemcpy(c->d_twN, tw, sizeof(double2) * N, hipMemcpyHostToDevice);
+  free(tw);
+  HIP_TRY(e);
+  return GNSSCORR_OK;
+}
+
+void acq64_free(gnsscorr_acq_ctx* c) {
+  void* bufs[] = {c->d_F64, c->d_X64, c->d_in64, c->d_twN, c->d_fmap64, c->d_lead64};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  c->d_F64 = c->d_X64 = c->d_in64 = c->d_twN = nullptr;
+  c->d_fmap64 = nullptr;
+  c->d_lead64 = nullptr;
+}
+
+int acq64_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
+  const int N = c->cfg.n_samples;
+  int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)n_codes * N, sizeof(double2));
+  if (rc) return rc;
+  const long n = (long)n_codes * N;
+  hipLaunchKernelGGL(acq64_codes_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, d_codes,
+                     n, (v2d*)c->d_in64);
+  HIP_TRY(hipGetLastError());
+  return c->plan64 == 1
+             ? fwd_launch<PlanA>(c, (const v2d*)c->d_in64, nullptr, 1, n_codes, (v2d*)c->d_F64)
+             : fwd_launch<PlanB>(c, (const v2d*)c->d_in64, nullptr, 1, n_codes, (v2d*)c->d_F64);
+}
+
+int acq64_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int n_freqs,
+                  const double* d_freqs) {
+  const int N = c->cfg.n_samples;
+  const int rows = n_freqs * n_blocks;   // upper bound: classes <= frequencies
+  int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)rows * N, sizeof(double2));
+  if (rc) return rc;
+  rc = acq_grow((void**)&c->d_X64, &c->cap_X64, (size_t)rows * c->rs64, sizeof(double2));
+  if (rc) return rc;
+  hipLaunchKernelGGL(acq64_classify_kernel, dim3(1), dim3(1024), 0, c->stream, d_freqs, n_freqs,
+                     c->cfg.samp_rate / N, N, c->d_fmap64, c->d_cfreq, c->d_nclass, c->d_resid,
+                     c->d_lead64);
+  HIP_TRY(hipGetLastError());
+  const long work = (long)rows * N;
+  const int grid = (int)((work + 255) / 256 < 8192 ? (work + 255) / 256 : 8192);
+  hipLaunchKernelGGL(acq64_wipe_kernel, dim3(grid), dim3(256), 0, c->stream, d_if, iq, n_blocks,
+                     c->coh, c->d_cfreq, c->d_nclass, 1.0 / c->cfg.samp_rate, N,
+                     (v2d*)c->d_in64);
+  HIP_TRY(hipGetLastError());
+  return c->plan64 == 1
+             ? fwd_launch<PlanA>(c, (const v2d*)c->d_in64, c->d_nclass, n_blocks, rows,
+                                 (v2d*)c->d_X64)
+             : fwd_launch<PlanB>(c, (const v2d*)c->d_in64, c->d_nclass, n_blocks, rows,
+                                 (v2d*)c->d_X64);
+}
+
+int acq64_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
+                    const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
+                    int dump_block) {
+  const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;
+  const int n_units = n_groups * n_bins * upr;
+  return c->plan64 == 1 ? corr_launch<PlanA>(c, n_blocks, mode, n_units, n_bins, d_gcode, d_gfreq,
+                                             spc, d_dump, dump_block)
+                        : corr_launch<PlanB>(c, n_blocks, mode, n_units, n_bins, d_gcode, d_gfreq,
+                                             spc, d_dump, dump_block);
+}

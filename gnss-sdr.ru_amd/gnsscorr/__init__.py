@@ -32,14 +32,15 @@ CHAN_STATE = np.dtype([("carrier_phase", "<u4"), ("carrier_cycle", "<u4"),
                        ("pad", "<i4")])
 TRACK_RESULT = np.dtype([("n_dumps", "<i4"), ("dump", "<i4", (6,)), ("msbit_reg", "<i4"),
                          ("tic", "<i4"), ("tic_regs", "<i4", (6,)), ("pad", "<i4")])
-ACQ_ROW = np.dtype([("peak", "<f4"), ("argmax", "<i4"), ("second", "<f4"), ("block", "<i4")])
-ACQ_RESULT = np.dtype([("peak", "<f4"), ("second", "<f4"), ("metric", "<f4"), ("bin", "<i4"),
-                       ("code_phase", "<i4"), ("pad", "<i4"), ("carr_freq", "<f8")])
+ACQ_ROW = np.dtype([("peak", "<f8"), ("second", "<f8"), ("argmax", "<i4"), ("block", "<i4")])
+ACQ_RESULT = np.dtype([("peak", "<f8"), ("second", "<f8"), ("metric", "<f8"), ("bin", "<i4"),
+                       ("code_phase", "<i4"), ("pad", "<i4"), ("pad2", "<i4"),
+                       ("carr_freq", "<f8")])
 SIG = np.dtype([("system", "<i4"), ("prn", "<i4"), ("fch", "<i4"), ("data_bits", "<i4"),
                 ("code_phase", "<f8"), ("doppler", "<f8"), ("cn0", "<f8"),
                 ("carr_phase", "<f8")])
 assert NCO_CMD.itemsize == 24 and CHAN_STATE.itemsize == 56 and TRACK_RESULT.itemsize == 64
-assert ACQ_ROW.itemsize == 16 and ACQ_RESULT.itemsize == 32 and SIG.itemsize == 48
+assert ACQ_ROW.itemsize == 24 and ACQ_RESULT.itemsize == 48 and SIG.itemsize == 48
 
 OSG_LOOP = np.dtype([("state", "<i4"), ("n_freq", "<i4"), ("i_confirm", "<i4"),
                      ("n_thresh", "<i4"), ("codes", "<i4"), ("del_freq", "<i4"),
@@ -113,6 +114,8 @@ SDR_RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
 
 ACQ_BEST_OF_BLOCKS = 0
 ACQ_NONCOHERENT = 1
+ACQ_F64 = 0      # reference precision (acquisition.sci evaluates in doubles)
+ACQ_F32 = 1      # single-precision fast path (n_samples 16368 only)
 
 
 class TrackCfg(C.Structure):
@@ -122,7 +125,8 @@ class TrackCfg(C.Structure):
 
 class AcqCfg(C.Structure):
     _fields_ = [("samp_rate", C.c_double), ("n_samples", C.c_int), ("device", C.c_int),
-                ("max_freqs", C.c_int), ("max_blocks", C.c_int), ("max_codes", C.c_int)]
+                ("max_freqs", C.c_int), ("max_blocks", C.c_int), ("max_codes", C.c_int),
+                ("precision", C.c_int)]
 
 
 class SgtCfg(C.Structure):
@@ -491,8 +495,10 @@ class AcqCtx:
     """Parallel code-phase acquisition context (SoftGNSS acquisition.sci semantics)."""
 
     def __init__(self, samp_rate: float = 16.368e6, n_samples: int = 16368, device: int = 0,
-                 max_freqs: int = 1024, max_blocks: int = 16, max_codes: int = 64):
-        cfg = AcqCfg(samp_rate, n_samples, device, max_freqs, max_blocks, max_codes)
+                 max_freqs: int = 1024, max_blocks: int = 16, max_codes: int = 64,
+                 precision: int = ACQ_F64):
+        cfg = AcqCfg(samp_rate, n_samples, device, max_freqs, max_blocks, max_codes, precision)
+        self.precision = precision
         h = C.c_void_p()
         _check(lib().gnsscorr_acq_create(C.byref(h), C.byref(cfg)), "gnsscorr_acq_create")
         self.h = h
@@ -553,7 +559,7 @@ class AcqCtx:
 
     def power_row(self, if_samples, n_blocks, block, freq, code, iq=True) -> np.ndarray:
         if_samples = np.ascontiguousarray(if_samples, np.int8)
-        out = np.empty(self.n, np.float32)
+        out = np.empty(self.n, np.float64)
         _check(lib().gnsscorr_acq_power_row(self.h, _ptr(if_samples), int(iq), n_blocks, block,
                                             freq, code, _ptr(out)), "gnsscorr_acq_power_row")
         return out

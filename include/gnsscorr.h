@@ -208,32 +208,42 @@ int gnsscorr_osg_closed_loop_dev(gnsscorr_track_ctx *ctx, const gnsscorr_osg_loo
 
 typedef struct gnsscorr_acq_ctx gnsscorr_acq_ctx;
 
+/* Arithmetic of the acquisition kernels (gnsscorr_acq_cfg.precision).
+ * F64 is the reference's own precision (Scilab evaluates acquisition.sci in
+ * doubles): wipe-off, transforms, products, powers and comparisons in fp64;
+ * n_samples 16368 (16.368 Msps) or 16000 (16 Msps, initSettings.sci:69).
+ * F32 is the faster single-precision path, n_samples 16368 only; its rows
+ * agree with fp64 to ~1e-5 of the row maximum. */
+#define GNSSCORR_ACQ_F64 0
+#define GNSSCORR_ACQ_F32 1
+
 typedef struct {
   double samp_rate;       /* settings.samplingFreq                                 */
-  int    n_samples;       /* samplesPerCode = round(fs/(codeFreq/codeLength)); must be
-                             16368 (= 16*3*11*31) in this build                     */
+  int    n_samples;       /* samplesPerCode = round(fs/(codeFreq/codeLength))       */
   int    device;
   int    max_freqs;       /* capacity of the carrier-frequency table               */
   int    max_blocks;      /* capacity of 1-ms IF blocks per search                 */
   int    max_codes;       /* capacity of the code table                            */
+  int    precision;       /* GNSSCORR_ACQ_F64 (default, 0) or GNSSCORR_ACQ_F32      */
 } gnsscorr_acq_cfg;
 
 /* Statistics of one correlation row (code x carrier frequency [x block]). */
 typedef struct {
-  float   peak;           /* max |ifft|^2 of the row                               */
+  double  peak;           /* max |ifft|^2 of the row                               */
+  double  second;         /* max outside the open +-spc window around argmax       */
   int32_t argmax;         /* 0-based sample index of the first maximum             */
-  float   second;         /* max outside the open +-spc window around argmax       */
   int32_t block;          /* which block the stats come from (best-of-blocks mode) */
 } gnsscorr_acq_row;
 
 /* Per search group (one PRN / FCH), acquisition.sci:141-186. */
 typedef struct {
-  float   peak;           /* peakSize                                              */
-  float   second;         /* secondPeakSize                                        */
-  float   metric;         /* peakSize / secondPeakSize                             */
+  double  peak;           /* peakSize                                              */
+  double  second;         /* secondPeakSize                                        */
+  double  metric;         /* peakSize / secondPeakSize                             */
   int32_t bin;            /* 0-based frequencyBinIndex-1                           */
   int32_t code_phase;     /* 1-based codePhase (as acquisition.sci returns it)     */
-  int32_t pad;
+  int32_t pad;            /* 1: an exact tie put the first column in another row   */
+  int32_t pad2;
   double  carr_freq;      /* carrier frequency of the winning bin [Hz]             */
 } gnsscorr_acq_result;
 
@@ -294,9 +304,9 @@ int gnsscorr_acq_select_dev(gnsscorr_acq_ctx *ctx, int n_groups, int n_bins, con
  * first code period of |ifft|^2 as acquisition.sci keeps them.  Needs
  * n_blocks * coh_ms <= max_blocks.  Default 1. */
 int gnsscorr_acq_set_coherent(gnsscorr_acq_ctx *ctx, int coh_ms);
-/* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples floats. */
+/* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples doubles. */
 int gnsscorr_acq_power_row(gnsscorr_acq_ctx *ctx, const int8_t *h_if, int iq, int n_blocks,
-                           int block, double freq, int code, float *h_power);
+                           int block, double freq, int code, double *h_power);
 int gnsscorr_acq_sync(gnsscorr_acq_ctx *ctx);
 void *gnsscorr_acq_stream(gnsscorr_acq_ctx *ctx);
 

@@ -1,14 +1,16 @@
-"""GPU parity: HIP prime-factor-FFT acquisition vs the fp64 acquisition.sci oracle.
+"""GPU parity: HIP acquisition vs the fp64 acquisition.sci oracle.
 
 Reference: POSTPROCESSING_SCILAB_RECEIVERS/GPS/L1/acquisition.sci:46-192 and
 GLONASS/L1/acquisition.sci:46-198, restated in oracle/acq_oracle.py.
 
-Tolerances (fp32 on the GPU vs fp64 oracle; written here):
-  * power rows: |P_gpu - P_ref| <= 2e-5 * max(P_ref row)  (elementwise)
-  * row peak / second peak: relative 1e-4
-  * code phase, frequency bin, chosen block: exact whenever the oracle's best
-    value beats the runner-up by more than the tolerance (ties in noise can
-    legitimately resolve either way in fp32).
+Two precisions (gnsscorr_acq_cfg.precision):
+  * F64 -- the reference's own arithmetic (Scilab doubles).  Tolerances are the
+    north_star contract, 1e-6 relative, on every power, row peak, second peak
+    and metric (observed errors are ~1e-13 and are printed); code phase,
+    frequency bin and chosen block must equal the oracle's unconditionally.
+  * F32 -- the single-precision fast path: powers within 2e-5 of the row max,
+    peaks 1e-4, decisions exact whenever the oracle's winner is clear of the
+    runner-up (ties in noise can resolve either way in fp32).
 """
 import numpy as np
 import pytest
@@ -18,50 +20,96 @@ import acq_oracle as A
 pytestmark = pytest.mark.gpu
 FS = 16.368e6
 N = 16368
+F64_TOL = 1e-6          # north_star: within 1e-6 relative on floating-point results
+F64_CLASS = 1e-9        # and genuinely double precision (fp32 anywhere would show ~1e-6)
 
 
 def _sig(prn, cp, dop, cn0=50.0, data=0):
     return dict(system=0, prn=prn, code_phase=cp, doppler=dop, cn0=cn0, data_bits=data)
 
 
-@pytest.fixture(scope="module")
-def acq(gpu):
-    ctx = gpu.AcqCtx(FS, N, max_freqs=1024, max_blocks=10, max_codes=40)
+@pytest.fixture(scope="module", params=["f64", "f32"])
+def acq(request, gpu):
+    prec = gpu.ACQ_F64 if request.param == "f64" else gpu.ACQ_F32
+    ctx = gpu.AcqCtx(FS, N, max_freqs=1024, max_blocks=10, max_codes=40, precision=prec)
     codes = np.stack([A.make_ca_table_row(p, FS) for p in range(1, 33)] +
                      [A.make_st_table_row(FS)])
     ctx.set_codes(codes)
     return ctx, codes
 
 
+def _is64(ctx):
+    return ctx.precision == 0
+
+
+def _rel(a, b):
+    return abs(float(a) - float(b)) / abs(float(b))
+
+
+def check_rows(res, rows, ref, ref_rows, f64, tol=1e-4, label=""):
+    """Row statistics and per-group results against the oracle; returns the
+    largest relative error seen (peaks, second peaks, metrics)."""
+    worst = 0.0
+    for g in range(len(ref)):
+        for b, rr in enumerate(ref_rows[g]):
+            r = rows[g, b]
+            if f64:
+                e = max(_rel(r["peak"], rr["peak"]), _rel(r["second"], rr["second"]))
+                worst = max(worst, e)
+                assert e <= F64_TOL, (label, g, b, e)
+                assert r["argmax"] == rr["argmax"], (label, g, b)
+                assert r["block"] == rr["block"], (label, g, b)
+            else:
+                assert abs(r["peak"] - rr["peak"]) <= tol * rr["peak"], (g, b)
+                assert abs(r["second"] - rr["second"]) <= tol * rr["peak"], (g, b)
+        rg = ref[g]
+        if f64:
+            e = max(_rel(res[g]["peak"], rg["peak"]), _rel(res[g]["second"], rg["second"]),
+                    _rel(res[g]["metric"], rg["metric"]))
+            worst = max(worst, e)
+            assert e <= F64_TOL, (label, g, e)
+            assert res[g]["bin"] == rg["bin"], (label, g)
+            assert res[g]["code_phase"] == rg["code_phase"], (label, g)
+        else:
+            assert abs(res[g]["peak"] - rg["peak"]) <= tol * rg["peak"]
+            assert abs(res[g]["metric"] - rg["metric"]) <= 10 * tol * rg["metric"]
+            pk = np.array([r["peak"] for r in ref_rows[g]])
+            srt = np.sort(pk)
+            if srt[-1] - srt[-2] > 1e-3 * srt[-1]:
+                assert res[g]["bin"] == rg["bin"], g
+            if rg["metric"] > 1.01:
+                assert res[g]["code_phase"] == rg["code_phase"], g
+    if f64:
+        print(f"[{label}] max relative error vs fp64 oracle: {worst:.3e}")
+        assert worst < F64_CLASS, (label, worst)
+    return worst
+
+
+# backwards-compatible name used by other test modules (fp32 tolerances)
+def _check_rows(res, rows, ref, ref_rows, tol=1e-4):
+    return check_rows(res, rows, ref, ref_rows, False, tol)
+
+
 def test_power_rows_match_oracle(gpu, acq):
     ctx, codes = acq
     IF = gpu.ifgen(2 * N, [_sig(7, 100.5, 1234.0), _sig(12, 800.0, -3000.0)], fs=FS, seed=3)
+    worst = 0.0
     for code, freq, blk in [(6, 2.42e6 + 1000, 0), (6, 2.42e6 + 1234, 1), (11, 2.42e6 - 3000, 0),
                             (0, 2.42e6, 1), (32, 1.0e6, 0)]:
         got = ctx.power_row(IF, 2, blk, freq, code)
         ref = A.power_rows(IF, FS, codes[code], freq)[blk]
-        err = np.abs(got.astype(np.float64) - ref).max() / ref.max()
-        assert err < 2e-5, (code, freq, blk, err)
+        err = np.abs(got - ref).max() / ref.max()
+        if _is64(ctx):
+            # every cell, relative to the row maximum, and the peak to itself
+            assert err < F64_TOL, (code, freq, blk, err)
+            assert _rel(got.max(), ref.max()) < F64_TOL
+            worst = max(worst, err)
+        else:
+            assert err < 2e-5, (code, freq, blk, err)
         assert np.argmax(got) == np.argmax(ref)
-
-
-def _check_rows(res, rows, ref, ref_rows, tol=1e-4):
-    G = len(ref)
-    for g in range(G):
-        for b, rr in enumerate(ref_rows[g]):
-            r = rows[g, b]
-            assert abs(r["peak"] - rr["peak"]) <= tol * rr["peak"], (g, b)
-            assert abs(r["second"] - rr["second"]) <= tol * rr["peak"], (g, b)
-        rg = ref[g]
-        assert abs(res[g]["peak"] - rg["peak"]) <= tol * rg["peak"]
-        assert abs(res[g]["metric"] - rg["metric"]) <= 10 * tol * rg["metric"]
-        # decisions exact when the oracle's winner is clear of the runner-up
-        pk = np.array([r["peak"] for r in ref_rows[g]])
-        srt = np.sort(pk)
-        if srt[-1] - srt[-2] > 1e-3 * srt[-1]:
-            assert res[g]["bin"] == rg["bin"], g
-        if rg["metric"] > 1.01:
-            assert res[g]["code_phase"] == rg["code_phase"], g
+    if _is64(ctx):
+        print(f"[power rows] max |P - P_ref| / max P_ref = {worst:.3e}")
+        assert worst < F64_CLASS
 
 
 def test_small_search_vs_oracle(gpu, acq):
@@ -73,7 +121,7 @@ def test_small_search_vs_oracle(gpu, acq):
     gcode = np.array([2, 8, 0, 31])                    # PRNs 3, 9, 1, 32
     res, rows = ctx.search(IF, 2, freqs, gcode, gf)
     ref, ref_rows = A.acquire(IF, FS, codes, freqs, gf, group_code=gcode, return_rows=True)
-    _check_rows(res, rows, ref, ref_rows)
+    check_rows(res, rows, ref, ref_rows, _is64(ctx), label="small")
     assert res[0]["metric"] > 3 and res[1]["metric"] > 3
 
 
@@ -89,7 +137,7 @@ def test_cold_start_32x41_config2(gpu, acq):
     gf = np.tile(np.arange(41), (32, 1))
     res, rows = ctx.search(IF, 2, freqs, np.arange(32), gf)
     ref, ref_rows = A.acquire(IF, FS, codes[:32], freqs, gf, return_rows=True)
-    _check_rows(res, rows, ref, ref_rows)
+    check_rows(res, rows, ref, ref_rows, _is64(ctx), label="config2")
     for p in planted:
         assert res[p - 1]["metric"] > 2.5, p
         assert res[p - 1]["code_phase"] == ref[p - 1]["code_phase"]
@@ -105,7 +153,10 @@ def test_noncoherent_10ms(gpu, acq):
     res, rows = ctx.search(IF, 10, freqs, gcode, gf, mode=gpu.ACQ_NONCOHERENT)
     ref, ref_rows = A.acquire(IF, FS, codes, freqs, gf, group_code=gcode, n_blocks=10,
                               noncoherent=True, return_rows=True)
-    _check_rows(res, rows, ref, ref_rows)
+    for rr in ref_rows:          # the non-coherent rows carry no block choice
+        for r in rr:
+            r["block"] = -1
+    check_rows(res, rows, ref, ref_rows, _is64(ctx), label="noncoherent")
 
 
 def test_glonass_fch_search(gpu, acq):
@@ -123,7 +174,7 @@ def test_glonass_fch_search(gpu, acq):
     gcode = np.full(len(fchs), 32)
     res, rows = ctx.search(IF, 2, freqs, gcode, gf)
     ref, ref_rows = A.acquire(IF, FS, codes, freqs, gf, group_code=gcode, return_rows=True)
-    _check_rows(res, rows, ref, ref_rows)
+    check_rows(res, rows, ref, ref_rows, _is64(ctx), label="glonass")
     best = [int(fchs[i]) for i in np.argsort([-r["metric"] for r in res])[:2]]
     assert sorted(best) == [-3, 4]
 
@@ -135,3 +186,22 @@ def test_search_rejects_bad_tables(gpu, acq):
         ctx.search(IF, 2, np.array([2.42e6]), [99], [[0]])
     with pytest.raises(gpu.GnssCorrError):
         ctx.search(IF, 2, np.array([2.42e6]), [0], [[5]])
+
+
+def test_zero_if_rows(gpu, acq):
+    """An all-zero IF gives all-zero power rows: peak 0, argmax 0 (first index of the
+    maximum, as Scilab's max), metric 0/0 = nan like the reference's division."""
+    ctx, _ = acq
+    IF = np.zeros(4 * N, np.int8)
+    res, rows = ctx.search(IF, 2, A.gps_bins(2.42e6, 2), [0], [np.arange(5)])
+    assert np.all(rows["peak"] == 0.0) and np.all(rows["argmax"] == 0)
+    assert res[0]["code_phase"] == 1 and res[0]["bin"] == 0
+
+
+def test_bad_precision_or_size_rejected(gpu):
+    with pytest.raises(gpu.GnssCorrError):
+        gpu.AcqCtx(FS, N, precision=7)
+    with pytest.raises(gpu.GnssCorrError):
+        gpu.AcqCtx(16.0e6, 16000, precision=gpu.ACQ_F32)   # fp32 path: 16368 only
+    with pytest.raises(gpu.GnssCorrError):
+        gpu.AcqCtx(16.1e6, 16100)                           # no fp64 plan for this N
