@@ -4,11 +4,13 @@
 Primary line (`value`): acquisition cells/s on BASELINE config 2 -- a full
 32-PRN x 41-Doppler-bin cold-start search (acquisition.sci semantics: 1 ms
 coherent, two consecutive 1-ms blocks, keep the better), 16368 samples per
-code period.  A step = one complete search of one 2-ms IF record that is
-already resident in HBM (wipe-off + FFT of 82 rows, 2624 correlation
-IFFTs, peak/second-peak/metric for 32 PRNs).  Weak scaling: every rank runs
-its own search on its own record each step (PRN x Doppler cells shard with no
-exchange step: no collective on the data path).
+code period, computed in fp64 like the reference (Scilab doubles; parity
+~1e-12 relative, tests/test_acq_gpu.py).  A step = one complete search of one
+2-ms IF record that is already resident in HBM (classes, wipe-off + FFT of the
+class rows, 2624 correlation IFFTs, peak/second-peak/metric for 32 PRNs).
+Weak scaling: every rank runs its own search on its own record each step (PRN
+x Doppler cells shard with no exchange step: no collective on the data path).
+The fp32 fast path is reported beside it as `acquisition_f32`.
 
 Secondary object (`tracking`): 1-ms E/P/L correlations per second --
 256 receivers x 12 GP2021 channels (BASELINE config 3 scaled out), each
@@ -40,6 +42,7 @@ CELLS_PER_SEARCH = N_PRN * N_BINS * N          # 21,474,816 (SURVEY
 # IFFT 5*log2(N) + complex multiply 6 + |.|^2 3 + max 1  
 FLOP_PER_CELL_BLOCK = 5.0 * np.log2(N) + 6 + 3 + 1
 PEAK_FP32_TFLOPS = 157.3                       # MI355X_MICROARCH.md (vector == matrix f32)
+ACQ64_KERNEL = "acq64_corr_kernel<PlanA,0,false>"   # 16368 = 16 x 33 x 31, best-of-blocks
 PEAK_HBM_GBS = 8000.0
 PEAK_INT_TOPS = 78.6                           # 256 CU x 128 lanes x 2.4 GHz, 32-bit VALU
 TRACK_RX, TRACK_CH, TRACK_NS = 256, 12, 16368
@@ -58,6 +61,9 @@ class Dist:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
         if self.world > 1:
+            # bind libgnsscorr.so (and the ROCm runtime it was built against)
+            # before torch.distributed pulls in torch's own libamdhip64
+            gc.lib()
             import torch.distributed as td
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             td.init_process_group("gloo", rank=self.rank, world_size=self.world)
@@ -88,7 +94,7 @@ class Dist:
             self.td.destroy_process_group()
 
 
-def acq_setup(dev, rank):
+def acq_setup(dev, rank, precision=gc.ACQ_F64):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     rng = np.random.default_rng(100 + rank)
     planted = rng.choice(np.arange(1, 33), 8, replace=False)
@@ -97,7 +103,8 @@ def acq_setup(dev, rank):
     IF = gc.ifgen(N_BLK * N, sigs, fs=FS, seed=0x5EED0002 + rank)
     codes = np.stack([gc.sample_code(gc.ca_code(p), 1.023e6, FS, N) for p in range(1, 33)])
     freqs = 2.42e6 - 10000.0 + 500.0 * np.arange(N_BINS)           # acquisition.sci:101-104
-    ctx = gc.AcqCtx(FS, N, device=dev, max_freqs=N_BINS, max_blocks=N_BLK, max_codes=N_PRN)
+    ctx = gc.AcqCtx(FS, N, device=dev, max_freqs=N_BINS, max_blocks=N_BLK, max_codes=N_PRN,
+                    precision=precision)
     ctx.set_codes(codes)
     bufs = dict(
         d_if=gc.DevBuf.from_array(IF, dev), d_freqs=gc.DevBuf.from_array(freqs, dev),
@@ -112,15 +119,17 @@ def acq_step(ctx, b, ev=None):
     ctx.spectra_dev(b["d_if"].ptr, N_BLK, N_BINS, b["d_freqs"].ptr)
     if ev:
         ev[0].record(ctx.stream)
-    # correlation, then the per-PRN selection kernel (acquisition.sci:126-186)
-    ctx.correlate_dev(N_BLK, b["d_freqs"].ptr, N_PRN, N_BINS, b["d_gcode"].ptr, b["d_gfreq"].ptr,
-                      b["d_rows"].ptr, b["d_res"].ptr)
+    # the correlation kernel alone between the events (row statistics stay in
+    # the context), then the per-PRN selection kernel (acquisition.sci:126-186)
+    ctx.correlate_dev(N_BLK, b["d_freqs"].ptr, N_PRN, N_BINS, b["d_gcode"].ptr, b["d_gfreq"].ptr)
     if ev:
         ev[1].record(ctx.stream)
+    ctx.select_dev(N_PRN, N_BINS, b["d_freqs"].ptr, b["d_gfreq"].ptr, b["d_rows"].ptr,
+                   b["d_res"].ptr)
 
 
-def run_acq(dist, dev, steps, warmup):
-    ctx, b, meta = acq_setup(dev, dist.rank)
+def run_acq(dist, dev, steps, warmup, precision=gc.ACQ_F64):
+    ctx, b, meta = acq_setup(dev, dist.rank, precision)
     for _ in range(warmup):
         acq_step(ctx, b)
     ctx.sync()
@@ -617,13 +626,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-track", action="store_true")
     a = ap.parse_args()
+    gc.lib()           # the library binds its HIP runtime first (see Dist)
     dist = Dist()
     n_dev = gc.device_count()
     if n_dev < 1:
         raise SystemExit("bench.py: no HIP device visible")
     dev = dist.local % n_dev     # one rank per GPU; wraps only when rehearsing on fewer GPUs
 
-    acq = run_acq(dist, dev, a.steps, a.warmup)
+    acq = run_acq(dist, dev, a.steps, a.warmup, gc.ACQ_F64)
+    acq32 = None if a.skip_track else run_acq(dist, dev, a.steps, a.warmup, gc.ACQ_F32)
+    rank_info = dist.gather(dict(rank=dist.rank, device=dev, pci_bus_id=gc.pci_bus_id(dev),
+                                 hip_runtime=gc.hip_runtime_path()))
     trk = None if a.skip_track else run_track(dist, dev, max(a.steps, 20), a.warmup)
     sgt = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup)
     sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps // 5, 5), 2)
@@ -639,22 +652,39 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": W,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": acq["dt"] / a.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (deterministic 2-bit IQ with 8 planted GPS signals per rank)",
             "config": {"workload": "BASELINE config 2: 32-PRN x 41-bin cold-start acquisition, "
-                                   "1 ms coherent, 2 blocks (acquisition.sci), 16.368 Msps",
+                                   "1 ms coherent, 2 blocks (acquisition.sci), 16.368 Msps, "
+                                   "fp64 as the reference computes it",
                        "prns": N_PRN, "bins": N_BINS, "blocks": N_BLK, "samples_per_code": N,
                        "cells_per_search": CELLS_PER_SEARCH,
                        "parallelism": f"weak: one search per GPU per step x {W} GPUs"},
-            "roofline": {"bound": "valu", "kernel": "acq_corr_pipe_kernel", "achieved": achieved,
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_TFLOPS,
-                         "traffic": pmc_traffic("acq_corr_pipe_kernel"),
+            "roofline": {"bound": "valu", "kernel": ACQ64_KERNEL, "achieved": achieved,
+                         "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
+                         "frac": achieved / PEAK_FP64_TFLOPS,
+                         "traffic": pmc_traffic(ACQ64_KERNEL),
                          "kernel_ms_per_launch": acq["corr_ms"],
                          "flop_per_launch": flop_launch},
             "search_latency_ms": acq["dt"] / a.steps * 1e3,
             "planted_found": f"{acq['found']}/{acq['n_planted']}",
+            "ranks": rank_info,
         }
+        if acq32:
+            a32 = flop_launch / (acq32["corr_ms"] * 1e-3) / 1e12
+            out["acquisition_f32"] = {
+                "metric": "acquisition cells/sec (config 2, single-precision fast path)",
+                "value": cells / acq32["dt"], "unit": "cells/s", "dtype": "f32",
+                "ms_per_step": acq32["dt"] / a.steps * 1e3,
+                "note": "rows within 2e-5 of the row max of fp64 (tests/test_acq_gpu.py[f32]); "
+                        "not the reference's precision",
+                "roofline": {"bound": "valu", "kernel": "acq_corr_pipe_kernel", "achieved": a32,
+                             "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s (fp32)",
+                             "frac": a32 / PEAK_FP32_TFLOPS,
+                             "traffic": pmc_traffic("acq_corr_pipe_kernel"),
+                             "kernel_ms_per_launch": acq32["corr_ms"]},
+                "planted_found": f"{acq32['found']}/{acq32['n_planted']}",
+            }
         if trk:
             C = trk["channels"]
             steps_t = max(a.steps, 20)

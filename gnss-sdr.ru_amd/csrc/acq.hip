@@ -1197,6 +1197,7 @@ __device__ void select_group(int g, int lane, const gnsscorr_acq_row* __restrict
     // 1 if an exact tie put the global first column in another row than the
     // winning row's own argmax (second peak then centred on the row's argmax)
     o.pad = cp != rb.argmax;
+    o.pad2 = 0;
     o.carr_freq = freqs[group_freq[(long)g * n_bins + bin]];
     res[g] = o;
   }

@@ -56,6 +56,12 @@
     }                                                                                   \
   } while (0)
 
+// Diagnostic hook: tools/acq64_stamps.hip defines ACQ64_STAMP(i) to record
+// s_memtime at the barriers of the correlation kernel; nothing in the library.
+#ifndef ACQ64_STAMP
+#define ACQ64_STAMP(i)
+#endif
+
 namespace {
 
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -300,11 +306,50 @@ struct Plan {
   static_assert(L * R3 <= T, "leftover stage-3 outputs must fit one per thread");
   static_assert(!PFA || (cgcd(R1, R2) == 1 && cgcd(R1, R3) == 1 && cgcd(R2, R3) == 1),
                 "PFA needs coprime factors");
+  // Code spectra are spectra of real sequences, F[-k] = conj(F[k]).  In PFA
+  // digits negation is digit-wise, so with two stage-1 groups per thread a
+  // thread can own a group and its negative and load F once for both:
+  // SYM plans pair the 1023 radix-16 groups as (g, -g) -- 511 pairs + group 0.
+  static constexpr bool SYM = PFA && K1 == 2 && R2 == 33 && R3 == 31 && T == 512;
+  // stage-3 group of main slot j of thread t.  CT plans with several groups
+  // per thread give a thread groups (k1, k2 + j R2/K3) so that ALL its outputs
+  // (natural k1 + R1 k2 + R1 R2 k3) lie at least N/(R3 K3) apart.
+  __device__ static __forceinline__ int group3(int t, int j) {
+    if constexpr (!PFA && K3 > 1 && L == 0 && R2 % K3 == 0 && T == R1 * (R2 / K3)) {
+      constexpr int W = R2 / K3;
+      return (t / W) * R2 + t % W + W * j;
+    } else {
+      return t + j * T;
+    }
+  }
+  // a thread's main stage-3 outputs are at least this far apart (circularly):
+  // any window of fewer samples holds at most one of them
+  static constexpr int SPACING =
+      (!PFA && K3 > 1 && L == 0 && R2 % K3 == 0 && T == R1 * (R2 / K3)) ? N / (R3 * K3)
+                                                                      : (K3 == 1 ? N / R3 : 1);
+  // stage-1 group of slot j of thread t (SYM: the pair (g, -g)), -1 if none
+  __device__ static __forceinline__ int group1(int t, int j) {
+    if constexpr (SYM) {
+      int g;
+      if (t < 495) g = (t / 15) * R3 + 1 + t % 15;    // n3 = 1..15, every n2
+      else if (t < 511) g = (t - 494) * R3;           // n3 = 0, n2 = 1..16
+      else g = t == 511 ? 0 : -1;                     // group 0 pairs with itself
+      if (j == 0 || g <= 0) return j == 0 ? g : -1;
+      const int n2 = g / R3, n3 = g % R3;
+      return ((R2 - n2) % R2) * R3 + (R3 - n3) % R3;
+    } else {
+      const int g = t + j * T;
+      return (t < T && g < G1) ? g : -1;
+    }
+  }
   // natural input index of stage-1 element (n1, g)
   __device__ static __forceinline__ int in_index(int n1, int g) {
     if constexpr (PFA) {
       const int n2 = g / R3, n3 = g % R3;
-      return (int)(((long)n1 * Q1 + (long)n2 * Q2 + (long)n3 * Q3) % N);
+      int n = n1 * Q1 + n2 * Q2;          // < 2N
+      n -= n >= N ? N : 0;
+      n += n3 * Q3;                        // < 2N
+      return n >= N ? n - N : n;
     } else {
       return n1 * G1 + g;
     }
@@ -313,13 +358,22 @@ struct Plan {
   __device__ static __forceinline__ void out_base(int g3, int& base, int& step) {
     const int k1 = g3 / R2, k2 = g3 % R2;
     if constexpr (PFA) {
-      base = (int)(((long)k1 * E1 + (long)k2 * E2) % N);
+      base = (k1 * E1 + k2 * E2) % N;      // < R1*N + R2*N < 2^31
       step = E3;
     } else {
       base = k1 + R1 * k2;
       step = R1 * R2;
     }
   }
+  // storage position of stage-3 output k3 of group g3: sbase(g3) + soff(k3).
+  // PFA: the natural index k = CRT(k1, k2, k3) has k mod R_i = k_i, so its
+  // storage digits are k_i * INV_i mod R_i -- no division per value.
+  __device__ static __forceinline__ int sbase(int g3) {
+    const int k1 = g3 / R2, k2 = g3 % R2;
+    if constexpr (PFA) return (k1 * INV1 % R1) * G1 + (k2 * INV2 % R2) * R3;
+    else return k1 + R1 * k2;
+  }
+  static constexpr int soff(int k3) { return PFA ? (k3 * INV3 % R3) : R1 * R2 * k3; }
   // storage position of natural index k in a spectrum row
   __device__ static __forceinline__ int store_index(int k) {
     if constexpr (PFA) {
@@ -330,6 +384,7 @@ struct Plan {
     }
   }
 };
+static_assert((long)16 * 15345 + (long)33 * 16368 < (1L << 31), "int index maps");
 
 typedef Plan<16368, 16, 33, 31, 512, true> PlanA;   // 16.368 Msps
 typedef Plan<16000, 40, 40, 10, 400, false> PlanB;  // 16 Msps
@@ -364,11 +419,14 @@ __device__ __forceinline__ void set_part(v2d& v, int p, double d) {
 // outputs v3 (main groups g3 = t + j*T) and vl (leftover output t < L*R3:
 // slot t % R3 of group K3*T + t / R3).  lds: N doubles; side: LS complex;
 // tw3: W_R3^q, q < R3 (LDS); twN: W_N^j (global, CT plans only).
-template <class P>
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <class P, class Hook = NoHook>
 __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
                                          const v2d* __restrict__ twN, int t,
                                          v2d (&v1)[P::K1][P::R1], v2d (&v3)[P::K3][P::R3],
-                                         v2d& vl) {
+                                         v2d& vl, const Hook& before_exchange = Hook()) {
   constexpr int R1 = P::R1, R2 = P::R2, R3 = P::R3, T = P::T, G1 = P::G1, G2 = P::G2;
   const bool act = t < T;
   // ---- stage 1
@@ -376,23 +434,25 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
   for (int j = 0; j < P::K1; j++) {
     dft<R1>(v1[j]);
     if constexpr (!P::PFA) {
-      const int g = t + j * T;
-      if (act && g < G1) twiddle_run<R1>(v1[j], twN[g]);
+      const int g = P::group1(t, j);
+      if (g >= 0) twiddle_run<R1>(v1[j], twN[g]);
     }
   }
+  before_exchange();   // the caller may still use the LDS up to here
   // ---- exchange 1: re then im
   v2d v2[P::K2][R2];
 #pragma unroll
   for (int p = 0; p < 2; p++) {
 #pragma unroll
     for (int j = 0; j < P::K1; j++) {
-      const int g = t + j * T;
-      if (act && g < G1) {
+      const int g = P::group1(t, j);
+      if (g >= 0) {
 #pragma unroll
         for (int k1 = 0; k1 < R1; k1++) lds[k1 * G1 + g] = part(v1[j][k1], p);
       }
     }
     __syncthreads();
+    ACQ64_STAMP(1 + 2 * p);
 #pragma unroll
     for (int j = 0; j < P::K2; j++) {
       const int g2 = t + j * T;
@@ -400,12 +460,10 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
         const int base = (g2 / R3) * G1 + g2 % R3;
 #pragma unroll
         for (int n2 = 0; n2 < R2; n2++) set_part(v2[j][n2], p, lds[base + n2 * R3]);
-      } else {
-#pragma unroll
-        for (int n2 = 0; n2 < R2; n2++) set_part(v2[j][n2], p, 0.0);
       }
     }
     __syncthreads();
+    ACQ64_STAMP(2 + 2 * p);
   }
   // ---- stage 2
 #pragma unroll
@@ -429,9 +487,10 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       }
     }
     __syncthreads();
+    ACQ64_STAMP(5 + 2 * p);
 #pragma unroll
     for (int j = 0; j < P::K3; j++) {
-      const int g3 = act ? t + j * T : 0;
+      const int g3 = act ? P::group3(t, j) : 0;
 #pragma unroll
       for (int n3 = 0; n3 < R3; n3++) set_part(v3[j][n3], p, lds[g3 * R3 + n3]);
     }
@@ -440,6 +499,7 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       if (p == 1 && t < P::L * R3) side[t] = vl;
     }
     __syncthreads();
+    ACQ64_STAMP(6 + 2 * p);
   }
   // ---- stage 3
 #pragma unroll
@@ -501,15 +561,67 @@ __device__ __forceinline__ double block_max0(double v, double* sm) {
 }
 
 // ---- forward transforms ------------------------------------------------------------
+// Inputs are written in the plan's storage order (element n at store_index(n)),
+// so the forward FFT reads its stage-1 groups with coalesced loads at constant
+// offsets, exactly like the correlation kernel reads the spectra.
 // IF rows: x[n] = sum_{p<coh} IF[blk][n + pN] * exp(i f ((n+pN)*2)*pi*ts), evaluated as
 // acquisition.sci:61-62,107 does (phasePoints = (0:L-1)*2*%pi*ts; exp(%i*f*phasePoints))
-// at the class frequency f = cfreq[cls]; row = cls * n_blocks + blk.
-__global__ __launch_bounds__(256) void acq64_wipe_kernel(const int8_t* __restrict__ src, int iq,
-                                                         int n_blocks, int coh,
-                                                         const double* __restrict__ cfreq,
-                                                         const int* __restrict__ n_cls_dev,
-                                                         double ts, int N, v2d* __restrict__ out) {
-  const long total = (long)(*n_cls_dev) * n_blocks * N;
+// at the class frequency f = cfreq[cls]; row = cls * n_blocks + blk.  With
+// fuse_n > 0 (short frequency tables) every workgroup first classifies the
+// table itself (acq64_classify_kernel's job) and workgroup 0 publishes it.
+constexpr int kFuseClass = 64;
+__device__ __forceinline__ double grid_residue(double f, double delta) {
+  double r = fmod(f, delta);
+  return r < 0 ? r + delta : r;
+}
+template <class P>
+__global__ __launch_bounds__(256) void acq64_wipe_kernel(
+    const int8_t* __restrict__ src, int iq, int n_blocks, int coh, const double* __restrict__ cfreq_in,
+    const int* __restrict__ n_cls_dev, double ts, v2d* __restrict__ out, int fuse_n,
+    const double* __restrict__ freqs, double delta, int2* __restrict__ fmap_out,
+    double* __restrict__ cfreq_out, int* __restrict__ nclass_out) {
+  constexpr int N = P::N;
+  __shared__ double s_r[kFuseClass], s_cf[kFuseClass];
+  __shared__ int s_l[kFuseClass], s_nc;
+  const double* cfreq = cfreq_in;
+  int n_cls;
+  if (fuse_n > 0) {
+    const int t = threadIdx.x;
+    if (t < fuse_n) s_r[t] = grid_residue(freqs[t], delta);
+    __syncthreads();
+    if (t < fuse_n) {
+      int l = t;
+      for (int j = 0; j < t; j++)
+        if (s_r[j] == s_r[t]) { l = j; break; }
+      s_l[t] = l;
+    }
+    __syncthreads();
+    if (t < fuse_n) {
+      const int l = s_l[t];
+      int cls = 0;
+      for (int k = 0; k < l; k++) cls += s_l[k] == k;
+      if (l == t) s_cf[cls] = s_r[t];
+      if (blockIdx.x == 0) {
+        const double q = rint((freqs[t] - s_r[t]) / delta);
+        int mN = fabs(q) < 1e9 ? (int)fmod(q, (double)N) : 0;
+        mN += mN < 0 ? N : 0;
+        fmap_out[t] = make_int2(cls, mN);
+        if (l == t) cfreq_out[cls] = s_r[t];
+      }
+    }
+    if (t == 0) {
+      int cnt = 0;
+      for (int k = 0; k < fuse_n; k++) cnt += s_l[k] == k;
+      s_nc = cnt;
+      if (blockIdx.x == 0) *nclass_out = cnt;
+    }
+    __syncthreads();
+    n_cls = s_nc;
+    cfreq = s_cf;
+  } else {
+    n_cls = *n_cls_dev;
+  }
+  const long total = (long)n_cls * n_blocks * N;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const int row = (int)(i / N), n = (int)(i % N);
@@ -527,17 +639,18 @@ __global__ __launch_bounds__(256) void acq64_wipe_kernel(const int8_t* __restric
       re += I * cs - Q * sn;
       im += I * sn + Q * cs;
     }
-    out[i] = (v2d){re, im};
+    out[(long)row * N + P::store_index(n)] = (v2d){re, im};
   }
 }
 
+template <class P>
 __global__ __launch_bounds__(256) void acq64_codes_kernel(const int8_t* __restrict__ codes,
                                                           long n, v2d* __restrict__ out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (v2d){(double)codes[i], 0.0};
+  if (i < n) out[i - i % P::N + P::store_index((int)(i % P::N))] = (v2d){(double)codes[i], 0.0};
 }
 
-// Natural-order complex rows -> spectra in the plan's storage order.
+// Rows in storage order -> spectra in storage order.
 template <class P>
 __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict__ in,
                                                           const int* __restrict__ n_cls_dev,
@@ -549,17 +662,18 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
   __shared__ v2d tw3[P::R3];
   const int t = threadIdx.x;
   init_tw3<P>(tw3);
+  // one row per workgroup; the grid is an upper bound of the rows
   const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
-  for (int w = blockIdx.x; w < rows; w += gridDim.x) {
+  const int w = blockIdx.x;
+  if (w >= rows) return;
+  {
     const v2d* src = in + (long)w * P::N;
     v2d v1[P::K1][P::R1];
 #pragma unroll
     for (int j = 0; j < P::K1; j++) {
-      const int g = t + j * P::T;
-      const bool ok = t < P::T && g < P::G1;
+      const int g0 = P::group1(t, j), g = g0 < 0 ? 0 : g0;
 #pragma unroll
-      for (int n1 = 0; n1 < P::R1; n1++)
-        v1[j][n1] = ok ? src[P::in_index(n1, g)] : (v2d){0.0, 0.0};
+      for (int n1 = 0; n1 < P::R1; n1++) v1[j][n1] = src[n1 * P::G1 + g];
     }
     v2d v3[P::K3][P::R3], vl = (v2d){0.0, 0.0};
     fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl);
@@ -567,23 +681,16 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
     if (t < P::T) {
 #pragma unroll
       for (int j = 0; j < P::K3; j++) {
-        int base, step;
-        P::out_base(t + j * P::T, base, step);
-        int k = base;
+        const int sb = P::sbase(P::group3(t, j));
 #pragma unroll
-        for (int k3 = 0; k3 < P::R3; k3++) {
-          o[P::store_index(k)] = v3[j][k3];
-          k += step;
-          if (k >= P::N) k -= P::N;
-        }
+        for (int k3 = 0; k3 < P::R3; k3++) o[sb + P::soff(k3)] = v3[j][k3];
       }
     }
     if constexpr (P::L > 0) {
       if (t < P::L * P::R3) {
         int base, step;
         P::out_base(P::K3 * P::T + t / P::R3, base, step);
-        const int k = (int)((base + (long)(t % P::R3) * step) % P::N);
-        o[P::store_index(k)] = vl;
+        o[P::store_index((base + (t % P::R3) * step) % P::N)] = vl;
       }
     }
   }
@@ -609,6 +716,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   const int t = threadIdx.x;
   const bool act = t < T;
   init_tw3<P>(tw3);
+  ACQ64_STAMP(0);
   const int unit = order[blockIdx.x];
   const int rowid = kNC ? unit : unit / n_blocks;
   const int blk0 = kNC ? 0 : unit % n_blocks;
@@ -618,55 +726,96 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   const int2 fm = fmap[group_freq[g * n_bins + bin]];
   const int m = fm.y;
   const double inv_n2 = 1.0 / ((double)N * (double)N);
-  const v2d* Fc = F + (long)code * rs;
+  const v2d* Fc0 = F + (long)code * rs;
 
   double pw[K3][R3], pwl = -1.0;
-#pragma unroll
-  for (int j = 0; j < K3; j++)
-#pragma unroll
-    for (int k = 0; k < R3; k++) pw[j][k] = 0.0;
-  if constexpr (kNC) pwl = 0.0;
 
   for (int i = 0; i < nblk; i++) {
     const int blk = blk0 + i;
     const v2d* Xb = X + ((long)fm.x * n_blocks + blk) * rs;
-    // stage-1 inputs: conj(X[k - m]) * F[k]  (= conj(X * conj(F)), acquisition.sci:116)
+    // the code row is the same for every block: keep the compiler from
+    // hoisting its loads out of the block loop (they would stay live in
+    // registers across the whole transform)
+    const v2d* Fc = Fc0;
+    asm volatile("" : "+s"(Fc));
+    // likewise every thread-dependent address: t is opaque per block, so the
+    // index arithmetic is redone per block instead of held across it
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    // stage-1 inputs: conj(X[k - m]) * F[k]  (= conj(X * conj(F)), acquisition.sci:116).
+    // Slots of groups a thread does not own are left as garbage: fft_core never
+    // stores them.
     v2d v1[P::K1][R1];
-#pragma unroll
-    for (int j = 0; j < P::K1; j++) {
-      const int gg0 = t + j * T;
-      const bool ok = act && gg0 < P::G1;
-      const int gg = ok ? gg0 : 0;
-      if constexpr (P::PFA) {
-        constexpr int R2 = P::R2;
-        const int m1 = (m % R1) * P::INV1 % R1, m2 = (m % R2) * P::INV2 % R2,
-                  m3 = (m % R3) * P::INV3 % R3;
-        int n2 = gg / R3 - m2, n3 = gg % R3 - m3;
+    if constexpr (P::PFA) {
+      constexpr int R2 = P::R2;
+      // digits of the shift: X_f[k] = X_r[k - m], negation of m digit-wise
+      const int m1 = (m % R1) * P::INV1 % R1, m2 = (m % R2) * P::INV2 % R2,
+                m3 = (m % R3) * P::INV3 % R3;
+      auto shifted = [&](int g) {
+        int n2 = g / R3 - m2, n3 = g % R3 - m3;
         n2 += n2 < 0 ? R2 : 0;
         n3 += n3 < 0 ? R3 : 0;
-        const int gs = n2 * R3 + n3;
+        return n2 * R3 + n3;
+      };
+      auto plane = [&](int n1) {
+        int a = n1 - m1;
+        return (a < 0 ? a + R1 : a) * P::G1;
+      };
+      if constexpr (P::SYM) {
+        // slot 0: group ga; slot 1: gb = -ga, whose code value at plane -n1 is
+        // conj(F[ga] at plane n1): one F load serves both
+        const int ga0 = P::group1(t, 0), ga = ga0 < 0 ? 0 : ga0;
+        const int gb0 = P::group1(t, 1), gb = gb0 < 0 ? ga : gb0;
+        const int sa = shifted(ga), sb = shifted(gb);
 #pragma unroll
         for (int n1 = 0; n1 < R1; n1++) {
-          int n1s = n1 - m1;
-          n1s += n1s < 0 ? R1 : 0;
-          const v2d x = Xb[n1s * P::G1 + gs], f = Fc[n1 * P::G1 + gg];
-          v1[j][n1] = ok ? (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))}
-                         : (v2d){0.0, 0.0};
+          const int nn = (R1 - n1) % R1;
+          const v2d f = Fc[n1 * P::G1 + ga];
+          const v2d xa = Xb[plane(n1) + sa], xb = Xb[plane(nn) + sb];
+          v1[0][n1] = (v2d){fma(xa.x, f.x, xa.y * f.y), fma(xa.x, f.y, -(xa.y * f.x))};
+          v1[1][nn] = (v2d){fma(xb.x, f.x, -(xb.y * f.y)), -fma(xb.x, f.y, xb.y * f.x)};
         }
       } else {
 #pragma unroll
+        for (int j = 0; j < P::K1; j++) {
+          const int g0 = P::group1(t, j), g = g0 < 0 ? 0 : g0;
+          const int gs = shifted(g);
+#pragma unroll
+          for (int n1 = 0; n1 < R1; n1++) {
+            const v2d x = Xb[plane(n1) + gs], f = Fc[n1 * P::G1 + g];
+            v1[j][n1] = (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))};
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < P::K1; j++) {
+        const int g0 = P::group1(t, j), g = g0 < 0 ? 0 : g0;
+#pragma unroll
         for (int n1 = 0; n1 < R1; n1++) {
-          const int n = n1 * P::G1 + gg;
+          const int n = n1 * P::G1 + g;
           int s = n - m;
           s += s < 0 ? N : 0;
           const v2d x = Xb[s], f = Fc[n];
-          v1[j][n1] = ok ? (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))}
-                         : (v2d){0.0, 0.0};
+          v1[j][n1] = (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))};
         }
       }
     }
     v2d v3[K3][R3], vl = (v2d){0.0, 0.0};
-    fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl);
+    // non-coherent: the running sums start at zero in the first block (the
+    // compiler spills them around the load phase, where registers are scarcest)
+    auto start_sums = [&]() {
+      if constexpr (kNC) {
+        if (i == 0) {
+#pragma unroll
+          for (int j = 0; j < K3; j++)
+#pragma unroll
+            for (int k = 0; k < R3; k++) pw[j][k] = 0.0;
+          pwl = 0.0;
+        }
+      }
+    };
+    fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl, start_sums);
     // |.|^2 / N^2 (|ifft(Y)|^2 = |fft(conj Y)|^2 / N^2)
 #pragma unroll
     for (int j = 0; j < K3; j++)
@@ -685,7 +834,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
 #pragma unroll
       for (int j = 0; j < K3; j++) {
         int base, step;
-        P::out_base(t + j * T, base, step);
+        P::out_base(P::group3(t, j), base, step);
         int k = base;
 #pragma unroll
         for (int k3 = 0; k3 < R3; k3++) {
@@ -698,38 +847,53 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
         if (t < L * R3) {
           int base, step;
           P::out_base(K3 * T + t / R3, base, step);
-          dump[(long)rowid * N + (int)((base + (long)(t % R3) * step) % N)] = pwl;
+          dump[(long)rowid * N + (base + (t % R3) * step) % N] = pwl;
         }
       }
     }
+
   }
-  // ---- row statistics (exact, two passes over the registers)
-  double bv = -1.0;
-  int bk = INT_MAX;
-  if (act) {
+  // ---- row statistics.  Per stage-3 group, the thread's outputs lie
+  // SPACING = N/R3 samples apart, so an exclusion window narrower than that
+  // holds at most one of them: a per-group top-2 (max with the first natural
+  // index of an exact tie, and the runner-up) gives the largest value outside
+  // the window in one pass.  Wider windows (spc > SPACING/2) take an exact
+  // second pass over the registers.
+  auto wrap_add = [](int k, int d) {   // (k + d) mod N for k, d in [0, N)
+    const unsigned u = (unsigned)(k + d);
+    return (int)min(u, u - (unsigned)N);
+  };
+  double a1 = -1.0, a2 = -1.0;
+  int ak = INT_MAX;
 #pragma unroll
-    for (int j = 0; j < K3; j++) {
-      int base, step;
-      P::out_base(t + j * T, base, step);
-      int k = base;
+  for (int j = 0; j < K3; j++) {
+    int base, step;
+    P::out_base(act ? P::group3(t, j) : 0, base, step);
+    int k = base;
 #pragma unroll
-      for (int k3 = 0; k3 < R3; k3++) {
-        if (better(pw[j][k3], k, bv, bk)) { bv = pw[j][k3]; bk = k; }
-        k += step;
-        if (k >= N) k -= N;
-      }
+    for (int k3 = 0; k3 < R3; k3++) {
+      const double v = pw[j][k3];
+      const bool take = v > a1 || (v == a1 && k < ak);
+      a2 = fmax(a2, fmin(a1, v));
+      ak = take ? k : ak;
+      a1 = fmax(a1, v);
+      k = wrap_add(k, step);
     }
   }
+  if (!act) { a1 = -1.0; a2 = -1.0; ak = INT_MAX; }
+  double bv = a1;
+  int bk = ak;
   int kl = INT_MAX;
   if constexpr (L > 0) {
     if (t < L * R3) {
       int base, step;
       P::out_base(K3 * T + t / R3, base, step);
-      kl = (int)((base + (long)(t % R3) * step) % N);
+      kl = (base + (t % R3) * step) % N;
       if (better(pwl, kl, bv, bk)) { bv = pwl; bk = kl; }
     }
   }
   block_argmax<P::NW>(bv, bk, s_v, s_k);
+  ACQ64_STAMP(9);
   // second peak: max outside the open circular window (bk - spc, bk + spc)
   auto outside = [&](int k) {
     int d = k - bk;
@@ -737,17 +901,18 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     return d >= spc && d <= N - spc;
   };
   double sv = -1.0;
-  if (act) {
+  if (2 * spc - 1 <= P::SPACING) {
+    sv = outside(ak) ? a1 : a2;
+  } else if (act) {
 #pragma unroll
     for (int j = 0; j < K3; j++) {
       int base, step;
-      P::out_base(t + j * T, base, step);
+      P::out_base(P::group3(t, j), base, step);
       int k = base;
 #pragma unroll
       for (int k3 = 0; k3 < R3; k3++) {
         if (outside(k)) sv = fmax(sv, pw[j][k3]);
-        k += step;
-        if (k >= N) k -= N;
+        k = wrap_add(k, step);
       }
     }
   }
@@ -755,6 +920,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     if (t < L * R3 && outside(kl)) sv = fmax(sv, pwl);
   }
   sv = block_max0<P::NW>(sv, s_m);
+  ACQ64_STAMP(10);
   if (t == 0) {
     gnsscorr_acq_row r;
     r.peak = bv;
@@ -768,10 +934,6 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
 // Frequencies -> spectrum classes on the fs/N grid: class = canonical residue
 // r = f mod fs/N (one forward FFT per class and block); bin f = r + m fs/N
 // reads the class spectrum shifted by m.  fmap[i] = {class, m mod N}.
-__device__ __forceinline__ double grid_residue(double f, double delta) {
-  double r = fmod(f, delta);
-  return r < 0 ? r + delta : r;
-}
 __global__ __launch_bounds__(1024) void acq64_classify_kernel(const double* __restrict__ freqs,
                                                               int n, double delta, int N,
                                                               int2* __restrict__ fmap,
@@ -810,8 +972,7 @@ __global__ __launch_bounds__(1024) void acq64_classify_kernel(const double* __re
 template <class P>
 int fwd_launch(gnsscorr_acq_ctx* c, const v2d* in, const int* n_cls_dev, int per_cls,
                int n_rows, v2d* out) {
-  const int grid = n_rows < 1024 ? n_rows : 1024;
-  hipLaunchKernelGGL((acq64_fwd_kernel<P>), dim3(grid), dim3(P::TB), 0, c->stream, in, n_cls_dev,
+  hipLaunchKernelGGL((acq64_fwd_kernel<P>), dim3(n_rows), dim3(P::TB), 0, c->stream, in, n_cls_dev,
                      per_cls, n_rows, out, c->rs64, (const v2d*)c->d_twN);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
@@ -821,6 +982,7 @@ template <class P>
 int corr_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_units, int n_bins,
                 const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
                 int dump_block) {
+
 #define ACQ64_LAUNCH(M, D)                                                                  \
   hipLaunchKernelGGL((acq64_corr_kernel<P, M, D>), dim3(n_units), dim3(P::TB), 0, c->stream, \
                      (const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, d_gcode,   \
@@ -880,42 +1042,59 @@ void acq64_free(gnsscorr_acq_ctx* c) {
   c->d_lead64 = nullptr;
 }
 
-int acq64_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
-  const int N = c->cfg.n_samples;
-  int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)n_codes * N, sizeof(double2));
-  if (rc) return rc;
-  const long n = (long)n_codes * N;
-  hipLaunchKernelGGL(acq64_codes_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, d_codes,
-                     n, (v2d*)c->d_in64);
+namespace {
+
+template <class P>
+int set_codes_launch(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
+  const long n = (long)n_codes * P::N;
+  hipLaunchKernelGGL(acq64_codes_kernel<P>, dim3((n + 255) / 256), dim3(256), 0, c->stream,
+                     d_codes, n, (v2d*)c->d_in64);
   HIP_TRY(hipGetLastError());
-  return c->plan64 == 1
-             ? fwd_launch<PlanA>(c, (const v2d*)c->d_in64, nullptr, 1, n_codes, (v2d*)c->d_F64)
-             : fwd_launch<PlanB>(c, (const v2d*)c->d_in64, nullptr, 1, n_codes, (v2d*)c->d_F64);
+  return fwd_launch<P>(c, (const v2d*)c->d_in64, nullptr, 1, n_codes, (v2d*)c->d_F64);
+}
+
+template <class P>
+int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int n_freqs,
+                   const double* d_freqs) {
+  constexpr int N = P::N;
+  const int rows = n_freqs * n_blocks;   // upper bound: classes <= frequencies
+  const double delta = c->cfg.samp_rate / N;
+  const int fuse = n_freqs <= kFuseClass ? n_freqs : 0;
+  if (!fuse) {
+    hipLaunchKernelGGL(acq64_classify_kernel, dim3(1), dim3(1024), 0, c->stream, d_freqs,
+                       n_freqs, delta, N, c->d_fmap64, c->d_cfreq, c->d_nclass, c->d_resid,
+                       c->d_lead64);
+    HIP_TRY(hipGetLastError());
+  }
+  const long work = (long)rows * N;
+  const int grid = (int)((work + 255) / 256 < 2048 ? (work + 255) / 256 : 2048);
+  hipLaunchKernelGGL(acq64_wipe_kernel<P>, dim3(grid), dim3(256), 0, c->stream, d_if, iq,
+                     n_blocks, c->coh, c->d_cfreq, c->d_nclass, 1.0 / c->cfg.samp_rate,
+                     (v2d*)c->d_in64, fuse, d_freqs, delta, c->d_fmap64, c->d_cfreq,
+                     c->d_nclass);
+  HIP_TRY(hipGetLastError());
+  return fwd_launch<P>(c, (const v2d*)c->d_in64, c->d_nclass, n_blocks, rows, (v2d*)c->d_X64);
+}
+
+}  // namespace
+
+int acq64_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
+  int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)n_codes * c->cfg.n_samples,
+                    sizeof(double2));
+  if (rc) return rc;
+  return c->plan64 == 1 ? set_codes_launch<PlanA>(c, d_codes, n_codes)
+                        : set_codes_launch<PlanB>(c, d_codes, n_codes);
 }
 
 int acq64_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int n_freqs,
                   const double* d_freqs) {
-  const int N = c->cfg.n_samples;
-  const int rows = n_freqs * n_blocks;   // upper bound: classes <= frequencies
-  int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)rows * N, sizeof(double2));
+  const size_t rows = (size_t)n_freqs * n_blocks;
+  int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, rows * c->cfg.n_samples, sizeof(double2));
   if (rc) return rc;
-  rc = acq_grow((void**)&c->d_X64, &c->cap_X64, (size_t)rows * c->rs64, sizeof(double2));
+  rc = acq_grow((void**)&c->d_X64, &c->cap_X64, rows * c->rs64, sizeof(double2));
   if (rc) return rc;
-  hipLaunchKernelGGL(acq64_classify_kernel, dim3(1), dim3(1024), 0, c->stream, d_freqs, n_freqs,
-                     c->cfg.samp_rate / N, N, c->d_fmap64, c->d_cfreq, c->d_nclass, c->d_resid,
-                     c->d_lead64);
-  HIP_TRY(hipGetLastError());
-  const long work = (long)rows * N;
-  const int grid = (int)((work + 255) / 256 < 8192 ? (work + 255) / 256 : 8192);
-  hipLaunchKernelGGL(acq64_wipe_kernel, dim3(grid), dim3(256), 0, c->stream, d_if, iq, n_blocks,
-                     c->coh, c->d_cfreq, c->d_nclass, 1.0 / c->cfg.samp_rate, N,
-                     (v2d*)c->d_in64);
-  HIP_TRY(hipGetLastError());
-  return c->plan64 == 1
-             ? fwd_launch<PlanA>(c, (const v2d*)c->d_in64, c->d_nclass, n_blocks, rows,
-                                 (v2d*)c->d_X64)
-             : fwd_launch<PlanB>(c, (const v2d*)c->d_in64, c->d_nclass, n_blocks, rows,
-                                 (v2d*)c->d_X64);
+  return c->plan64 == 1 ? spectra_launch<PlanA>(c, d_if, iq, n_blocks, n_freqs, d_freqs)
+                        : spectra_launch<PlanB>(c, d_if, iq, n_blocks, n_freqs, d_freqs);
 }
 
 int acq64_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,

@@ -14,6 +14,12 @@
     }                                                                                   \
   } while (0)
 
+extern "C" int gnsscorr_device_pci_bus_id(int device, char* buf, int len) {
+  if (!buf || len < 13) return GNSSCORR_EINVAL;
+  HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
+  return GNSSCORR_OK;
+}
+
 extern "C" int gnsscorr_dev_alloc(int device, size_t bytes, void** d_ptr) {
   if (!d_ptr || bytes == 0) return GNSSCORR_EINVAL;
   HIP_TRY(hipSetDevice(device));

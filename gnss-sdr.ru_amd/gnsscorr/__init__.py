@@ -150,6 +150,7 @@ class SdrAcqCfg(C.Structure):
 # every symbol include/gnsscorr.h + include/gnsscorr_osg.h declare
 EXPORTED_FUNCTIONS = [
     "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
+    "gnsscorr_device_pci_bus_id",
     "gnsscorr_track_create", "gnsscorr_track_destroy", "gnsscorr_track_max_dumps",
     "gnsscorr_track", "gnsscorr_track_dev", "gnsscorr_track_next_tic",
     "gnsscorr_track_replay_dev", "gnsscorr_track_get_state", "gnsscorr_track_set_state",
@@ -204,6 +205,7 @@ def lib() -> C.CDLL:
         "gnsscorr_last_error": (C.c_char_p, []),
         "gnsscorr_version": (C.c_char_p, []),
         "gnsscorr_device_count": (I, []),
+        "gnsscorr_device_pci_bus_id": (I, [I, P, I]),
         "gnsscorr_track_create": (I, [C.POINTER(P), C.POINTER(TrackCfg)]),
         "gnsscorr_track_destroy": (I, [P]),
         "gnsscorr_track_max_dumps": (I, [P]),
@@ -310,6 +312,24 @@ def _ptr(a: np.ndarray) -> int:
 
 def device_count() -> int:
     return int(lib().gnsscorr_device_count())
+
+
+def pci_bus_id(device: int = 0) -> str:
+    buf = C.create_string_buffer(64)
+    _check(lib().gnsscorr_device_pci_bus_id(device, buf, 64), "gnsscorr_device_pci_bus_id")
+    return buf.value.decode()
+
+
+def hip_runtime_path() -> str:
+    """The libamdhip64 this process mapped (the library binds the first one loaded)."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    return line.split()[-1]
+    except OSError:
+        pass
+    return ""
 
 
 # ---------------------------------------------------------------- device memory

@@ -39,6 +39,8 @@ const char *gnsscorr_version(void);
 /* Number of visible HIP devices (0 on a CPU-only host; never initialises
  * more than hipGetDeviceCount does). */
 int gnsscorr_device_count(void);
+/* PCI bus id ("0000:xx:00.0") of a device, for run records. */
+int gnsscorr_device_pci_bus_id(int device, char *buf, int len);
 
 /* ======================================================================
  * Tracking correlator (GP2021 integer semantics)
