@@ -250,8 +250,8 @@ def run_sgt(dist, dev, steps, warmup):
                           1e6 + 0.5625e6 * np.arange(-7, 7))
     d14 = gc.DevBuf.from_array(ch14, dev)
     ctx.track_dev(d_if.ptr, stride, ns, 14, d14.ptr, warmup, d_ep.ptr)
+    ctx.sync()          # DevBuf copies are not ordered against the context stream
     d14.upload(ch14)
-    ctx.sync()
     e0.record(ctx.stream)
     ctx.track_dev(d_if.ptr, stride, ns, 14, d14.ptr, steps, d_ep.ptr)
     e1.record(ctx.stream)

@@ -34,14 +34,19 @@ extern "C" int gnsscorr_dev_free(int device, void* d_ptr) {
   return GNSSCORR_OK;
 }
 
+// The plain copies wait for the whole device first: a hipMemcpy on the null
+// stream is not ordered against the contexts' non-blocking streams, so a
+// copy issued while a kernel still uses the buffer would race with it.
 extern "C" int gnsscorr_memcpy_htod(int device, void* d, const void* h, size_t bytes) {
   HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
   return GNSSCORR_OK;
 }
 
 extern "C" int gnsscorr_memcpy_dtoh(int device, void* h, const void* d, size_t bytes) {
   HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost));
   return GNSSCORR_OK;
 }

@@ -674,9 +674,16 @@ extern "C" int gnsscorr_sdr_acq_create(gnsscorr_sdr_acq_ctx** out, const gnsscor
     gnsscorr_sdr_post_dft((int16_t*)(w10 + 4 * (size_t)kWipe));
     gnsscorr_sdr_prn_codes(tmp);
     memcpy(h + 4 * kN, tmp, sizeof(uint32_t) * 51 * kN);
-    // cmulsc_d2 negates the code's Q component in int16 (sdr_strong_kernel)
-    for (size_t k = 0; k < (size_t)51 * kN * 2; k++)
-      if (((const int16_t*)tmp)[k] == -32768) rc = GNSSCORR_EINVAL;
+    // cmulsc_d2 negates the code's Q component in int16 (sdr_strong_kernel):
+    // -32768 would not be representable (the table is within +-502,
+    // pinned by tests/test_codes_host.py)
+    for (size_t k = 1; k < (size_t)51 * kN * 2; k += 2)
+      if (((const int16_t*)tmp)[k] == -32768) {
+        gnsscorr_set_error("gnsscorr_sdr_acq_create: PRN spectrum Q == -32768 is not "
+                           "representable for the negated code product");
+        rc = GNSSCORR_EINVAL;
+        break;
+      }
     gnsscorr_sdr_twiddles((int16_t*)(h + 55 * kN), (int16_t*)(h + 55 * kN + kN / 2));
   }
   hipError_t e = hipSuccess;

@@ -542,6 +542,7 @@ extern "C" int gnsscorr_sdr_channel_accum_dev(gnsscorr_sdr_corr_ctx* ctx, int n_
     return GNSSCORR_EINVAL;
   }
   if (n_ms == 0) return GNSSCORR_OK;
+  HIP_TRY(hipSetDevice(gnsscorr_sdr_corr_device(ctx)));
   hipStream_t s = (hipStream_t)gnsscorr_sdr_corr_stream(ctx);
   static const Twiddles tw = make_twiddles();
   hipLaunchKernelGGL(sdr_channel_kernel, dim3((n_ch + 63) / 64), dim3(64), 0, s, n_ch, n_ms,

@@ -82,8 +82,10 @@ __global__ __launch_bounds__(kThreads) void sdr_accum_kernel(
   for (int k = 0; k < 3; k++) {
     const size_t bit0 = cb[k] + (size_t)wave0;
     sh[k] = (uint32_t)bit0 & 31u;
-    // words 0..32 cover bits up to sh + 1023; an idle wave loads nothing
-    cw[k] = (lane <= 32 && wave0 < nend) ? codebits[(bit0 >> 5) + lane] : 0u;
+    // words 0..32 cover bits up to sh + 1023; a lane loads only a word the
+    // wave's samples reach (an idle wave loads nothing)
+    const int last = ((int)sh[k] + (nend - wave0) - 1) >> 5;
+    cw[k] = (wave0 < nend && lane <= last) ? codebits[(bit0 >> 5) + lane] : 0u;
   }
   for (int n0 = wave0; n0 < nend; n0 += 64) {
     const int n = n0 + lane;
@@ -254,8 +256,9 @@ extern "C" int gnsscorr_sdr_corr_create(gnsscorr_sdr_corr_ctx** out,
   auto* c = new gnsscorr_sdr_corr_ctx();
   c->cfg = *cfg;
   const size_t ncar = (size_t)kSBins * kRow;
-  // + 4 words: the kernel's word window may end one word past a row's last bit
-  const size_t nbits = (size_t)kSV * kCBins * kRow, nwords = nbits / 32 + 4;
+  // + 33 words: a wave's 33-word window (sdr_accum_kernel) starting in the
+  // last row stays inside the allocation even before its lane clamp
+  const size_t nbits = (size_t)kSV * kCBins * kRow, nwords = nbits / 32 + 33;
   std::vector<uint32_t> car(ncar), bits(nwords, 0u);
   // carrier rows: sine_gen(row, -IF_FREQUENCY - (float)k*CARRIER_SPACING, fs, 4096)
   for (int k = -kCarrBins; k <= kCarrBins; k++) {
@@ -472,4 +475,8 @@ extern "C" int gnsscorr_sdr_corr_sync(gnsscorr_sdr_corr_ctx* c) {
 
 extern "C" void* gnsscorr_sdr_corr_stream(gnsscorr_sdr_corr_ctx* c) {
   return c ? (void*)c->stream : nullptr;
+}
+
+extern "C" int gnsscorr_sdr_corr_device(const gnsscorr_sdr_corr_ctx* c) {
+  return c ? c->cfg.device : -1;
 }

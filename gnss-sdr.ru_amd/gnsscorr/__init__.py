@@ -169,7 +169,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sdr_acq_search_dev", "gnsscorr_sdr_acq_acquire",
     "gnsscorr_sdr_corr_create", "gnsscorr_sdr_corr_destroy", "gnsscorr_sdr_init_chan",
     "gnsscorr_sdr_accum_dev", "gnsscorr_sdr_correlate", "gnsscorr_sdr_corr_sync",
-    "gnsscorr_sdr_corr_stream",
+    "gnsscorr_sdr_corr_stream", "gnsscorr_sdr_corr_device",
     "gnsscorr_sdr_gn3s_products", "gnsscorr_sdr_fe_create", "gnsscorr_sdr_fe_destroy",
     "gnsscorr_sdr_gn3s_dev", "gnsscorr_sdr_gn3s", "gnsscorr_sdr_downsample_count",
     "gnsscorr_sdr_downsample_dev", "gnsscorr_sdr_fe_sync", "gnsscorr_sdr_fe_stream",
@@ -257,6 +257,7 @@ def lib() -> C.CDLL:
         "gnsscorr_sdr_correlate": (I, [P, P, I, I, P, P, P, P, P]),
         "gnsscorr_sdr_corr_sync": (I, [P]),
         "gnsscorr_sdr_corr_stream": (P, [P]),
+        "gnsscorr_sdr_corr_device": (I, [P]),
         "gnsscorr_sdr_gn3s_products": (None, [P]),
         "gnsscorr_osg_loop_cfg_init": (None, [P, D, D, D, I, I, D, C.c_long, C.c_long, C.c_long,
                                               C.c_long, C.c_long, I]),
@@ -863,6 +864,7 @@ class SdrCorrCtx:
                                                                                int(saturate)))),
                "gnsscorr_sdr_corr_create")
         self.h = h
+        self.device = device
 
     def close(self):
         if getattr(self, "h", None):
@@ -900,18 +902,23 @@ class SdrCorrCtx:
         corr = np.ascontiguousarray(corr, np.int32)
         n_ms, n_ch = corr.shape[0], corr.shape[1]
         assert chans.dtype == SDR_CHANNEL and len(chans) == n_ch
-        d_c = DevBuf.from_array(corr)
-        d_s = DevBuf.from_array(chans)
-        d_fb = DevBuf(max(n_ms, 1) * n_ch * SDR_FEEDBACK.itemsize) if all_feedback else None
-        d_last = DevBuf(n_ch * SDR_FEEDBACK.itemsize)
-        d_ev = DevBuf(max(max_events, 1) * SDR_SUBFRAME.itemsize)
-        d_n = DevBuf.from_array(np.zeros(1, np.int32))
+        dev = self.device
+        d_c = DevBuf.from_array(corr, dev)
+        d_s = DevBuf.from_array(chans, dev)
+        d_fb = DevBuf(max(n_ms, 1) * n_ch * SDR_FEEDBACK.itemsize, dev) if all_feedback else None
+        d_last = DevBuf(n_ch * SDR_FEEDBACK.itemsize, dev)
+        d_ev = DevBuf(max(max_events, 1) * SDR_SUBFRAME.itemsize, dev)
+        d_n = DevBuf.from_array(np.zeros(1, np.int32), dev)
         self.channel_accum_dev(n_ch, n_ms, d_c.ptr, d_s.ptr, d_fb.ptr if d_fb else None,
                                d_last.ptr, d_ev.ptr, max_events, d_n.ptr)
         self.sync()
         chans[:] = d_s.download(np.uint8).view(SDR_CHANNEL)
         n = int(d_n.download(np.int32)[0])
-        ev = d_ev.download(np.uint8).view(SDR_SUBFRAME)[:min(n, max_events)]
+        if n > max_events:
+            # the kernel keeps whichever max_events subframes won the append race
+            raise GnssCorrError(f"channel_accum: {n} subframes exceed max_events={max_events}; "
+                                "the kept set would be arbitrary -- raise max_events")
+        ev = d_ev.download(np.uint8).view(SDR_SUBFRAME)[:n]
         ev = ev[np.lexsort((ev["chan"], ev["ms"]))]
         if all_feedback:
             fb = d_fb.download(np.uint8).view(SDR_FEEDBACK)[:n_ms * n_ch].reshape(n_ms, n_ch)

@@ -529,6 +529,8 @@ int gnsscorr_sdr_correlate(gnsscorr_sdr_corr_ctx *ctx, const int16_t *h_packets,
                            gnsscorr_sdr_corr *corr, gnsscorr_sdr_dump_fn cb, void *user);
 int gnsscorr_sdr_corr_sync(gnsscorr_sdr_corr_ctx *ctx);
 void *gnsscorr_sdr_corr_stream(gnsscorr_sdr_corr_ctx *ctx);
+/* Device the context was created on (-1 for NULL). */
+int gnsscorr_sdr_corr_device(const gnsscorr_sdr_corr_ctx *ctx);
 
 /* ======================================================================
  * GPS-SDR channel: Channel::Accum
@@ -577,7 +579,10 @@ int gnsscorr_sdr_channel_start(gnsscorr_sdr_channel *ch, int chan, int sv, int a
  * is channel c's Correlation_S of call m (E, P, L); d_fb[m*n_ch + c] gets the
  * NCO_Command_S it fills (d_fb NULL: only the last call's, in d_fb_last).
  * Valid subframes are appended to d_events (up to max_events; *d_n_events
- * counts them all, order = call, then channel).  Async on the context stream. */
+ * counts them all; slots are taken in arrival order, so sort by (call,
+ * channel)).  On overflow (*d_n_events > max_events) WHICH subframes were
+ * kept is arbitrary: size max_events from n_ch * n_ms / 6000 + n_ch (one
+ * subframe per 6 s per channel) or retry larger.  Async on the context stream. */
 int gnsscorr_sdr_channel_accum_dev(gnsscorr_sdr_corr_ctx *ctx, int n_ch, int n_ms,
                                    const gnsscorr_sdr_corr *d_corr, gnsscorr_sdr_channel *d_ch,
                                    gnsscorr_sdr_feedback *d_fb, gnsscorr_sdr_feedback *d_fb_last,
@@ -626,6 +631,8 @@ void *gnsscorr_sdr_fe_stream(gnsscorr_sdr_fe_ctx *ctx);
  * ==================================================================== */
 int gnsscorr_dev_alloc(int device, size_t bytes, void **d_ptr);
 int gnsscorr_dev_free(int device, void *d_ptr);
+/* Synchronous copies: each first waits until the device is idle, so they are
+ * ordered after every kernel already queued on any context stream. */
 int gnsscorr_memcpy_htod(int device, void *d_dst, const void *h_src, size_t bytes);
 int gnsscorr_memcpy_dtoh(int device, void *h_dst, const void *d_src, size_t bytes);
 int gnsscorr_dev_synchronize(int device);

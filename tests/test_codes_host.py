@@ -82,3 +82,11 @@ def test_acq_oracle_finds_planted_signal(gc):
     assert abs(res[0]["code_phase"] - 1 - (1023 - 300) * 16) <= 1
     assert abs(res[0]["carr_freq"] - (2.42e6 + 2250)) <= 250
     assert res[0]["metric"] > 2.5 and res[1]["metric"] < res[0]["metric"]
+
+
+def test_sdr_prn_spectra_range(gc):
+    """sdr_strong_kernel multiplies by the negated Q of the PRN spectra in int16
+    (sdr_acq.hip cmulsc_d2): the table (prn_codes.h values, gen_fft_codes.m
+    scaling to 2^9) must stay within +-502, far from -32768."""
+    pc = gc.sdr_prn_codes().astype(np.int32)
+    assert np.abs(pc).max() <= 502
