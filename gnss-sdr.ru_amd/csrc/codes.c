@@ -13,6 +13,9 @@
  *  gnsscorr_ifgen            int8 IQ at {-3,-1,1,3} (gps_source.cpp:692 levels)
  */
 #include "gnsscorr_internal.h"
+#include <pthread.h>
+#include <stdlib.h>
+#include <unistd.h>
 #include <math.h>
 #include <string.h>
 #include <stdlib.h>
@@ -145,6 +148,81 @@ static inline int8_t quant2(double x)
   return (int8_t)(x > -1.0 ? -1 : -3);
 }
 
+/* g advanced by k steps of lcg_next (LCG jump-ahead by squaring) */
+static uint64_t lcg_jump(uint64_t s, uint64_t k)
+{
+  uint64_t a = 6364136223846793005ULL, c = 1442695040888963407ULL, A = 1, C = 0;
+  while (k) {
+    if (k & 1) { A *= a; C = C * a + c; }
+    c *= a + 1;
+    a *= a;
+    k >>= 1;
+  }
+  return s * A + C;
+}
+
+typedef struct {
+  int8_t *out;
+  int64_t nsamp;
+  int iq;
+  double fs;
+  int n_sigs;
+  const gnsscorr_sig *sigs;
+  uint64_t seed;
+  int8_t (*codes)[1023];
+  int *clen;
+  double *amp, *fcar, *crate, *bit_ms;
+  uint32_t (*bits)[64];
+  int64_t next;   /* next chunk (atomic) */
+} ifgen_job;
+
+#define IFGEN_CHUNK ((int64_t)1 << 18)
+
+static void *ifgen_worker(void *arg)
+{
+  ifgen_job *j = (ifgen_job *)arg;
+  const gnsscorr_sig *sigs = j->sigs;
+  for (;;) {
+    const int64_t n0 = __atomic_fetch_add(&j->next, IFGEN_CHUNK, __ATOMIC_RELAXED);
+    if (n0 >= j->nsamp) break;
+    const int64_t n1 = n0 + IFGEN_CHUNK < j->nsamp ? n0 + IFGEN_CHUNK : j->nsamp;
+    lcg_t g = { lcg_jump(j->seed, 2 * (uint64_t)n0) };   /* two draws per sample */
+    for (int64_t n = n0; n < n1; n++) {
+      double t = (double)n / j->fs;
+      double re = 0, im = 0;
+      for (int s = 0; s < j->n_sigs; s++) {
+        double chips = sigs[s].code_phase + t * j->crate[s];
+        double per = floor(chips / j->clen[s]);
+        long ci = (long)(chips - per * j->clen[s]);
+        if (ci < 0) ci += j->clen[s];
+        if (ci >= j->clen[s]) ci -= j->clen[s];
+        double v = j->amp[s] * j->codes[s][ci];
+        if (sigs[s].data_bits) {
+          long bi = (long)floor(per * (1.0 / (j->bit_ms[s])));   /* one code period = 1 ms */
+          bi = ((bi % 4096) + 4096) % 4096;
+          if ((j->bits[s][(bi >> 5) & 63] >> (bi & 31)) & 1u) v = -v;
+        }
+        /* The reference front-end's complex IF is spectrum-inverted: the signal
+         * sits at -f (acquisition.sci:107-111 and the GP2021 mixer,
+         * correlator.c:213-215, both wipe off with exp(+i 2 pi f t)). */
+        double ph = 2.0 * M_PI * j->fcar[s] * t + sigs[s].carr_phase;
+        re += v * cos(ph);
+        im -= v * sin(ph);
+      }
+      double u1 = lcg_unif(&g), u2 = lcg_unif(&g);
+      double rad = sqrt(-2.0 * log(u1));
+      double e1 = rad * cos(2.0 * M_PI * u2), e2 = rad * sin(2.0 * M_PI * u2);
+      if (j->iq) {
+        j->out[2 * n] = quant2(re + e1);
+        j->out[2 * n + 1] = quant2(im + e2);
+      } else {
+        j->out[n] = quant2(re * 1.41421356237309505 + e1);
+      }
+    }
+  }
+  return NULL;
+}
+
 int gnsscorr_ifgen(int8_t *out, int64_t nsamp, int iq, double fs, double if_gps, double if_glo,
                    int n_sigs, const gnsscorr_sig *sigs, uint64_t seed)
 {
@@ -172,38 +250,24 @@ int gnsscorr_ifgen(int8_t *out, int64_t nsamp, int iq, double fs, double if_gps,
     lcg_t b = { seed ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(s + 1)) };
     for (int w = 0; w < 64; w++) bits[s][w] = g->data_bits ? (uint32_t)(lcg_next(&b) >> 32) : 0u;
   }
-  lcg_t g = { seed ? seed : 0x5EED0000ULL };
-  for (int64_t n = 0; n < nsamp; n++) {
-    double t = (double)n / fs;
-    double re = 0, im = 0;
-    for (int s = 0; s < n_sigs; s++) {
-      double chips = sigs[s].code_phase + t * crate[s];
-      double per = floor(chips / clen[s]);
-      long ci = (long)(chips - per * clen[s]);
-      if (ci < 0) ci += clen[s];
-      if (ci >= clen[s]) ci -= clen[s];
-      double v = amp[s] * codes[s][ci];
-      if (sigs[s].data_bits) {
-        long bi = (long)floor(per * (1.0 / (bit_ms[s])));   /* one code period = 1 ms */
-        bi = ((bi % 4096) + 4096) % 4096;
-        if ((bits[s][(bi >> 5) & 63] >> (bi & 31)) & 1u) v = -v;
-      }
-      /* The reference front-end's complex IF is spectrum-inverted: the signal
-       * sits at -f (acquisition.sci:107-111 and the GP2021 mixer,
-       * correlator.c:213-215, both wipe off with exp(+i 2 pi f t)). */
-      double ph = 2.0 * M_PI * fcar[s] * t + sigs[s].carr_phase;
-      re += v * cos(ph);
-      im -= v * sin(ph);
-    }
-    double u1 = lcg_unif(&g), u2 = lcg_unif(&g);
-    double rad = sqrt(-2.0 * log(u1));
-    double n1 = rad * cos(2.0 * M_PI * u2), n2 = rad * sin(2.0 * M_PI * u2);
-    if (iq) {
-      out[2 * n] = quant2(re + n1);
-      out[2 * n + 1] = quant2(im + n2);
-    } else {
-      out[n] = quant2(re * 1.41421356237309505 + n1);
-    }
+  ifgen_job job = {out, nsamp, iq, fs, n_sigs, sigs, seed ? seed : 0x5EED0000ULL, codes, clen,
+                   amp, fcar, crate, bit_ms, bits, 0};
+  /* chunks of samples over threads; each chunk starts its noise LCG by an
+   * exact jump-ahead, so the output does not depend on the thread count */
+  int nt = 1;
+  const char *e = getenv("GNSSCORR_IFGEN_THREADS");
+  if (e) nt = atoi(e);
+  else {
+    long c = sysconf(_SC_NPROCESSORS_ONLN);
+    nt = (int)(c > 16 ? 16 : c);
   }
+  if (nt < 1) nt = 1;
+  if (nsamp < (1 << 20)) nt = 1;
+  pthread_t th[16];
+  int started = 0;
+  for (int i = 1; i < nt && i < 16; i++)
+    if (pthread_create(&th[started], NULL, ifgen_worker, &job) == 0) started++;
+  ifgen_worker(&job);
+  for (int i = 0; i < started; i++) pthread_join(th[i], NULL);
   return GNSSCORR_OK;
 }

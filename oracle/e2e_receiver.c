@@ -16,9 +16,15 @@
  * The two traces must be byte-identical: the closed-loop DLL/PLL sees exactly
  * the same accumulators from the GPU as from the reference correlator.
  *
+ * The _16368 builds (oracle/Makefile e2e16368) stream globals.h with SAMP_RATE
+ * rewritten to 16.368e6 into every compile (BASELINE config 1); e2e_gpu_16368
+ * runs with GNSSCORR_SAMP_RATE=16.368e6 for the shim's correlator_init.
+ *
  * usage: e2e_xxx <if.bin> <trace.bin> <n_calls> <prn ch0> [prn ch1 ...]
  */
+#ifndef MAIN
 #define MAIN
+#endif
 #include "globals.h"
 #include <stdlib.h>
 #include <string.h>
