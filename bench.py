@@ -562,7 +562,12 @@ def cpu_baseline_sgt(budget_s=6.0):
 def cpu_baseline_acq(meta, budget_s=12.0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import acq_oracle
-    workers = max(1, min(16, os.cpu_count() or 1))
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    workers = max(1, min(16, aff or 1))
+    gf1 = np.tile(np.arange(N_BINS), (N_PRN, 1))
+    t0 = time.perf_counter()
+    acq_oracle.acquire_batched(meta["IF"], FS, meta["codes"], meta["freqs"], gf1, workers=1)
+    one = CELLS_PER_SEARCH / (time.perf_counter() - t0)
     gf = np.tile(np.arange(N_BINS), (N_PRN, 1))
     n, t0 = 0, time.perf_counter()
     while True:
@@ -574,38 +579,80 @@ def cpu_baseline_acq(meta, budget_s=12.0):
     dt = time.perf_counter() - t0
     return dict(value=n * CELLS_PER_SEARCH / dt, unit="cells/s", cores=workers, kind="port",
                 sample=f"{n} full 32x41 searches (fp64 numpy/scipy pocketfft restatement of "
-                       f"acquisition.sci, oracle/acq_oracle.py), {dt:.1f} s")
+                       f"acquisition.sci, oracle/acq_oracle.py), {dt:.1f} s",
+                port_1core=dict(value=one, cores=1, sample="1 full 32x41 search, 1 worker"),
+                host=host_info())
 
 
-def cpu_baseline_track(budget_s=8.0):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import osg_oracle
-    if not os.path.exists(osg_oracle.ORACLE_SO):
-        return None
-    o = osg_oracle.OracleOSG()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n_inst, if_calls = threads, 32
-    IF = np.random.default_rng(1).choice(np.array([-3, -1, 1, 3], np.int8),
-                                         size=n_inst * if_calls * TRACK_NS * 2)
-    # size the sample: grow the call count until a run takes >= budget/4, then
-    # scale to the budget (the first calls also pay thread start + page faults)
-    calls = 50
+def host_info():
+    """The host cores the CPU baselines ran on (nproc, affinity, model)."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return dict(nproc=os.cpu_count(), affinity=aff, cpu_model=model)
+
+
+def _timed(fn, budget_s):
+    """Run fn(calls) -> work with calls grown until one run takes >= budget/4,
+    then once more sized to the budget; returns (work, seconds, calls)."""
+    calls = 20
     while True:
         t0 = time.perf_counter()
-        o.L.osgo_bench(n_inst, TRACK_CH, IF.ctypes.data, TRACK_NS, calls, if_calls, 31750430,
-                       6710886, threads)
+        fn(calls)
         probe = time.perf_counter() - t0
         if probe >= budget_s / 4 or calls >= 1 << 20:
             break
         calls *= 4
     calls = max(calls, int(calls * budget_s / max(probe, 1e-3)))
     t0 = time.perf_counter()
-    work = o.L.osgo_bench(n_inst, TRACK_CH, IF.ctypes.data, TRACK_NS, calls, if_calls, 31750430,
-                          6710886, threads)
-    dt = time.perf_counter() - t0
-    return dict(value=work / TRACK_NS / dt, unit="channel-ms/s", cores=threads, kind="port",
-                sample=f"{n_inst} receivers x {TRACK_CH} ch x {calls} 1-ms calls of the scalar "
-                       f"Sim_GP2021_int restatement (oracle/osg_corr.c), {dt:.1f} s")
+    work = fn(calls)
+    return work, time.perf_counter() - t0, calls
+
+
+def cpu_baseline_track(budget_s=6.0):
+    """BASELINE config 3 CPU path: the REFERENCE Sim_GP2021_int (correlator.c built
+    from /root/reference into oracle/_ref/libosg_ref.so) on one core -- the
+    reference keeps its state in globals, one instance per process -- beside our
+    C port (oracle/osg_corr.c) on one core and on all cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes as C
+    import osg_oracle
+    if not os.path.exists(osg_oracle.ORACLE_SO):
+        return None
+    IF = np.random.default_rng(1).choice(np.array([-3, -1, 1, 3], np.int8),
+                                         size=16 * 32 * TRACK_NS * 2)
+    o = osg_oracle.OracleOSG()
+    out = {}
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                         else os.cpu_count() or 1))
+    for tag, th, ninst in (("port_1core", 1, 1), ("port_all_cores", threads, threads)):
+        w, dt, calls = _timed(lambda c: o.L.osgo_bench(ninst, TRACK_CH, IF.ctypes.data, TRACK_NS,
+                                                       c, 32, 31750430, 6710886, th), budget_s)
+        out[tag] = dict(value=w / TRACK_NS / dt, cores=th,
+                        sample=f"{ninst} receivers x {TRACK_CH} ch x {calls} 1-ms calls, {dt:.1f} s")
+    ref = None
+    if osg_oracle.have_ref():
+        L = C.CDLL(osg_oracle.REF_SO)
+        L.ref_bench.restype = C.c_double
+        L.ref_bench.argtypes = [C.c_void_p, C.c_long, C.c_int, C.c_int, C.c_long, C.c_long]
+        w, dt, calls = _timed(lambda c: L.ref_bench(IF.ctypes.data, TRACK_NS, c, 32, 31750430,
+                                                    6710886), budget_s)
+        ref = dict(value=w / TRACK_NS / dt, unit="channel-ms/s", cores=1, kind="reference",
+                   sample=f"12 ch x {calls} 1-ms calls of the reference Sim_GP2021_int "
+                          f"(correlator.c built from /root/reference, oracle/_ref/libosg_ref.so), "
+                          f"{dt:.1f} s")
+    base = ref or dict(value=out["port_all_cores"]["value"], unit="channel-ms/s",
+                       cores=out["port_all_cores"]["cores"], kind="port",
+                       sample="reference build absent: " + out["port_all_cores"]["sample"])
+    base.update(out)
+    base["host"] = host_info()
+    return base
 
 
 def pmc_traffic(kernel):

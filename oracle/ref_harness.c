@@ -135,3 +135,30 @@ void ref_isr_step(int dump_mask, const int32_t *dumps, int32_t *regs)
   gpsisr();
   memcpy(regs, REG_write, sizeof(int) * 256);
 }
+
+/* ---- CPU baseline: the reference Sim_GP2021_int itself, one core ---------
+ * 12 channels active (PRNs 1..12, the given carrier / code words), n_calls
+ * calls over if_calls rotating IF buffers of nsamp interleaved int8 I,Q
+ * samples.  Returns channel-samples processed.  The reference keeps its state
+ * in globals, so this is one instance on one thread by construction. */
+void Sim_GP2021_int(char *IF, long nsamp);
+void ch_cntl(int ch, int prn);
+void ch_carrier(int ch, long freq);
+void ch_code(int ch, long freq);
+double ref_bench(const int8_t *IF, long nsamp, int n_calls, int if_calls, long carrier_word,
+                 long code_word)
+{
+  use_iq_processing = 1;
+  correlator_init(tic_period);
+  for (int ch = 0; ch < N_CHANNELS; ch++) {
+    ch_cntl(ch, 1 + ch);
+    ch_carrier(ch, carrier_word + 13 * ch);
+    ch_code(ch, code_word);
+  }
+  double work = 0;
+  for (int c = 0; c < n_calls; c++) {
+    Sim_GP2021_int((char *)IF + (size_t)(c % if_calls) * (size_t)nsamp * 2, nsamp);
+    work += (double)N_CHANNELS * (double)nsamp;
+  }
+  return work;
+}

@@ -3,7 +3,10 @@
 * bench.Dist: barrier + max-over-ranks timing (the bench contract);
 * full-sky sharding (gnsscorr/fullsky.py): every rank takes a disjoint group
   set, the per-group results are gathered (all_gather_object over gloo) and
-  merged on rank 0 in group order -- the only exchange config 5 needs.
+  merged on rank 0 in group order -- the only exchange config 5 needs;
+* tracking sharding (gnsscorr/trackshard.py): channels round-robin over
+  ranks, each rank's NCO commands remapped onto its local IF copies, results
+  gathered by global channel index.
 No GPU: each rank fabricates its shard's results.
 """
 import os
@@ -73,3 +76,67 @@ def test_shard_is_a_partition():
         assert max(map(len, parts)) - min(map(len, parts)) <= 1
     with pytest.raises(ValueError):
         shard(46, 2, 2)
+
+
+def _track_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "gnss-sdr.ru_amd")]
+    import bench
+    import gnsscorr as gc
+    from gnsscorr.trackshard import local_cmds, merge, plan
+    d = bench.Dist()
+    n_rx, n_ch = 5, 12
+    cmds = np.zeros(n_rx * n_ch, gc.NCO_CMD)
+    cmds["prn"] = np.arange(n_rx * n_ch) % 32 + 1
+    cmds["stream"] = np.repeat(np.arange(n_rx), n_ch)
+    mine, streams, lstream = plan(n_rx, n_ch, world, rank)
+    lc = local_cmds(cmds, mine, lstream)
+    # every local channel reads the local copy of its own receiver's stream
+    ok = all(streams[lc["stream"][i]] == cmds["stream"][g] for i, g in enumerate(mine))
+    res = np.zeros(len(mine), gc.TRACK_RESULT)
+    res["n_dumps"] = np.asarray(mine) * 3 + 1       # a per-channel fingerprint
+    parts = d.gather((mine, res))
+    if rank == 0:
+        m = merge(parts, n_rx * n_ch)
+        q.put(("ok", bool(ok), m["n_dumps"].tolist(), len(streams)))
+    d.close()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_track_sharding(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_track_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        tag, ok, dumps, nstreams = q.get(timeout=120)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert tag == "ok" and ok
+    assert dumps == [g * 3 + 1 for g in range(60)]
+    assert nstreams == 5                  # round-robin channels: every stream is copied
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_track_plan_partition_and_merge_checks():
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gnss-sdr.ru_amd"))
+    import gnsscorr as gc
+    from gnsscorr.trackshard import merge, plan
+    for world in (1, 2, 3, 8):
+        parts = [plan(7, 12, world, r)[0] for r in range(world)]
+        assert sorted(g for p in parts for g in p) == list(range(84))
+        assert max(map(len, parts)) - min(map(len, parts)) <= 1
+    with pytest.raises(RuntimeError):
+        merge([([0, 1], np.zeros(2, gc.TRACK_RESULT))], 3)
+    with pytest.raises(ValueError):
+        plan(2, 12, 2, 5)
