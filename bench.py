@@ -42,7 +42,7 @@ CELLS_PER_SEARCH = N_PRN * N_BINS * N          # 21,474,816 (SURVEY
 # IFFT 5*log2(N) + complex multiply 6 + |.|^2 3 + max 1  
 FLOP_PER_CELL_BLOCK = 5.0 * np.log2(N) + 6 + 3 + 1
 PEAK_FP32_TFLOPS = 157.3                       # MI355X_MICROARCH.md (vector == matrix f32)
-ACQ64_KERNEL = "acq64_corr_kernel<PlanA,0,false>"   # 16368 = 16 x 33 x 31, best-of-blocks
+ACQ64_KERNEL = "acq64_corr_kernel<Plan<16368, 16, 33, 31, 512, true>, 0, false>"  # best-of-blocks
 PEAK_HBM_GBS = 8000.0
 PEAK_INT_TOPS = 78.6                           # 256 CU x 128 lanes x 2.4 GHz, 32-bit VALU
 TRACK_RX, TRACK_CH, TRACK_NS = 256, 12, 16368

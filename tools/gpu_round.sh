@@ -7,7 +7,7 @@ O=gpurun_out/$TAG
 mkdir -p $O/pmc
 export TMPDIR=/tmp
 echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 tail -3 $O/pytest.log
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1

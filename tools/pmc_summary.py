@@ -53,6 +53,9 @@ def main():
                 if base not in keep or m["hbm_bytes_per_launch"] > keep[base]["hbm_bytes_per_launch"]:
                     keep[base] = {"hbm_bytes_per_launch": m["hbm_bytes_per_launch"],
                                   "source": os.path.relpath(o), "instance": k}
+                if k != base:   # every template instantiation under its own name too
+                    keep[k] = {"hbm_bytes_per_launch": m["hbm_bytes_per_launch"],
+                               "source": os.path.relpath(o), "instance": k}
         json.dump(keep, open(t, "w"), indent=1, sort_keys=True)
     for k, m in sorted(s.items()):
         print(k, {c: round(v, 3) for c, v in m.items() if c in
