@@ -213,6 +213,128 @@ def run_track(dist, dev, steps, warmup):
     return dict(dt=dt, kern_ms=kern_ms, channels=C, dumps_ok=dumps_ok, dt_cl=dt_cl, cl_ms=cl_ms)
 
 
+def _replay_timed(dist, dev, ctx, d_if, stride, if_step_bytes, d_cmds, d_res, C, steps, warmup):
+    """warmup + steps replayed 1-ms calls; returns (wall s, kernel ms per call, results)."""
+    ctx.replay_dev(d_if.ptr, stride, TRACK_NS, warmup, d_cmds.ptr, d_res.ptr)
+    ctx.sync()
+    e0, e1 = gc.Event(dev), gc.Event(dev)
+    dist.barrier()
+    gc.dev_synchronize(dev)
+    t0 = time.perf_counter()
+    e0.record(ctx.stream)
+    ctx.replay_dev(d_if.ptr + warmup * if_step_bytes, stride, TRACK_NS, steps,
+                   d_cmds.ptr + warmup * C * gc.NCO_CMD.itemsize,
+                   d_res.ptr + warmup * C * gc.TRACK_RESULT.itemsize)
+    e1.record(ctx.stream)
+    ctx.sync()
+    gc.dev_synchronize(dev)
+    dt = dist.max(time.perf_counter() - t0)
+    res = d_res.download(gc.TRACK_RESULT, C, (warmup + steps - 1) * C * gc.TRACK_RESULT.itemsize)
+    return dt, dist.max(e0.elapsed_ms(e1) / steps), res
+
+
+def _track_cmds(rng, C, streams):
+    cmd1 = np.zeros(C, gc.NCO_CMD)
+    cmd1["prn"] = rng.integers(1, 33, C)
+    cmd1["stream"] = streams
+    cmd1["carrier_incr"] = 635008600 + rng.integers(-262000, 262000, C) * 20   # +-5 kHz
+    cmd1["code_incr"] = 6710886 * 40 + rng.integers(-10, 10, C)
+    cmd1["epoch_load"] = -1
+    return cmd1
+
+
+def run_track_io(dist, dev, steps, warmup):
+    """Tracking layouts beside the main line (all 16.368 Msps, 1-ms calls):
+    * one IF stream PER CHANNEL (C_s = 1: the layout where HBM bytes bind), int8 and
+      2-bit packed (GNSSCORR_IF_PACKED2), 3072 channels, distinct data every call;
+    * the main 256 x 12 layout with packed streams;
+    * PCIe-inclusive: gnsscorr_track from host buffers (256 x 12 channels per call);
+    * config 3 as the reference runs it: 12 channels, Sim_GP2021_int per 512-us
+      interrupt (osgnss_next_step.c:150,168-184) through the legacy shim, per-call latency."""
+    out = {}
+    K = steps + warmup
+    rng = np.random.default_rng(17 + dist.rank)
+    C1 = 3072
+    for packed in (False, True):
+        stride = K * TRACK_NS
+        bytes_stream = stride * 2 // (4 if packed else 1)
+        d_if = gc.DevBuf(C1 * bytes_stream, dev)
+        d_if.fill_if2(0x5EED000B + dist.rank)      # any byte is a valid packed code
+        cmd1 = _track_cmds(rng, C1, np.arange(C1))
+        d_cmds = gc.DevBuf.from_array(np.tile(cmd1, K), dev)
+        d_res = gc.DevBuf(K * C1 * gc.TRACK_RESULT.itemsize, dev)
+        ctx = gc.TrackCtx(C1, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS,
+                          packed=packed)
+        dt, kms, res = _replay_timed(dist, dev, ctx, d_if, stride, ctx.if_bytes(TRACK_NS),
+                                     d_cmds, d_res, C1, steps, warmup)
+        out["cs1_packed2" if packed else "cs1_int8"] = dict(
+            dt=dt, kern_ms=kms, channels=C1, bytes_launch=C1 * (ctx.if_bytes(TRACK_NS) + 64),
+            ok=bool((res["n_dumps"] >= 0).all() and (res["n_dumps"] <= 2).all()))
+        ctx.close()
+        d_if.free()
+    # main layout, packed
+    C = TRACK_RX * TRACK_CH
+    stride = K * TRACK_NS
+    d_if = gc.DevBuf(TRACK_RX * stride // 2, dev)
+    d_if.fill_if2(0x5EED000C + dist.rank)
+    cmd1 = _track_cmds(rng, C, np.repeat(np.arange(TRACK_RX), TRACK_CH))
+    d_cmds = gc.DevBuf.from_array(np.tile(cmd1, K), dev)
+    d_res = gc.DevBuf(K * C * gc.TRACK_RESULT.itemsize, dev)
+    ctx = gc.TrackCtx(C, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS, packed=True)
+    dt, kms, res = _replay_timed(dist, dev, ctx, d_if, stride, ctx.if_bytes(TRACK_NS), d_cmds,
+                                 d_res, C, steps, warmup)
+    out["rx12_packed2"] = dict(dt=dt, kern_ms=kms, channels=C,
+                               bytes_launch=C * (ctx.if_bytes(TRACK_NS) / TRACK_CH + 64))
+    ctx.close()
+    d_if.free()
+    # PCIe-inclusive: host IF (pageable numpy) -> gnsscorr_track -> host results, per call
+    for packed in (False, True):
+        ctx = gc.TrackCtx(C, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS, packed=packed)
+        h_if = np.random.default_rng(3).integers(-128, 128, TRACK_RX * ctx.if_bytes(TRACK_NS),
+                                                 dtype=np.int8)
+        if not packed:
+            h_if = np.random.default_rng(3).choice(np.array([-3, -1, 1, 3], np.int8), h_if.size)
+        n_calls = max(steps, 20)
+        for _ in range(3):
+            ctx.track(h_if, TRACK_NS, cmd1, n_streams=TRACK_RX, stream_stride=TRACK_NS)
+        lat = []
+        dist.barrier()
+        for _ in range(n_calls):
+            t0 = time.perf_counter()
+            ctx.track(h_if, TRACK_NS, cmd1, n_streams=TRACK_RX, stream_stride=TRACK_NS)
+            lat.append(time.perf_counter() - t0)
+        lat = np.array(lat)
+        out["host_packed2" if packed else "host_int8"] = dict(
+            channels=C, calls=n_calls, mean_ms=dist.max(float(lat.mean()) * 1e3),
+            p99_ms=dist.max(float(np.percentile(lat, 99)) * 1e3),
+            h2d_bytes=TRACK_RX * ctx.if_bytes(TRACK_NS))
+        ctx.close()
+    # config 3 through the legacy shim: 12 channels, 512-us interrupts
+    ns = int(FS * 512 / 1.0e6)                   # osgnss_next_step.c:150 (nsamp = fs*interr_int)
+    osg = gc.OSG(samp_rate=FS, n_channels=12, use_iq=True, device=dev)
+    osg.correlator_init(0.0)
+    for ch in range(12):
+        osg.ch_cntl(ch, ch + 1)
+        osg.ch_carrier(ch, osg.gps_carrier_ref + 300 * ch)
+        osg.ch_code(ch, osg.gps_code_ref)
+    IF12 = np.random.default_rng(4).choice(np.array([-3, -1, 1, 3], np.int8), 2 * ns * 64)
+    n_calls = 2000
+    for k in range(20):
+        osg.sim(IF12[(k % 64) * 2 * ns:], ns)
+    lat = np.empty(n_calls)
+    for k in range(n_calls):
+        chunk = IF12[(k % 64) * 2 * ns:(k % 64 + 1) * 2 * ns]
+        t0 = time.perf_counter()
+        osg.sim(chunk, ns)
+        lat[k] = time.perf_counter() - t0
+    out["sim_gp2021_12ch"] = dict(nsamp=ns, calls=n_calls, budget_us=512.0,
+                                  mean_us=float(lat.mean() * 1e6),
+                                  p50_us=float(np.percentile(lat, 50) * 1e6),
+                                  p99_us=float(np.percentile(lat, 99) * 1e6),
+                                  max_us=float(lat.max() * 1e6))
+    return out
+
+
 def run_sgt(dist, dev, steps, warmup):
     """BASELINE config 4: GLONASS L1OF 14 FDMA channels, tracking.sci float loop on the GPU.
     Throughput: SGT_RX records x 14 FCH; latency: one 14-channel receiver."""
@@ -584,6 +706,29 @@ def cpu_baseline_acq(meta, budget_s=12.0):
                 host=host_info())
 
 
+def cpu_baseline_fullsky(budget_s=8.0):
+    """Config 5 on the host: the fp64 acquisition.sci restatement in non-coherent
+    mode (oracle/acq_oracle.py acquire, numpy pocketfft, one core) over GPS
+    groups of the same shape (41 bins x 16368 x 10 ms), as many as fit the budget."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import acq_oracle
+    IF = gc.ifgen(10 * N, [dict(system=0, prn=3, code_phase=100.0, doppler=1000.0, cn0=45.0)],
+                  fs=FS, seed=0x5EED000D)
+    freqs = 2.42e6 + 500.0 * (np.arange(N_BINS) - (N_BINS - 1) / 2.0)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        code = acq_oracle.make_ca_table_row(n % 32 + 1, FS)[None]
+        acq_oracle.acquire(IF, FS, code, freqs, np.arange(N_BINS)[None], n_blocks=10,
+                           noncoherent=True)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=n * N_BINS * N * 10 / dt, unit="cell-ms/s", cores=1, kind="port",
+                sample=f"{n} GPS groups x {N_BINS} bins x 10 ms non-coherent (fp64 numpy "
+                       f"restatement of acquisition.sci, oracle/acq_oracle.py), {dt:.1f} s")
+
+
 def host_info():
     """The host cores the CPU baselines ran on (nproc, affinity, model)."""
     model = ""
@@ -685,6 +830,7 @@ def main():
     rank_info = dist.gather(dict(rank=dist.rank, device=dev, pci_bus_id=gc.pci_bus_id(dev),
                                  hip_runtime=gc.hip_runtime_path()))
     trk = None if a.skip_track else run_track(dist, dev, max(a.steps, 20), a.warmup)
+    tio = None if a.skip_track else run_track_io(dist, dev, max(a.steps, 20), a.warmup)
     sgt = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup)
     sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps // 5, 5), 2)
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
@@ -764,6 +910,47 @@ def main():
                     "ms_per_call": trk["cl_ms"],
                 },
             }
+        if tio:
+            lay = {}
+            for key, desc in (("cs1_int8", "one int8 IQ stream per channel (C_s = 1)"),
+                              ("cs1_packed2", "one 2-bit packed IQ stream per channel (C_s = 1)"),
+                              ("rx12_packed2", f"{TRACK_RX} receivers x {TRACK_CH} channels, "
+                                               "2-bit packed IQ streams")):
+                r = tio[key]
+                k_s = r["kern_ms"] * 1e-3
+                lay[key] = {
+                    "config": f"{r['channels']} channels, {desc}, distinct IF every call",
+                    "value": r["channels"] * steps_t * W / r["dt"], "unit": "channel-ms/s",
+                    "kernel_ms_per_launch": r["kern_ms"],
+                    "realtime_channels_per_gpu": r["channels"] / r["kern_ms"],
+                    "roofline": {"bound": "hbm", "kernel": "osg_track_kernel",
+                                 "achieved": r["bytes_launch"] / k_s / 1e9, "peak": PEAK_HBM_GBS,
+                                 "unit": "GB/s (algorithmic: IF bytes + 64 B state/command/"
+                                         "result per channel)",
+                                 "frac": r["bytes_launch"] / k_s / 1e9 / PEAK_HBM_GBS,
+                                 "int_ops_frac": r["channels"] * TRACK_NS * TRACK_OPS_PER_SAMPLE
+                                 / k_s / 1e12 / PEAK_INT_TOPS},
+                }
+                if "ok" in r:
+                    lay[key]["dumps_sane"] = r["ok"]
+            out["tracking"]["layouts"] = lay
+            out["tracking"]["pcie_inclusive"] = {
+                k: {"config": f"gnsscorr_track from pageable host buffers: {r['channels']} "
+                              f"channels on {TRACK_RX} streams, {r['h2d_bytes']} B H2D + results "
+                              "D2H + stream sync per 1-ms call",
+                    "value": r["channels"] / (r["mean_ms"] * 1e-3), "unit": "channel-ms/s",
+                    "mean_ms_per_call": r["mean_ms"], "p99_ms_per_call": r["p99_ms"],
+                    "realtime": r["p99_ms"] < 1.0}
+                for k, r in (("int8", tio["host_int8"]), ("packed2", tio["host_packed2"]))}
+            r = tio["sim_gp2021_12ch"]
+            out["tracking"]["config3_realtime"] = {
+                "config": f"BASELINE config 3 as the reference runs it: Sim_GP2021_int "
+                          f"(legacy shim) for 12 channels, {r['nsamp']} samples = one 512-us "
+                          f"interrupt per call (osgnss_next_step.c:150,168-184), host IF, "
+                          f"{r['calls']} calls",
+                "mean_us": r["mean_us"], "p50_us": r["p50_us"], "p99_us": r["p99_us"],
+                "max_us": r["max_us"], "budget_us": r["budget_us"],
+                "realtime": r["p99_us"] < r["budget_us"]}
         if sgt:
             C = sgt["channels"]
             k_s = sgt["kern_ms"] * 1e-3
@@ -788,6 +975,8 @@ def main():
                 "epochs_sane": sgt["ok"],
             }
         if sky:
+            sky_ms = sky["dt"] / sky["steps"] * 1e3
+            sky_flop = sky["cells"] * FLOP_PER_CELL_BLOCK       # cell-ms x flop per cell-block
             out["fullsky"] = {
                 "metric": "acquisition cell-ms/s (full-sky, 10 ms non-coherent)",
                 "value": sky["cells"] * sky["steps"] / sky["dt"], "unit": "cell-ms/s",
@@ -797,6 +986,15 @@ def main():
                           f"x 10 ms non-coherent = {sky['cells']} cell-ms per search; groups "
                           f"sharded round-robin over {W} GPU(s), results gathered over gloo",
                 "planted_found": f"{sky['found']}/{sky['n_planted']}",
+                "dtype": "f64",
+                "roofline": {"bound": "valu", "kernel": "acq64_corr_kernel<PlanA, NONCOHERENT>",
+                             "achieved": sky_flop / (sky_ms * 1e-3) / 1e12 / W,
+                             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64, per GPU)",
+                             "frac": sky_flop / (sky_ms * 1e-3) / 1e12 / W / PEAK_FP64_TFLOPS,
+                             "timing": "whole search per step (forward spectra included): a "
+                                       "lower bound on the correlation kernel's rate",
+                             "traffic": pmc_traffic("acq64_corr_kernel<Plan<16368, 16, 33, 31, "
+                                                    "512, true>, 1, false>")},
             }
         if gco:
             cells = 14 * gco["nb"] * N
@@ -876,6 +1074,8 @@ def main():
                     out["tracking"]["cpu_baseline"] = tb
             if sgt:
                 out["glonass_tracking"]["cpu_baseline"] = cpu_baseline_sgt()
+            if sky:
+                out["fullsky"]["cpu_baseline"] = cpu_baseline_fullsky()
             if sdr:
                 out["sdr_acquisition"]["cpu_baseline"] = cpu_baseline_sdr(sdr["bufs"])
                 for kind in sdr["mw"]:

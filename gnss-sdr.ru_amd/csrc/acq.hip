@@ -31,6 +31,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "acq_ctx.h"
+#include "if2.h"
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -390,12 +391,14 @@ __global__ __launch_bounds__(kFwd1Threads) void acq_fwd16_kernel(
     if (mode == 0) {
       const int cls = row / n_blocks, blk = row % n_blocks;
       const double f = cfreqs[cls];
-      const int8_t* s = src + (long)blk * coh * N * (iq ? 2 : 1);
+      const bool cplx = iq & GNSSCORR_IF_IQ, pk = iq & GNSSCORR_IF_PACKED2;
+      const int ne = cplx ? 2 : 1;
+      const long e0 = (long)blk * coh * N * ne;   // first element of the block
       double re = 0.0, im = 0.0;
       for (int p = 0; p < coh; p++) {
         const int n = n0 + p * N;
-        const double I = iq ? (double)s[2 * n] : (double)s[n];
-        const double Q = iq ? (double)s[2 * n + 1] : 0.0;
+        const double I = (double)if_elem(src, e0 + (long)ne * n, pk);
+        const double Q = cplx ? (double)if_elem(src, e0 + 2L * n + 1, pk) : 0.0;
         // acquisition.sci:61-62, 107: phasePoints = (0:coh*N-1)*2*%pi*ts; exp(i f pp)
         const double th = f * ((((double)n * 2.0) * M_PI) * ts);
         double sn, cs;
@@ -1614,6 +1617,10 @@ static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n
                           int n_freqs, const double* d_freqs) {
   int rc = check_search(c, n_blocks, n_freqs, GNSSCORR_ACQ_BEST_OF_BLOCKS);
   if (rc) return rc;
+  if (iq & ~(GNSSCORR_IF_IQ | GNSSCORR_IF_PACKED2)) {
+    gnsscorr_set_error("gnsscorr_acq: iq must be a set of GNSSCORR_IF_* flags (got %d)", iq);
+    return GNSSCORR_EINVAL;
+  }
   if (c->prec == GNSSCORR_ACQ_F64) {
     rc = acq64_spectra(c, d_if, iq, n_blocks, n_freqs, d_freqs);
     if (rc) return rc;
@@ -1791,7 +1798,10 @@ static int stage_host(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blo
   if ((rc = acq_grow((void**)&c->d_res, &c->cap_res, n_groups, sizeof(gnsscorr_acq_result)))) return rc;
   if ((rc = acq_grow((void**)&c->d_gcode, &c->cap_gcode, n_groups, sizeof(int)))) return rc;
   if ((rc = acq_grow((void**)&c->d_gfreq, &c->cap_gfreq, R, sizeof(int)))) return rc;
-  HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)n_blocks * c->coh * c->cfg.n_samples * (iq ? 2 : 1),
+  HIP_TRY(hipMemcpyAsync(c->d_if, h_if,
+                         (size_t)if_bytes((int64_t)n_blocks * c->coh * c->cfg.n_samples *
+                                              ((iq & GNSSCORR_IF_IQ) ? 2 : 1),
+                                          iq & GNSSCORR_IF_PACKED2),
                          hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_freqs, h_freqs, sizeof(double) * n_freqs, hipMemcpyHostToDevice,
                          c->stream));

@@ -45,6 +45,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "acq_ctx.h"
+#include "if2.h"
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -627,12 +628,14 @@ __global__ __launch_bounds__(256) void acq64_wipe_kernel(
     const int row = (int)(i / N), n = (int)(i % N);
     const int cls = row / n_blocks, blk = row % n_blocks;
     const double f = cfreq[cls];
-    const int8_t* s = src + (long)blk * coh * N * (iq ? 2 : 1);
+    const bool cplx = iq & GNSSCORR_IF_IQ, pk = iq & GNSSCORR_IF_PACKED2;
+    const int ne = cplx ? 2 : 1;
+    const long e0 = (long)blk * coh * N * ne;   // first element of the block
     double re = 0.0, im = 0.0;
     for (int p = 0; p < coh; p++) {
       const long m = n + (long)p * N;
-      const double I = iq ? (double)s[2 * m] : (double)s[m];
-      const double Q = iq ? (double)s[2 * m + 1] : 0.0;
+      const double I = (double)if_elem(src, e0 + ne * m, pk);
+      const double Q = cplx ? (double)if_elem(src, e0 + 2 * m + 1, pk) : 0.0;
       const double th = f * ((((double)m * 2.0) * M_PI) * ts);
       double sn, cs;
       sincos(th, &sn, &cs);

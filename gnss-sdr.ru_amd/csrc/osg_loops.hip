@@ -369,7 +369,7 @@ extern "C" int gnsscorr_osg_closed_loop_dev(gnsscorr_track_ctx* ctx,
     return GNSSCORR_EINVAL;
   }
   hipStream_t s = (hipStream_t)gnsscorr_track_stream(ctx);
-  const int64_t bytes_per_call = nsamp * (gnsscorr_track_iq(ctx) ? 2 : 1);
+  const int64_t bytes_per_call = gnsscorr_track_if_bytes(ctx, nsamp);
   for (int k = 0; k < n_calls; k++) {
     gnsscorr_track_result* r = d_res_hist + (size_t)k * n_ch;
     const int64_t tic = gnsscorr_track_next_tic(ctx, nsamp);

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "gnsscorr_internal.h"
+#include "if2.h"
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -292,7 +293,9 @@ __device__ __forceinline__ int xcd_channel(int b, int G) {
 // staged once in LDS with coalesced 16-byte loads and shared by the cpw
 // channels: each lane's run would otherwise be 8 loads that put every lane on
 // its own cache line (8x the L2 -> CU bytes, once per channel).
-template <bool IQ>
+// PK: the IF streams are GNSSCORR_IF_PACKED2 (if2.h): staged runs are expanded
+// to int8 in LDS; unstaged runs expand per 16-element word in registers.
+template <bool IQ, bool PK>
 __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
     const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp, int n_channels, int cpw,
     const gnsscorr_nco_cmd* __restrict__ cmds, gnsscorr_chan_state* __restrict__ state,
@@ -384,20 +387,50 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
       else if (v != sst) uni = false;
     }
   }
-  const bool stage = IQ && stage_ok && uni && sst >= 0;
+  // stage_ok: 0 no staging; 1 a stream shared by the whole workgroup is
+  // staged once; 2 otherwise each channel stages its own stream in its own slot
+  const bool shared_stage = IQ && stage_ok && uni && sst >= 0;
+  const bool perch_stage = IQ && stage_ok == 2 && !shared_stage;
+  const bool stage = shared_stage || perch_stage;
+  const int slot_chunks = ((nsamp + kRun - 1) / kRun) * kPitch;
+  uint4* s_ifq = s_if + (perch_stage ? q * slot_chunks : 0);
   if (stage) {
-    // full 64-sample runs only; consecutive threads load consecutive 16-byte chunks
-    const int4* g = reinterpret_cast<const int4*>(ifbuf + (int64_t)sst * stream_stride * 2);
-    const int n_full = nsamp / kRun, n_chunks = n_full * (kRun * 2 / 16);
-    for (int ch = threadIdx.x; ch < n_chunks; ch += blockDim.x) {
-      const int4 v = g[ch];
-      s_if[(ch >> 3) * kPitch + (ch & 7)] = make_uint4(v.x, v.y, v.z, v.w);
+    const int n_full = nsamp / kRun;
+    const int st_id = shared_stage ? sst : s_stream[q];
+    const int lt = shared_stage ? (int)threadIdx.x : tid;       // staging lane and width
+    const int nt = shared_stage ? (int)blockDim.x : T;
+    uint32_t* t32 = reinterpret_cast<uint32_t*>(s_ifq + n_full * kPitch);
+    if (st_id >= 0) {
+    if constexpr (!PK) {
+      // full 64-sample runs only; consecutive threads load consecutive 16-byte chunks
+      const int4* g = reinterpret_cast<const int4*>(ifbuf + (int64_t)st_id * stream_stride * 2);
+      const int n_chunks = n_full * (kRun * 2 / 16);
+      for (int ch = lt; ch < n_chunks; ch += nt) {
+        const int4 v = g[ch];
+        s_ifq[(ch >> 3) * kPitch + (ch & 7)] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      // the whole sample pairs of the tail run go to the next slot (an odd last
+      // sample is read from global memory by its lane)
+      const uint32_t* g32 = reinterpret_cast<const uint32_t*>(g) + n_full * (kRun / 2);
+      for (int wi = lt; wi < (nsamp - n_full * kRun) / 2; wi += nt) t32[wi] = g32[wi];
+    } else {
+      // packed: one byte per sample pair; an 8-byte chunk (packed data is
+      // only 8-byte aligned: 1 ms at 16.368 Msps is 8184 bytes) is a quarter
+      // run and expands to two 16-byte int8 chunks (once per workgroup,
+      // shared by its cpw channels)
+      const uint8_t* gb = reinterpret_cast<const uint8_t*>(ifbuf) + (int64_t)st_id * stream_stride / 2;
+      const uint2* g = reinterpret_cast<const uint2*>(gb);
+      const int n_chunks = n_full * 4;
+      for (int ch = lt; ch < n_chunks; ch += nt) {
+        const uint2 v = g[ch];
+        uint4* d = &s_ifq[(ch >> 2) * kPitch + (ch & 3) * 2];
+        d[0] = if2_expand_word(v.x);
+        d[1] = if2_expand_word(v.y);
+      }
+      for (int wi = lt; wi < (nsamp - n_full * kRun) / 2; wi += nt)
+        t32[wi] = if2_expand_byte(gb[n_full * (kRun / 2) + wi]);
     }
-    // the whole sample pairs of the tail run go to the next slot (an odd last
-    // sample is read from global memory by its lane)
-    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(g) + n_full * (kRun / 2);
-    uint32_t* t32 = reinterpret_cast<uint32_t*>(s_if + n_full * kPitch);
-    for (int wi = threadIdx.x; wi < (nsamp - n_full * kRun) / 2; wi += blockDim.x) t32[wi] = g32[wi];
+    }
     __syncthreads();
   }
   TRACK_PSTAMP(2);
@@ -427,58 +460,80 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
       eb = (int)(int8_t)((w >> 16) & 0xFFu);
     }
     constexpr int kBps = IQ ? 2 : 1;
-    const int8_t* src = ifbuf + (int64_t)cmd.stream * stream_stride * kBps + (int64_t)n0 * kBps;
+    // element offset of the run (a multiple of 64: n0 and the stream base are);
+    // src is its first byte in either format
+    const int64_t e_run = ((int64_t)cmd.stream * stream_stride + n0) * kBps;
+    const int8_t* src = PK ? ifbuf + (e_run >> 2) : ifbuf + e_run;
+    const uint8_t* srcb = reinterpret_cast<const uint8_t*>(src);
+    // {I, Q} word of sample k of the run (odd last sample of a tail run)
+    auto single_word = [&](int k) -> uint32_t {
+      if constexpr (PK)
+        return (if2_expand_byte(srcb[k >> 1]) >> (16 * (k & 1))) & 0xFFFFu;
+      else
+        return (uint32_t)srcb[2 * k] | (uint32_t)srcb[2 * k + 1] << 8;
+    };
     if (IQ && pk_lds) {   // (a channel whose half-chip range exceeds the staged row takes
                           //  the per-sample path below, reading the table from global memory)
-      const int4* v = reinterpret_cast<const int4*>(src);
-      constexpr int kVec = kRun * kBps / 16;
+      constexpr int kVec = kRun * 2 / 16;
       const int L = min(kRun, nsamp - n0);
       auto body = [&](auto tb) {
         int si = 0, sq = 0;
-        if (L == kRun || stage) {
+        const int np = L >> 1;
+        // one 16-byte int8 chunk = 4 sample pairs (chunk j of the run)
+        auto chunk = [&](const uint4 u, int j) {
+          const uint32_t words[4] = {u.x, u.y, u.z, u.w};
+          if (4 * j + 4 <= np) {
+#pragma unroll
+            for (int wd = 0; wd < 4; wd++)
+              corr_pair(words[wd], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched,
+                        s_lo, tb);
+          } else {
+            for (int wd = 0; wd < 4; wd++)
+              if (4 * j + wd < np)
+                corr_pair(words[wd], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched,
+                          s_lo, tb);
+          }
+        };
+        if (stage || (!PK && L == kRun)) {
           // one 16-byte chunk (4 pairs) per iteration with the next one in
           // flight: a rolled loop keeps the register footprint small enough
           // for two 1024-thread workgroups per CU.  The tail run (staged in
           // LDS) goes through the same loop with its missing pairs masked, so
           // it does not serialise behind the full runs of its wave.
-          const int np = L >> 1;
-          const uint4* run = stage ? &s_if[tid * kPitch] : reinterpret_cast<const uint4*>(v);
+          const uint4* run = stage ? &s_ifq[tid * kPitch] : reinterpret_cast<const uint4*>(src);
           uint4 nx = run[0];
 #pragma unroll 1
           for (int j = 0; j < kVec; j++) {
             const uint4 u = nx;
             if (j + 1 < kVec) nx = run[j + 1];
-            const uint32_t words[4] = {u.x, u.y, u.z, u.w};
-            if (4 * j + 4 <= np) {
-#pragma unroll
-              for (int wd = 0; wd < 4; wd++)
-                corr_pair(words[wd], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched,
-                          s_lo, tb);
-            } else {
-              for (int wd = 0; wd < 4; wd++)
-                if (4 * j + wd < np)
-                  corr_pair(words[wd], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first,
-                            switched, s_lo, tb);
-            }
+            chunk(u, j);
           }
-          if (L & 1)
-            corr_single((uint32_t)(uint8_t)src[2 * (L - 1)] |
-                            (uint32_t)(uint8_t)src[2 * (L - 1) + 1] << 8,
-                        phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched, s_lo, tb);
+        } else if (PK && L == kRun) {
+          // packed, unstaged (channels of a workgroup on different streams):
+          // the run is 32 bytes (8-byte aligned), each 4-byte word expands
+          // to one int8 chunk
+          const uint2* prun = reinterpret_cast<const uint2*>(src);
+          uint2 nx = prun[0];
+#pragma unroll 1
+          for (int h = 0; h < 4; h++) {
+            const uint2 p = nx;
+            if (h + 1 < 4) nx = prun[h + 1];
+            chunk(if2_expand_word(p.x), 2 * h);
+            chunk(if2_expand_word(p.y), 2 * h + 1);
+          }
         } else {   // tail run without staging (one lane): same arithmetic, word loads
           const uint32_t* w32 = reinterpret_cast<const uint32_t*>(src);
-          for (int k = 0; k < (L >> 1); k++)
-            corr_pair(w32[k], phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched, s_lo,
-                      tb);
-          if (L & 1)
-            corr_single((uint32_t)(uint8_t)src[2 * (L - 1)] |
-                            (uint32_t)(uint8_t)src[2 * (L - 1) + 1] << 8,
-                        phase, kph, c, hc, lb, pb, eb, si, sq, cur, first, switched, s_lo, tb);
+          for (int k = 0; k < np; k++)
+            corr_pair(PK ? if2_expand_byte(srcb[k]) : w32[k], phase, kph, c, hc, lb, pb, eb, si,
+                      sq, cur, first, switched, s_lo, tb);
         }
+        if (L & 1)
+          corr_single(single_word(L - 1), phase, kph, c, hc, lb, pb, eb, si, sq, cur, first,
+                      switched, s_lo, tb);
         seg_flush(si, sq, lb, pb, eb, cur);
       };
       body(s_pk8);
-    } else if (n0 + kRun <= nsamp) {
+    } else if (!PK && n0 + kRun <= nsamp) {
       const int4* v = reinterpret_cast<const int4*>(src);
       constexpr int kVec = kRun * kBps / 16;
 #pragma unroll
@@ -501,10 +556,11 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
           }
         }
       }
-    } else {
-      for (int n = n0; n < nsamp; n++) {
-        const int I = src[(n - n0) * kBps];
-        const int Q = IQ ? src[(n - n0) * kBps + 1] : 0;
+    } else {   // per sample (tail runs; every packed run off the fast path)
+      const int L = min(kRun, nsamp - n0);
+      for (int k = 0; k < L; k++) {
+        const int I = if_elem(src, (int64_t)k * kBps, PK);
+        const int Q = IQ ? if_elem(src, (int64_t)k * kBps + 1, PK) : 0;
         corr_sample<IQ>(I, Q, phase, kph, c, hc, lb, pb, eb, cur, first, switched, pk);
       }
     }
@@ -628,9 +684,17 @@ struct gnsscorr_track_ctx {
   int max_dumps = 0;
   int64_t tic = 0, tic_ref = 0;
   int stage_if = 1;   // GNSSCORR_TRACK_STAGE_IF=0: lanes read their IF runs from global memory
+  int cpw_override = 0;   // GNSSCORR_TRACK_CPW: channels per workgroup
+  int stage_perch = 0;    // GNSSCORR_TRACK_STAGE_PERCH=1: channels on different streams stage their own
 };
 
-extern "C" int gnsscorr_track_iq(const gnsscorr_track_ctx* ctx) { return ctx && ctx->cfg.iq; }
+extern "C" int gnsscorr_track_iq(const gnsscorr_track_ctx* ctx) { return ctx && (ctx->cfg.iq & GNSSCORR_IF_IQ); }
+static bool packed(const gnsscorr_track_ctx* c) { return (c->cfg.iq & GNSSCORR_IF_PACKED2) != 0; }
+static int bps_of(const gnsscorr_track_ctx* c) { return (c->cfg.iq & GNSSCORR_IF_IQ) ? 2 : 1; }
+// bytes of `samples` consecutive samples of one stream in the context's format
+extern "C" int64_t gnsscorr_track_if_bytes(const gnsscorr_track_ctx* c, int64_t samples) {
+  return if_bytes(samples * bps_of(c), packed(c));
+}
 
 static int set_dev(int dev) {
   HIP_TRY(hipSetDevice(dev));
@@ -638,9 +702,10 @@ static int set_dev(int dev) {
 }
 
 extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_track_cfg* cfg) {
-  if (!out || !cfg || cfg->n_channels < 1 || cfg->max_nsamp < 1 || cfg->max_nsamp > kMaxNsamp) {
-    gnsscorr_set_error("gnsscorr_track_create: bad config (n_channels>=1, 1<=max_nsamp<=%d)",
-                       kMaxNsamp);
+  if (!out || !cfg || cfg->n_channels < 1 || cfg->max_nsamp < 1 || cfg->max_nsamp > kMaxNsamp ||
+      (cfg->iq & ~(GNSSCORR_IF_IQ | GNSSCORR_IF_PACKED2))) {
+    gnsscorr_set_error("gnsscorr_track_create: bad config (n_channels>=1, 1<=max_nsamp<=%d, "
+                       "iq = GNSSCORR_IF_* flags)", kMaxNsamp);
     return GNSSCORR_EINVAL;
   }
   *out = nullptr;
@@ -661,6 +726,8 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   c->tic_ref = (int64_t)(cfg->samp_rate * cfg->tic_period);
   c->tic = c->tic_ref;
   if (const char* e = getenv("GNSSCORR_TRACK_STAGE_IF")) c->stage_if = atoi(e) != 0;
+  if (const char* e = getenv("GNSSCORR_TRACK_CPW")) c->cpw_override = atoi(e);
+  if (const char* e = getenv("GNSSCORR_TRACK_STAGE_PERCH")) c->stage_perch = atoi(e) != 0;
   const int C = cfg->n_channels;
   auto fail = [&](int code) {
     gnsscorr_track_destroy(c);
@@ -728,29 +795,46 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
     gnsscorr_set_error("nsamp %lld outside [1, max_nsamp=%d]", (long long)nsamp, c->cfg.max_nsamp);
     return GNSSCORR_EINVAL;
   }
-  const int bps = c->cfg.iq ? 2 : 1;
-  if (((uintptr_t)d_if & 15) || ((stride * bps) & 15)) {
-    gnsscorr_set_error("IF base and stream stride must be 16-byte aligned");
+  const int bps = bps_of(c);
+  const bool pk = packed(c), iq = bps == 2;
+  // 16-byte aligned int8 runs; packed runs are read in 8-byte words
+  if (((uintptr_t)d_if & (pk ? 7 : 15)) || ((stride * bps) & (pk ? 31 : 15))) {
+    gnsscorr_set_error("IF base and stream stride must be %d-byte aligned", pk ? 8 : 16);
     return GNSSCORR_EINVAL;
   }
   int threads = (int)((nsamp + kRun - 1) / kRun);
   threads = (threads + 63) & ~63;
-  const int cpw = min(kMaxCpw, kMaxThreads / threads);
   const int C = c->cfg.n_channels;
-  dim3 grid((C + cpw - 1) / cpw), block(threads * cpw);
   const size_t stage_bytes = (size_t)((nsamp + kRun - 1) / kRun) * kPitch * 16;
-  const int stage = c->cfg.iq && c->stage_if && stage_bytes <= (size_t)kStageMaxBytes;
+  int stage = iq && c->stage_if && stage_bytes <= (size_t)kStageMaxBytes;
+  if (stage && c->stage_perch) stage = 2;
   // dynamic LDS: epoch sums, E/P/L row bytes, staged IF (kernel layout)
-  const size_t sum_bytes = (size_t)((cpw * ((int)nsamp / GNSSCORR_OSG_ROW + 2) * 6 + 3) & ~3) * 4;
-  const size_t dyn = sum_bytes + (c->cfg.iq ? (size_t)cpw * kPk8Stage + (stage ? stage_bytes : 0) : 0);
-  if (c->cfg.iq)
-    hipLaunchKernelGGL(osg_track_kernel<true>, grid, block, dyn, c->stream, d_if, stride,
-                       (int)nsamp, C, cpw, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps,
-                       c->d_pk, c->d_pk8, tic_count, stage);
+  auto lds_bytes = [&](int cpw) {
+    const size_t sum_bytes = (size_t)((cpw * ((int)nsamp / GNSSCORR_OSG_ROW + 2) * 6 + 3) & ~3) * 4;
+    return sum_bytes + (iq ? (size_t)cpw * kPk8Stage + (stage ? stage_bytes * (stage == 2 ? cpw : 1) : 0) : 0);
+  };
+  // Channels per workgroup: as many as fit 1024 threads (they share one staged
+  // IF copy).  The 1.5-round tail at 3072 channels (768 workgroups, 512
+  // resident) is cheaper than smaller workgroups (MI355X, 3072 x 1 ms:
+  // cpw 4 33.4 us, 3 35.2, 2 34.1, 1 46.4); GNSSCORR_TRACK_CPW overrides.
+  int cpw = min(kMaxCpw, kMaxThreads / threads);
+  if (c->cpw_override > 0) cpw = min(cpw, c->cpw_override);
+  if (stage == 2 && lds_bytes(cpw) + 1024 > 160 * 1024) stage = 1;   // per-channel slots must fit
+  dim3 grid((C + cpw - 1) / cpw), block(threads * cpw);
+  const size_t dyn = lds_bytes(cpw);
+#define TRACK_LAUNCH(IQ, PK, ST)                                                               \
+  hipLaunchKernelGGL((osg_track_kernel<IQ, PK>), grid, block, dyn, c->stream, d_if, stride,    \
+                     (int)nsamp, C, cpw, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps,     \
+                     c->d_pk, c->d_pk8, tic_count, ST)
+  if (iq && pk)
+    TRACK_LAUNCH(true, true, stage);
+  else if (iq)
+    TRACK_LAUNCH(true, false, stage);
+  else if (pk)
+    TRACK_LAUNCH(false, true, 0);
   else
-    hipLaunchKernelGGL(osg_track_kernel<false>, grid, block, dyn, c->stream, d_if, stride,
-                       (int)nsamp, C, cpw, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps,
-                       c->d_pk, c->d_pk8, tic_count, 0);
+    TRACK_LAUNCH(false, false, 0);
+#undef TRACK_LAUNCH
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
@@ -778,10 +862,16 @@ extern "C" int gnsscorr_track(gnsscorr_track_ctx* c, const int8_t* h_if, int64_t
   }
   int rc = set_dev(c->cfg.device);
   if (rc) return rc;
-  const int bps = c->cfg.iq ? 2 : 1;
-  // device copy with a 16-byte aligned stride
-  const int64_t dstride = n_streams > 1 ? ((stride * bps + 15) & ~15LL) / bps : 0;
-  const size_t need = (size_t)((n_streams - 1) * dstride + ((nsamp * bps + 15) & ~15LL) / bps) * bps;
+  const int bps = bps_of(c);
+  const bool pk = packed(c);
+  if (pk && n_streams > 1 && (stride * bps) & 3) {
+    gnsscorr_set_error("gnsscorr_track: packed streams need a whole-byte stream stride");
+    return GNSSCORR_EINVAL;
+  }
+  // device copy with an aligned stride (16 int8 bytes / 8 packed bytes = 32 elements)
+  const int64_t al = pk ? 32 : 16;
+  const int64_t dstride = n_streams > 1 ? ((stride * bps + al - 1) & ~(al - 1)) / bps : 0;
+  const size_t need = (size_t)if_bytes((n_streams - 1) * dstride * bps + ((nsamp * bps + al - 1) & ~(al - 1)), pk);
   if (need > c->if_cap) {
     if (c->d_if) (void)hipFree(c->d_if);
     c->d_if = nullptr;
@@ -790,11 +880,11 @@ extern "C" int gnsscorr_track(gnsscorr_track_ctx* c, const int8_t* h_if, int64_t
     c->if_cap = need;
   }
   if (n_streams == 1 || dstride == stride) {
-    HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)((n_streams - 1) * stride + nsamp) * bps,
+    HIP_TRY(hipMemcpyAsync(c->d_if, h_if, (size_t)if_bytes(((n_streams - 1) * stride + nsamp) * bps, pk),
                            hipMemcpyHostToDevice, c->stream));
   } else {
-    HIP_TRY(hipMemcpy2DAsync(c->d_if, dstride * bps, h_if, stride * bps, nsamp * bps, n_streams,
-                             hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpy2DAsync(c->d_if, if_bytes(dstride * bps, pk), h_if, if_bytes(stride * bps, pk),
+                             if_bytes(nsamp * bps, pk), n_streams, hipMemcpyHostToDevice, c->stream));
   }
   HIP_TRY(hipMemcpyAsync(c->d_cmds, h_cmds, sizeof(gnsscorr_nco_cmd) * C, hipMemcpyHostToDevice,
                          c->stream));
@@ -835,11 +925,11 @@ extern "C" int gnsscorr_track_replay_dev(gnsscorr_track_ctx* c, const int8_t* d_
   }
   int rc = set_dev(c->cfg.device);
   if (rc) return rc;
-  const int bps = c->cfg.iq ? 2 : 1;
   const int C = c->cfg.n_channels;
   for (int k = 0; k < n_steps; k++) {
     const int64_t tic = gnsscorr_track_next_tic(c, nsamp);
-    rc = launch(c, d_if + (int64_t)k * nsamp * bps, stride, nsamp, d_cmds + (int64_t)k * C,
+    rc = launch(c, d_if + gnsscorr_track_if_bytes(c, (int64_t)k * nsamp), stride, nsamp,
+                d_cmds + (int64_t)k * C,
                 d_res + (int64_t)k * C, nullptr, tic);
     if (rc) return rc;
   }

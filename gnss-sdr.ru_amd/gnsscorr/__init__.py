@@ -112,6 +112,8 @@ SDR_ACQ_MS = {0: 1, 1: 10, 2: 310}                       # ms per request (acqui
 SDR_RESULT = np.dtype([("sv", "<i4"), ("code_phase", "<i4"), ("doppler", "<i4"),
                        ("magnitude", "<u4"), ("success", "<i4"), ("row", "<i4")])
 
+IF_IQ = 1        # GNSSCORR_IF_IQ: interleaved I,Q
+IF_PACKED2 = 2   # GNSSCORR_IF_PACKED2: 2-bit codes, 4 elements per byte (GN3S LUT {-3,-1,1,3})
 ACQ_BEST_OF_BLOCKS = 0
 ACQ_NONCOHERENT = 1
 ACQ_F64 = 0      # reference precision (acquisition.sci evaluates in doubles)
@@ -152,6 +154,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
     "gnsscorr_device_pci_bus_id",
     "gnsscorr_track_create", "gnsscorr_track_destroy", "gnsscorr_track_max_dumps",
+    "gnsscorr_pack2", "gnsscorr_track_if_bytes",
     "gnsscorr_track", "gnsscorr_track_dev", "gnsscorr_track_next_tic",
     "gnsscorr_track_replay_dev", "gnsscorr_track_get_state", "gnsscorr_track_set_state",
     "gnsscorr_track_sync", "gnsscorr_track_stream",
@@ -212,6 +215,8 @@ def lib() -> C.CDLL:
         "gnsscorr_track": (I, [P, P, I64, I, I64, P, P, P, C.POINTER(I)]),
         "gnsscorr_track_dev": (I, [P, P, I64, I64, P, P, P, I64]),
         "gnsscorr_track_next_tic": (I64, [P, I64]),
+        "gnsscorr_track_if_bytes": (I64, [P, I64]),
+        "gnsscorr_pack2": (I, [P, I64, P]),
         "gnsscorr_track_replay_dev": (I, [P, P, I64, I64, I, P, P]),
         "gnsscorr_track_get_state": (I, [P, P]),
         "gnsscorr_track_set_state": (I, [P, P]),
@@ -309,6 +314,26 @@ def _check(rc: int, what: str) -> None:
 
 def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
+
+
+def _if_bytes(a) -> np.ndarray:
+    """IF samples as the C ABI's int8 byte buffer (packed data may come as uint8)."""
+    a = np.ascontiguousarray(a)
+    return a.view(np.int8) if a.dtype == np.uint8 else np.ascontiguousarray(a, np.int8)
+
+
+def iq_flags(iq, packed=False) -> int:
+    """The `iq` argument of the C ABI: GNSSCORR_IF_* flags (iq may already be flags)."""
+    f = int(iq)
+    return f | IF_PACKED2 if packed else f
+
+
+def pack2(levels) -> np.ndarray:
+    """int8 levels in {-3,-1,1,3} -> GNSSCORR_IF_PACKED2 bytes (gnsscorr_pack2)."""
+    lv = np.ascontiguousarray(levels, np.int8).ravel()
+    out = np.empty((lv.size + 3) // 4, np.uint8)
+    _check(lib().gnsscorr_pack2(_ptr(lv), lv.size, _ptr(out)), "gnsscorr_pack2")
+    return out
 
 
 def device_count() -> int:
@@ -451,10 +476,12 @@ class TrackCtx:
 
     def __init__(self, n_channels: int, iq: bool = True, device: int = 0,
                  max_nsamp: int = 65536, samp_rate: float = 16.368e6,
-                 tic_period: float = 0.0):
+                 tic_period: float = 0.0, packed: bool = False):
         self.n_channels = n_channels
-        self.iq = bool(iq)
-        cfg = TrackCfg(n_channels, int(iq), device, max_nsamp, samp_rate, tic_period)
+        self.iq = bool(int(iq) & IF_IQ)
+        self.packed = bool(packed or int(iq) & IF_PACKED2)
+        cfg = TrackCfg(n_channels, iq_flags(self.iq, self.packed), device, max_nsamp, samp_rate,
+                       tic_period)
         h = C.c_void_p()
         _check(lib().gnsscorr_track_create(C.byref(h), C.byref(cfg)), "gnsscorr_track_create")
         self.h = h
@@ -469,7 +496,7 @@ class TrackCtx:
 
     def track(self, if_samples: np.ndarray, nsamp: int, cmds: np.ndarray, n_streams: int = 1,
               stream_stride: int = 0, all_dumps: bool = False):
-        if_samples = np.ascontiguousarray(if_samples, np.int8)
+        if_samples = _if_bytes(if_samples)
         cmds = np.ascontiguousarray(cmds, NCO_CMD)
         assert len(cmds) == self.n_channels
         res = np.zeros(self.n_channels, TRACK_RESULT)
@@ -490,6 +517,10 @@ class TrackCtx:
                    d_res: int):
         _check(lib().gnsscorr_track_replay_dev(self.h, d_if, stream_stride, nsamp, n_steps,
                                                d_cmds, d_res), "gnsscorr_track_replay_dev")
+
+    def if_bytes(self, samples: int) -> int:
+        """Bytes of `samples` samples of one stream in this context's format."""
+        return int(lib().gnsscorr_track_if_bytes(self.h, samples))
 
     def next_tic(self, nsamp: int) -> int:
         return int(lib().gnsscorr_track_next_tic(self.h, nsamp))
@@ -540,7 +571,7 @@ class AcqCtx:
 
     def search(self, if_samples, n_blocks, freqs, group_code, group_freq, spc=16, iq=True,
                mode=ACQ_BEST_OF_BLOCKS):
-        if_samples = np.ascontiguousarray(if_samples, np.int8)
+        if_samples = _if_bytes(if_samples)
         freqs = np.ascontiguousarray(freqs, np.float64)
         group_code = np.ascontiguousarray(group_code, np.int32)
         group_freq = np.ascontiguousarray(group_freq, np.int32).reshape(len(group_code), -1)
@@ -579,7 +610,7 @@ class AcqCtx:
                                              d_rows, d_res), "gnsscorr_acq_select_dev")
 
     def power_row(self, if_samples, n_blocks, block, freq, code, iq=True) -> np.ndarray:
-        if_samples = np.ascontiguousarray(if_samples, np.int8)
+        if_samples = _if_bytes(if_samples)
         out = np.empty(self.n, np.float64)
         _check(lib().gnsscorr_acq_power_row(self.h, _ptr(if_samples), int(iq), n_blocks, block,
                                             freq, code, _ptr(out)), "gnsscorr_acq_power_row")

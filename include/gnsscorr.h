@@ -43,6 +43,29 @@ int gnsscorr_device_count(void);
 int gnsscorr_device_pci_bus_id(int device, char *buf, int len);
 
 /* ======================================================================
+ * IF sample formats.  Every batched entry point that takes IF samples has an
+ * `iq` argument (or gnsscorr_track_cfg.iq): a set of these flags.
+ *   0                      int8 real samples, one byte each
+ *   GNSSCORR_IF_IQ         int8 interleaved I,Q (two bytes per sample)
+ *   | GNSSCORR_IF_PACKED2  2-bit codes, four elements per byte: element e of a
+ *                          stream (I,Q,I,Q,... when complex) in bits
+ *                          2*(e%4)..2*(e%4)+1 of byte e/4; code c is the level
+ *                          2c-3, the GN3S LUT {-3,-1,1,3} of GPS_Source::Read_GN3S
+ *                          (REALTIME_RECEIVERS/GPS/GPS_SDR_REAL_TIME_GPS_RECEIVER/
+ *                          objects/gps_source.cpp:692).  Results equal the int8
+ *                          path on the unpacked levels; HBM and PCIe bytes are 1/4.
+ * Strides and sample counts stay in samples; byte offsets of packed data are
+ * element offsets / 4 (stream strides must make them whole 16-byte multiples
+ * on the device).
+ * ==================================================================== */
+#define GNSSCORR_IF_IQ      1
+#define GNSSCORR_IF_PACKED2 2
+/* Host helper: pack n int8 levels in {-3,-1,1,3} into (n+3)/4 bytes of
+ * GNSSCORR_IF_PACKED2 codes.  Returns GNSSCORR_EINVAL (and packs nothing) if a
+ * value is not one of the four levels. */
+int gnsscorr_pack2(const int8_t *h_in, int64_t n, uint8_t *h_out);
+
+/* ======================================================================
  * Tracking correlator (GP2021 integer semantics)
  * Replaces: Sim_GP2021_int, osgnss_next_step/src/correlator/correlator.c:148-316
  * ==================================================================== */
@@ -53,8 +76,8 @@ typedef struct gnsscorr_track_ctx gnsscorr_track_ctx;
 
 typedef struct {
   int    n_channels;     /* channels in this context (any number >= 1)           */
-  int    iq;             /* 1: interleaved int8 I,Q (use_iq_processing=1, globals.h:56)
-                            0: int8 I only                                       */
+  int    iq;             /* GNSSCORR_IF_* flags: IQ = interleaved I,Q (use_iq_processing=1,
+                            globals.h:56), else I only; | PACKED2 = 2-bit codes   */
   int    device;         /* HIP device ordinal                                    */
   int    max_nsamp;      /* largest nsamp per call (sizes the dump buffers)       */
   double samp_rate;      /* Hz, only used for tic_ref (correlator.c:124)          */
@@ -118,6 +141,8 @@ int gnsscorr_track(gnsscorr_track_ctx *ctx, const int8_t *h_if, int64_t stream_s
 int gnsscorr_track_dev(gnsscorr_track_ctx *ctx, const int8_t *d_if, int64_t stream_stride,
                        int64_t nsamp, const gnsscorr_nco_cmd *d_cmds,
                        gnsscorr_track_result *d_res, int32_t *d_all_dumps, int64_t tic_count);
+/* Bytes of `samples` consecutive samples of one stream in the context's format. */
+int64_t gnsscorr_track_if_bytes(const gnsscorr_track_ctx *ctx, int64_t samples);
 /* Advances the context's TIC counter by nsamp (correlator.c:155-165) and
  * returns the TIC sample index for that call, or -1. */
 int64_t gnsscorr_track_next_tic(gnsscorr_track_ctx *ctx, int64_t nsamp);
@@ -259,8 +284,8 @@ int gnsscorr_acq_destroy(gnsscorr_acq_ctx *ctx);
  * the device and kept resident. */
 int gnsscorr_acq_set_codes(gnsscorr_acq_ctx *ctx, int n_codes, const int8_t *h_codes);
 
-/* Search.  IF: n_blocks consecutive blocks of n_samples complex samples,
- * interleaved int8 I,Q (iq=1) or int8 real (iq=0).  freqs: n_freqs carrier
+/* Search.  IF: n_blocks consecutive blocks of n_samples samples, format
+ * `iq` (GNSSCORR_IF_* flags: interleaved I,Q or real, int8 or 2-bit packed).  freqs: n_freqs carrier
  * frequencies [Hz] (wipe-off exp(i*2*pi*f*t), t = n/fs).  Groups: n_groups
  * searches, each of n_bins rows: group g uses code group_code[g] and
  * frequency index group_freq[g*n_bins + b] for bin b.

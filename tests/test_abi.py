@@ -64,3 +64,18 @@ def test_product_has_no_oracle_dependency(gc):
     so = open(gc.LIB_PATH, "rb").read()
     for needle in (b"osgo_", b"liboracle", b"libosg_ref", b"ref_harness"):
         assert needle not in so
+
+
+def test_pack2_layout(gc):
+    """GNSSCORR_IF_PACKED2 packing (host): element e in bits 2(e%4) of byte e/4,
+    code c = (level+3)/2 -- the inverse of the GN3S LUT {-3,-1,1,3}
+    (GPS_SDR_REAL_TIME_GPS_RECEIVER/objects/gps_source.cpp:692)."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    lv = rng.choice(np.array([-3, -1, 1, 3], np.int8), 4 * 1000 + 3)
+    got = gc.pack2(lv)
+    codes = np.concatenate([(lv.astype(np.int16) + 3) // 2, np.zeros(1, np.int16)])
+    want = (codes[0::4] | codes[1::4] << 2 | codes[2::4] << 4 | codes[3::4] << 6).astype(np.uint8)
+    assert np.array_equal(got, want)
+    with pytest.raises(gc.GnssCorrError):
+        gc.pack2(np.array([1, 0, 3], np.int8))     # 0 is not a 2-bit level

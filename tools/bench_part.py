@@ -9,4 +9,6 @@ part = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 d = bench.Dist()
 r = getattr(bench, "run_" + part)(d, 0, steps, 3)
-print({k: v for k, v in r.items() if isinstance(v, (int, float, str))})
+import json  # noqa: E402
+print(json.dumps({k: v for k, v in r.items() if isinstance(v, (int, float, str, dict))},
+                 default=str))
