@@ -212,6 +212,42 @@ __device__ __forceinline__ void dft_prime(v2d (&x)[P]) {
   }
   x[0] = X0;
 }
+// symmetric prime DFT fused with |.|^2 * scale: pw[k] = |X_k|^2 scale (ACC:
+// added to pw).  Outputs are folded into the powers as each (m, P-m) pair is
+// formed, so the complex outputs are never all live (register pressure of the
+// non-coherent kernel, whose running sums stay live across the transform).
+template <int P, bool ACC>
+__device__ __forceinline__ void dft_prime_power(v2d (&x)[P], double (&pw)[P], double scale) {
+  constexpr int H = (P - 1) / 2;
+#pragma unroll
+  for (int j = 1; j <= H; j++) {
+    const v2d a = x[j], b = x[P - j];
+    x[j] = a + b;        // s_j
+    x[P - j] = a - b;    // d_j
+  }
+  v2d X0 = x[0];
+#pragma unroll
+  for (int j = 1; j <= H; j++) X0 += x[j];
+  auto put = [&](int k, v2d v) {
+    const double p = fma(v.x, v.x, v.y * v.y) * scale;
+    pw[k] = ACC ? pw[k] + p : p;
+  };
+#pragma unroll
+  for (int m = 1; m <= H; m++) {
+    v2d A = x[0], B = (v2d){0.0, 0.0};
+#pragma unroll
+    for (int j = 1; j <= H; j++) {
+      const int q = (j * m) % P;
+      const double c = kTw<P>.c[q], sn = kTw<P>.s[q];
+      A = (v2d){fma(c, x[j].x, A.x), fma(c, x[j].y, A.y)};
+      B = (v2d){fma(sn, x[P - j].x, B.x), fma(sn, x[P - j].y, B.y)};
+    }
+    put(m, (v2d){A.x + B.y, A.y - B.x});       // A - iB
+    put(P - m, (v2d){A.x - B.y, A.y + B.x});   // A + iB
+  }
+  put(0, X0);
+}
+
 // Good-Thomas R = A * B, gcd(A, B) = 1: n = (a B + b A) mod R, k = CRT(ka, kb)
 template <int A, int B>
 __device__ __forceinline__ void dft_pfa(v2d (&x)[A * B]) {
@@ -304,7 +340,17 @@ struct Plan {
   static constexpr int E2 = PFA ? (int)((long)Q2 * INV2 % N) : 0;
   static constexpr int E3 = PFA ? (int)((long)Q3 * INV3 % N) : 0;
   static_assert(R1 * R2 * R3 == N, "plan factors");
-  static_assert(L * R3 <= T, "leftover stage-3 outputs must fit one per thread");
+  static_assert(L * R3 <= T, "leftover stage-3 inputs must fit one per thread");
+  // leftover stage-3 groups run as symmetric tasks (group, m), m = 0..(R3-1)/2:
+  // task t computes outputs m and R3-m (m > 0) of group K3*T + t % L
+  static constexpr int LT = L * ((R3 + 1) / 2);
+  static_assert(LT <= T, "leftover tasks must fit one per thread");
+  __device__ static __forceinline__ bool lvalid(int t, int j) {
+    return t < LT && (j == 0 || t >= L);
+  }
+  __device__ static __forceinline__ int lslot(int t, int j) {
+    return j == 0 ? t / L : R3 - t / L;
+  }
   static_assert(!PFA || (cgcd(R1, R2) == 1 && cgcd(R1, R3) == 1 && cgcd(R2, R3) == 1),
                 "PFA needs coprime factors");
   // Code spectra are spectra of real sequences, F[-k] = conj(F[k]).  In PFA
@@ -331,9 +377,14 @@ struct Plan {
   // stage-1 group of slot j of thread t (SYM: the pair (g, -g)), -1 if none
   __device__ static __forceinline__ int group1(int t, int j) {
     if constexpr (SYM) {
+      // slot 0 takes whole rows n2 = 1..16 (every n3) and row 0's n3 = 1..15;
+      // the mirrors (rows 32..17, row 0's n3 = 30..16) are slot 1.  A wave's
+      // slot-0 (and slot-1) groups are then ~2 consecutive 31-group rows:
+      // each of its 16-byte loads covers ~1 KB of contiguous storage
+      // (circularly shifted by the bin), not ~5 runs of 15 groups
       int g;
-      if (t < 495) g = (t / 15) * R3 + 1 + t % 15;    // n3 = 1..15, every n2
-      else if (t < 511) g = (t - 494) * R3;           // n3 = 0, n2 = 1..16
+      if (t < 496) g = (1 + t / R3) * R3 + t % R3;    // n2 = 1..16, n3 = 0..30
+      else if (t < 511) g = t - 495;                  // n2 = 0, n3 = 1..15
       else g = t == 511 ? 0 : -1;                     // group 0 pairs with itself
       if (j == 0 || g <= 0) return j == 0 ? g : -1;
       const int n2 = g / R3, n3 = g % R3;
@@ -417,17 +468,17 @@ __device__ __forceinline__ void set_part(v2d& v, int p, double d) {
 }
 
 // The transform from stage-1 inputs v1 (loaded by the caller) to stage-3
-// outputs v3 (main groups g3 = t + j*T) and vl (leftover output t < L*R3:
-// slot t % R3 of group K3*T + t / R3).  lds: N doubles; side: LS complex;
+// outputs v3 (main groups g3 = t + j*T) and vl[j] (leftover outputs where
+// P::lvalid(t, j): slot P::lslot(t, j) of group K3*T + t % L).  lds: N doubles; side: LS complex;
 // tw3: W_R3^q, q < R3 (LDS); twN: W_N^j (global, CT plans only).
 struct NoHook {
   __device__ void operator()() const {}
 };
-template <class P, class Hook = NoHook>
+template <class P, class Hook = NoHook, bool kStage3 = true>
 __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
                                          const v2d* __restrict__ twN, int t,
                                          v2d (&v1)[P::K1][P::R1], v2d (&v3)[P::K3][P::R3],
-                                         v2d& vl, const Hook& before_exchange = Hook()) {
+                                         v2d (&vl)[2], const Hook& before_exchange = Hook()) {
   constexpr int R1 = P::R1, R2 = P::R2, R3 = P::R3, T = P::T, G1 = P::G1, G2 = P::G2;
   const bool act = t < T;
   // ---- stage 1
@@ -496,28 +547,37 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       for (int n3 = 0; n3 < R3; n3++) set_part(v3[j][n3], p, lds[g3 * R3 + n3]);
     }
     if constexpr (P::L > 0) {
-      if (t < P::L * R3) set_part(vl, p, lds[P::K3 * T * R3 + t]);
-      if (p == 1 && t < P::L * R3) side[t] = vl;
+      if (t < P::L * R3) set_part(vl[0], p, lds[P::K3 * T * R3 + t]);
+      if (p == 1 && t < P::L * R3) side[t] = vl[0];
     }
     __syncthreads();
     ACQ64_STAMP(6 + 2 * p);
   }
-  // ---- stage 3
+  // ---- stage 3 (main groups: left to the caller when !kStage3)
+  if constexpr (kStage3) {
 #pragma unroll
-  for (int j = 0; j < P::K3; j++) dft<R3>(v3[j]);
+    for (int j = 0; j < P::K3; j++) dft<R3>(v3[j]);
+  }
   if constexpr (P::L > 0) {
-    if (t < P::L * R3) {
-      const int lg = t / R3, m = t % R3;
+    // leftover groups: the symmetric prime DFT (dft_prime) split by output
+    // pair, inputs from the side copy, W^(jm) from the tw3 table (cos, -sin)
+    if (t < P::LT) {
+      constexpr int H = (R3 - 1) / 2;
+      const int lg = t % P::L, m = t / P::L;
       const v2d* x = side + lg * R3;
-      v2d acc = (v2d){0.0, 0.0};
-      int q = 0;
+      v2d A = x[0], B = (v2d){0.0, 0.0};
+      int q = m;
 #pragma unroll
-      for (int n = 0; n < R3; n++) {
-        acc += cmul(x[n], tw3[q]);
+      for (int j = 1; j <= H; j++) {
+        const v2d a = x[j], b = x[R3 - j], w = tw3[q];
+        const v2d sj = a + b, dj = a - b;
+        A = (v2d){fma(w.x, sj.x, A.x), fma(w.x, sj.y, A.y)};
+        B = (v2d){fma(-w.y, dj.x, B.x), fma(-w.y, dj.y, B.y)};
         q += m;
-        if (q >= R3) q -= R3;
+        q -= q >= R3 ? R3 : 0;
       }
-      vl = acc;
+      vl[0] = (v2d){A.x + B.y, A.y - B.x};   // A - iB
+      vl[1] = (v2d){A.x - B.y, A.y + B.x};   // A + iB (slot R3 - m)
     }
   }
 }
@@ -529,17 +589,60 @@ __device__ __forceinline__ void init_tw3(v2d* tw3) {
 }
 
 // ---- workgroup reductions --------------------------------------------------------
+// Wave step: DPP row_shr 1/2/4/8 (a Hillis-Steele scan inside each 16-lane row,
+// the identity shifted in) leaves each row's result in its lane 15; the four
+// rows combine in scalar registers.  VALU only: no ds_bpermute round trips
+// (a 64-bit __shfl_xor is two LDS-crossbar operations per step).  Every lane
+// of the wave must be active.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double ident, double v) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(ident), __double2loint(v), CTRL, 0xF,
+                                             0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(ident), __double2hiint(v), CTRL, 0xF,
+                                             0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 __device__ __forceinline__ bool better(double v1, int k1, double v0, int k0) {
   return v1 > v0 || (v1 == v0 && k1 < k0);
 }
+template <int CTRL>
+__device__ __forceinline__ void argmax_step(double& v, int& k) {
+  const double v2 = dpp_f64<CTRL>(-1.0, v);
+  const int k2 = __builtin_amdgcn_update_dpp(INT_MAX, k, CTRL, 0xF, 0xF, false);
+  if (better(v2, k2, v, k)) { v = v2; k = k2; }
+}
+// argmax (largest value, first index on ties) of the wave; uniform result
+__device__ __forceinline__ void wave_argmax(double& v, int& k) {
+  argmax_step<0x111>(v, k);
+  argmax_step<0x112>(v, k);
+  argmax_step<0x114>(v, k);
+  argmax_step<0x118>(v, k);
+  double bv = readlane_f64(v, 15);
+  int bk = __builtin_amdgcn_readlane(k, 15);
+#pragma unroll
+  for (int r = 31; r < 64; r += 16) {
+    const double v2 = readlane_f64(v, r);
+    const int k2 = __builtin_amdgcn_readlane(k, r);
+    if (better(v2, k2, bv, bk)) { bv = v2; bk = k2; }
+  }
+  v = bv;
+  k = bk;
+}
+__device__ __forceinline__ double wave_max(double v) {   // values >= -1
+  v = fmax(v, dpp_f64<0x111>(-1.0, v));
+  v = fmax(v, dpp_f64<0x112>(-1.0, v));
+  v = fmax(v, dpp_f64<0x114>(-1.0, v));
+  v = fmax(v, dpp_f64<0x118>(-1.0, v));
+  return fmax(fmax(readlane_f64(v, 15), readlane_f64(v, 31)),
+              fmax(readlane_f64(v, 47), readlane_f64(v, 63)));
+}
 template <int NW>
 __device__ __forceinline__ void block_argmax(double& v, int& k, double* sv, int* sk) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double v2 = __shfl_xor(v, o, 64);
-    const int k2 = __shfl_xor(k, o, 64);
-    if (better(v2, k2, v, k)) { v = v2; k = k2; }
-  }
+  wave_argmax(v, k);
   if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; sk[threadIdx.x >> 6] = k; }
   __syncthreads();
   v = sv[0];
@@ -550,8 +653,7 @@ __device__ __forceinline__ void block_argmax(double& v, int& k, double* sv, int*
 }
 template <int NW>
 __device__ __forceinline__ double block_max0(double v, double* sm) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  v = wave_max(v);
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -678,7 +780,7 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
 #pragma unroll
       for (int n1 = 0; n1 < P::R1; n1++) v1[j][n1] = src[n1 * P::G1 + g];
     }
-    v2d v3[P::K3][P::R3], vl = (v2d){0.0, 0.0};
+    v2d v3[P::K3][P::R3], vl[2] = {(v2d){0.0, 0.0}, (v2d){0.0, 0.0}};
     fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl);
     v2d* o = out + (long)w * rs;
     if (t < P::T) {
@@ -690,11 +792,13 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
       }
     }
     if constexpr (P::L > 0) {
-      if (t < P::L * P::R3) {
-        int base, step;
-        P::out_base(P::K3 * P::T + t / P::R3, base, step);
-        o[P::store_index((base + (t % P::R3) * step) % P::N)] = vl;
-      }
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+        if (P::lvalid(t, j)) {
+          int base, step;
+          P::out_base(P::K3 * P::T + t % P::L, base, step);
+          o[P::store_index((base + P::lslot(t, j) * step) % P::N)] = vl[j];
+        }
     }
   }
 }
@@ -731,7 +835,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   const double inv_n2 = 1.0 / ((double)N * (double)N);
   const v2d* Fc0 = F + (long)code * rs;
 
-  double pw[K3][R3], pwl = -1.0;
+  double pw[K3][R3], pwl[2] = {-1.0, -1.0};   // pwl: leftover outputs (P::lvalid)
 
   for (int i = 0; i < nblk; i++) {
     const int blk = blk0 + i;
@@ -804,7 +908,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
         }
       }
     }
-    v2d v3[K3][R3], vl = (v2d){0.0, 0.0};
+    v2d v3[K3][R3], vl[2] = {(v2d){0.0, 0.0}, (v2d){0.0, 0.0}};
     // non-coherent: the running sums start at zero in the first block (the
     // compiler spills them around the load phase, where registers are scarcest)
     auto start_sums = [&]() {
@@ -814,24 +918,34 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
           for (int j = 0; j < K3; j++)
 #pragma unroll
             for (int k = 0; k < R3; k++) pw[j][k] = 0.0;
-          pwl = 0.0;
+          pwl[0] = P::lvalid(t, 0) ? 0.0 : -1.0;
+          pwl[1] = P::lvalid(t, 1) ? 0.0 : -1.0;
         }
       }
     };
-    fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl, start_sums);
-    // |.|^2 / N^2 (|ifft(Y)|^2 = |fft(conj Y)|^2 / N^2)
+    // |.|^2 / N^2 (|ifft(Y)|^2 = |fft(conj Y)|^2 / N^2); a prime radix-R3
+    // stage is fused with the powers
+    constexpr bool kFuse = is_prime(R3);
+    fft_core<P, decltype(start_sums), !kFuse>(lds, side, tw3, twN, t, v1, v3, vl, start_sums);
 #pragma unroll
-    for (int j = 0; j < K3; j++)
+    for (int j = 0; j < K3; j++) {
+      if constexpr (kFuse) {
+        dft_prime_power<R3, kNC>(v3[j], pw[j], inv_n2);
+      } else {
 #pragma unroll
-      for (int k3 = 0; k3 < R3; k3++) {
-        const double p = fma(v3[j][k3].x, v3[j][k3].x, v3[j][k3].y * v3[j][k3].y) * inv_n2;
-        pw[j][k3] = kNC ? pw[j][k3] + p : p;
+        for (int k3 = 0; k3 < R3; k3++) {
+          const double p = fma(v3[j][k3].x, v3[j][k3].x, v3[j][k3].y * v3[j][k3].y) * inv_n2;
+          pw[j][k3] = kNC ? pw[j][k3] + p : p;
+        }
       }
+    }
     if constexpr (L > 0) {
-      if (t < L * R3) {
-        const double p = fma(vl.x, vl.x, vl.y * vl.y) * inv_n2;
-        pwl = kNC ? pwl + p : p;
-      }
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+        if (P::lvalid(t, j)) {
+          const double p = fma(vl[j].x, vl[j].x, vl[j].y * vl[j].y) * inv_n2;
+          pwl[j] = kNC ? pwl[j] + p : p;
+        }
     }
     if (DUMP && blk == dump_block && act) {
 #pragma unroll
@@ -847,11 +961,13 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
         }
       }
       if constexpr (L > 0) {
-        if (t < L * R3) {
-          int base, step;
-          P::out_base(K3 * T + t / R3, base, step);
-          dump[(long)rowid * N + (base + (t % R3) * step) % N] = pwl;
-        }
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          if (P::lvalid(t, j)) {
+            int base, step;
+            P::out_base(K3 * T + t % P::L, base, step);
+            dump[(long)rowid * N + (base + P::lslot(t, j) * step) % N] = pwl[j];
+          }
       }
     }
 
@@ -886,14 +1002,16 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   if (!act) { a1 = -1.0; a2 = -1.0; ak = INT_MAX; }
   double bv = a1;
   int bk = ak;
-  int kl = INT_MAX;
+  int kl[2] = {INT_MAX, INT_MAX};
   if constexpr (L > 0) {
-    if (t < L * R3) {
-      int base, step;
-      P::out_base(K3 * T + t / R3, base, step);
-      kl = (base + (t % R3) * step) % N;
-      if (better(pwl, kl, bv, bk)) { bv = pwl; bk = kl; }
-    }
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+      if (P::lvalid(t, j)) {
+        int base, step;
+        P::out_base(K3 * T + t % P::L, base, step);
+        kl[j] = (base + P::lslot(t, j) * step) % N;
+        if (better(pwl[j], kl[j], bv, bk)) { bv = pwl[j]; bk = kl[j]; }
+      }
   }
   block_argmax<P::NW>(bv, bk, s_v, s_k);
   ACQ64_STAMP(9);
@@ -920,7 +1038,9 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     }
   }
   if constexpr (L > 0) {
-    if (t < L * R3 && outside(kl)) sv = fmax(sv, pwl);
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+      if (P::lvalid(t, j) && outside(kl[j])) sv = fmax(sv, pwl[j]);
   }
   sv = block_max0<P::NW>(sv, s_m);
   ACQ64_STAMP(10);
