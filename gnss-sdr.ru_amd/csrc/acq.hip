@@ -1380,8 +1380,8 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
     return GNSSCORR_EINVAL;
   }
   if (cfg->precision == GNSSCORR_ACQ_F64 && !acq64_plan_for(cfg->n_samples)) {
-    gnsscorr_set_error("gnsscorr_acq_create: no fp64 plan for n_samples %d (supported: 16368, "
-                       "16000)", cfg->n_samples);
+    gnsscorr_set_error("gnsscorr_acq_create: n_samples %d outside the fp64 range [64, %d]",
+                       cfg->n_samples, 1 << 19);
     return GNSSCORR_EINVAL;
   }
   *out = nullptr;

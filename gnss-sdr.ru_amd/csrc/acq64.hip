@@ -1124,17 +1124,355 @@ int corr_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_units, int n_
 
 }  // namespace
 
+// ==================================================================================
+// Generic N (any other samplesPerCode, e.g. acquisition.sci at fs = 5 or 38.192 MHz):
+// the same fp64 pipeline with every length-N DFT done by Bluestein's chirp-z
+// identity  X_k = c_k sum_n (a_n c_n) conj(c_{k-n}),  c_n = exp(-i pi n^2 / N),
+// i.e. a cyclic convolution of length M = 16^P >= 2N - 1 through two radix-16
+// Stockham FFTs in global memory.  A fallback for sizes without a compiled
+// plan: correct to fp64 rounding, not tuned.
+// ==================================================================================
+namespace {
+
+constexpr int kGThreads = 256;
+
+// one radix-16 Stockham pass (autosort), forward: Ns = 16^p
+__global__ __launch_bounds__(kGThreads) void g_fft_pass(const v2d* __restrict__ in,
+                                                        v2d* __restrict__ out, int M, int Ns,
+                                                        const v2d* __restrict__ twM) {
+  const int j = blockIdx.x * kGThreads + threadIdx.x;   // < M / 16
+  const long row = (long)blockIdx.y * M;
+  if (j >= M / 16) return;
+  const int k = j & (Ns - 1);
+  const int tstep = k * (M / (16 * Ns));                  // twiddle W_M^(r * tstep)
+  v2d v[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const v2d x = in[row + j + r * (M / 16)];
+    v[r] = r == 0 ? x : cmul(x, twM[(r * tstep) & (M - 1)]);
+  }
+  dft<16>(v);
+  const int d = (j / Ns) * Ns * 16 + k;
+#pragma unroll
+  for (int r = 0; r < 16; r++) out[row + d + r * Ns] = v[r];
+}
+
+// A[row] = (a_n c_n | 0...) from natural rows a (stride src_rs)
+__global__ __launch_bounds__(kGThreads) void g_pre_kernel(const v2d* __restrict__ a, int src_rs,
+                                                          const v2d* __restrict__ chirp, int N,
+                                                          int M, v2d* __restrict__ A) {
+  const int n = blockIdx.x * kGThreads + threadIdx.x;
+  if (n >= M) return;
+  const long r = blockIdx.y;
+  A[r * M + n] = n < N ? cmul(a[r * src_rs + n], chirp[n]) : (v2d){0.0, 0.0};
+}
+
+// correlation rows of a chunk: Y_k = conj(X_cls,blk[k - m]) F_code[k] (as acq64_corr_kernel),
+// times c_k, zero padded.  unit = u0 + blockIdx.y; block `blk` of it (-1: the unit's own).
+__global__ __launch_bounds__(kGThreads) void g_corr_pre_kernel(
+    const v2d* __restrict__ X, const v2d* __restrict__ F, int rs, int n_blocks, int nc_blk,
+    const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins,
+    const int2* __restrict__ fmap, int u0, const v2d* __restrict__ chirp, int N, int M,
+    v2d* __restrict__ A) {
+  const int n = blockIdx.x * kGThreads + threadIdx.x;
+  if (n >= M) return;
+  const int unit = u0 + blockIdx.y;
+  const int rowid = nc_blk >= 0 ? unit : unit / n_blocks;
+  const int blk = nc_blk >= 0 ? nc_blk : unit % n_blocks;
+  const int g = rowid / n_bins, bin = rowid % n_bins;
+  v2d y = (v2d){0.0, 0.0};
+  if (n < N) {
+    const int2 fm = fmap[group_freq[g * n_bins + bin]];
+    int s = n - fm.y;
+    s += s < 0 ? N : 0;
+    const v2d x = X[((long)fm.x * n_blocks + blk) * rs + s];
+    const v2d f = F[(long)group_code[g] * rs + n];
+    y = cmul((v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))}, chirp[n]);
+  }
+  A[(long)blockIdx.y * M + n] = y;
+}
+
+// B = conj(A * Vf)   (IFFT_M(Z) = conj(FFT_M(conj Z)) / M)
+__global__ __launch_bounds__(kGThreads) void g_mulv_kernel(const v2d* __restrict__ A,
+                                                           const v2d* __restrict__ vf, int M,
+                                                           v2d* __restrict__ B) {
+  const int n = blockIdx.x * kGThreads + threadIdx.x;
+  if (n >= M) return;
+  const long i = (long)blockIdx.y * M + n;
+  const v2d z = cmul(A[i], vf[n]);
+  B[i] = (v2d){z.x, -z.y};
+}
+
+// spectra: out[k] = c_k conj(D_k) / M
+__global__ __launch_bounds__(kGThreads) void g_post_kernel(const v2d* __restrict__ D,
+                                                           const v2d* __restrict__ chirp, int N,
+                                                           int M, v2d* __restrict__ out, int rs) {
+  const int k = blockIdx.x * kGThreads + threadIdx.x;
+  if (k >= N) return;
+  const v2d d = D[(long)blockIdx.y * M + k];
+  const double inv = 1.0 / (double)M;
+  out[(long)blockIdx.y * rs + k] = cmul((v2d){d.x * inv, -d.y * inv}, chirp[k]);
+}
+
+// powers |DFT_N(Y)|^2 / N^2 = |D_k|^2 / (M N)^2, stored or added
+__global__ __launch_bounds__(kGThreads) void g_power_kernel(const v2d* __restrict__ D, int N,
+                                                            int M, int acc,
+                                                            double* __restrict__ pw) {
+  const int k = blockIdx.x * kGThreads + threadIdx.x;
+  if (k >= N) return;
+  const v2d d = D[(long)blockIdx.y * M + k];
+  const double sc = 1.0 / ((double)M * (double)N);
+  const double p = fma(d.x * sc, d.x * sc, (d.y * sc) * (d.y * sc));
+  double* o = pw + (long)blockIdx.y * N + k;
+  *o = acc ? *o + p : p;
+}
+
+// row statistics of a power row (acq64_corr_kernel's: first natural index of
+// the maximum, max outside the open circular window (argmax - spc, argmax + spc))
+__global__ __launch_bounds__(kGThreads) void g_stats_kernel(const double* __restrict__ pw, int N,
+                                                            int u0, int n_blocks, int nc, int spc,
+                                                            gnsscorr_acq_row* __restrict__ stats,
+                                                            double* __restrict__ dump,
+                                                            int dump_block) {
+  __shared__ double s_v[kGThreads / 64], s_m[kGThreads / 64];
+  __shared__ int s_k[kGThreads / 64];
+  const int unit = u0 + blockIdx.x;
+  const double* row = pw + (long)blockIdx.x * N;
+  const int rowid = nc ? unit : unit / n_blocks;
+  const int blk0 = nc ? 0 : unit % n_blocks;
+  double bv = -1.0;
+  int bk = INT_MAX;
+  for (int k = threadIdx.x; k < N; k += kGThreads)
+    if (row[k] > bv) { bv = row[k]; bk = k; }     // first index within the thread's stride
+  block_argmax<kGThreads / 64>(bv, bk, s_v, s_k);
+  double sv = -1.0;
+  for (int k = threadIdx.x; k < N; k += kGThreads) {
+    int d = k - bk;
+    d += d < 0 ? N : 0;
+    if (d >= spc && d <= N - spc) sv = fmax(sv, row[k]);
+  }
+  sv = block_max0<kGThreads / 64>(sv, s_m);
+  if (dump && !nc && blk0 == dump_block)
+    for (int k = threadIdx.x; k < N; k += kGThreads) dump[(long)rowid * N + k] = row[k];
+  if (threadIdx.x == 0) {
+    gnsscorr_acq_row r;
+    r.peak = bv;
+    r.second = sv;
+    r.argmax = bk;
+    r.block = nc ? -1 : blk0;
+    stats[(long)rowid * n_blocks + blk0] = r;
+  }
+}
+
+// wipe-off rows in natural order (acq64_wipe_kernel with a runtime N)
+__global__ __launch_bounds__(256) void g_wipe_kernel(const int8_t* __restrict__ src, int iq,
+                                                     int n_blocks, int coh,
+                                                     const double* __restrict__ cfreq,
+                                                     const int* __restrict__ n_cls_dev, double ts,
+                                                     int N, v2d* __restrict__ out) {
+  const long total = (long)(*n_cls_dev) * n_blocks * N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(i / N), n = (int)(i % N);
+    const int cls = row / n_blocks, blk = row % n_blocks;
+    const double f = cfreq[cls];
+    const bool cplx = iq & GNSSCORR_IF_IQ, pk = iq & GNSSCORR_IF_PACKED2;
+    const int ne = cplx ? 2 : 1;
+    const long e0 = (long)blk * coh * N * ne;
+    double re = 0.0, im = 0.0;
+    for (int p = 0; p < coh; p++) {
+      const long m = n + (long)p * N;
+      const double I = (double)if_elem(src, e0 + ne * m, pk);
+      const double Q = cplx ? (double)if_elem(src, e0 + 2 * m + 1, pk) : 0.0;
+      const double th = f * ((((double)m * 2.0) * M_PI) * ts);
+      double sn, cs;
+      sincos(th, &sn, &cs);
+      re += I * cs - Q * sn;
+      im += I * sn + Q * cs;
+    }
+    out[(long)row * N + n] = (v2d){re, im};
+  }
+}
+
+__global__ __launch_bounds__(256) void g_codes_kernel(const int8_t* __restrict__ codes, long n,
+                                                      v2d* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (v2d){(double)codes[i], 0.0};
+}
+
+// FFT_M of `rows` rows in place in A (B is the ping-pong buffer); result in *res
+int g_fft(gnsscorr_acq_ctx* c, v2d* A, v2d* B, int rows, v2d** res) {
+  const int M = c->gM;
+  v2d *in = A, *out = B;
+  for (int p = 0, Ns = 1; p < c->gP; p++, Ns *= 16) {
+    hipLaunchKernelGGL(g_fft_pass, dim3((M / 16 + kGThreads - 1) / kGThreads, rows),
+                       dim3(kGThreads), 0, c->stream, in, out, M, Ns, (const v2d*)c->d_twM);
+    HIP_TRY(hipGetLastError());
+    v2d* t = in;
+    in = out;
+    out = t;
+  }
+  *res = in;
+  return GNSSCORR_OK;
+}
+
+// DFT_N of `rows` natural rows a (stride src_rs) -> out (stride rs), via chunks
+int g_dft_rows(gnsscorr_acq_ctx* c, const v2d* a, int src_rs, int rows, v2d* out, int rs) {
+  const int N = c->cfg.n_samples, M = c->gM;
+  for (int r0 = 0; r0 < rows; r0 += c->g_chunk) {
+    const int nr = rows - r0 < c->g_chunk ? rows - r0 : c->g_chunk;
+    v2d *A = (v2d*)c->d_gA, *B = (v2d*)c->d_gB, *D;
+    hipLaunchKernelGGL(g_pre_kernel, dim3((M + kGThreads - 1) / kGThreads, nr), dim3(kGThreads),
+                       0, c->stream, a + (long)r0 * src_rs, src_rs, (const v2d*)c->d_chirp, N, M,
+                       A);
+    HIP_TRY(hipGetLastError());
+    int rc = g_fft(c, A, B, nr, &D);
+    if (rc) return rc;
+    v2d* E = D == A ? B : A;
+    hipLaunchKernelGGL(g_mulv_kernel, dim3((M + kGThreads - 1) / kGThreads, nr), dim3(kGThreads),
+                       0, c->stream, D, (const v2d*)c->d_vf, M, E);
+    HIP_TRY(hipGetLastError());
+    rc = g_fft(c, E, D, nr, &D);
+    if (rc) return rc;
+    hipLaunchKernelGGL(g_post_kernel, dim3((N + kGThreads - 1) / kGThreads, nr), dim3(kGThreads),
+                       0, c->stream, D, (const v2d*)c->d_chirp, N, M, out + (long)r0 * rs, rs);
+    HIP_TRY(hipGetLastError());
+  }
+  return GNSSCORR_OK;
+}
+
+int g_init(gnsscorr_acq_ctx* c) {
+  const long N = c->cfg.n_samples;
+  int M = 16, P = 1;
+  while (M < 2 * N - 1) { M *= 16; P++; }
+  c->gM = M;
+  c->gP = P;
+  // chunk: ~64 MiB per work buffer
+  c->g_chunk = (int)((64L << 20) / ((long)M * 16));
+  if (c->g_chunk < 1) c->g_chunk = 1;
+  if (c->g_chunk > 4096) c->g_chunk = 4096;
+  HIP_TRY(hipMalloc(&c->d_chirp, sizeof(double2) * N));
+  HIP_TRY(hipMalloc(&c->d_vf, sizeof(double2) * M));
+  HIP_TRY(hipMalloc(&c->d_twM, sizeof(double2) * M));
+  HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)M * c->g_chunk));
+  HIP_TRY(hipMalloc(&c->d_gB, sizeof(double2) * (size_t)M * c->g_chunk));
+  HIP_TRY(hipMalloc(&c->d_gpw, sizeof(double) * (size_t)N * c->g_chunk));
+  double2* h = (double2*)malloc(sizeof(double2) * M);
+  if (!h) return GNSSCORR_ENOMEM;
+  // chirp: exact argument reduction n^2 mod 2N
+  for (long n = 0; n < N; n++) {
+    const long q = (n * n) % (2 * N);
+    const double a = -M_PI * ((double)q / (double)N);
+    h[n] = make_double2(cos(a), sin(a));
+  }
+  hipError_t e = hipMemcpy(c->d_chirp, h, sizeof(double2) * N, hipMemcpyHostToDevice);
+  // W_M^t with the angle reduced to the first octant by symmetry
+  for (long t = 0; e == hipSuccess && t < M; t++) {
+    const double a = -2.0 * M_PI * ((double)t / (double)M);
+    h[t] = make_double2(cos(a), sin(a));
+  }
+  if (e == hipSuccess) e = hipMemcpy(c->d_twM, h, sizeof(double2) * M, hipMemcpyHostToDevice);
+  // two-sided conjugate chirp v_m = conj(c_|m|), wrapped to M
+  for (long m = 0; m < M; m++) h[m] = make_double2(0.0, 0.0);
+  for (long m = 0; m < N; m++) {
+    const long q = (m * m) % (2 * N);
+    const double a = M_PI * ((double)q / (double)N);
+    h[m] = make_double2(cos(a), sin(a));
+    if (m > 0) h[M - m] = h[m];
+  }
+  if (e == hipSuccess) e = hipMemcpy(c->d_gA, h, sizeof(double2) * M, hipMemcpyHostToDevice);
+  free(h);
+  HIP_TRY(e);
+  v2d* D;
+  int rc = g_fft(c, (v2d*)c->d_gA, (v2d*)c->d_gB, 1, &D);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_vf, D, sizeof(double2) * M, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GNSSCORR_OK;
+}
+
+int g_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
+  const long n = (long)n_codes * c->cfg.n_samples;
+  hipLaunchKernelGGL(g_codes_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, d_codes, n,
+                     (v2d*)c->d_in64);
+  HIP_TRY(hipGetLastError());
+  return g_dft_rows(c, (const v2d*)c->d_in64, c->cfg.n_samples, n_codes, (v2d*)c->d_F64, c->rs64);
+}
+
+int g_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int n_freqs,
+              const double* d_freqs) {
+  const int N = c->cfg.n_samples;
+  hipLaunchKernelGGL(acq64_classify_kernel, dim3(1), dim3(1024), 0, c->stream, d_freqs, n_freqs,
+                     c->cfg.samp_rate / N, N, c->d_fmap64, c->d_cfreq, c->d_nclass, c->d_resid,
+                     c->d_lead64);
+  HIP_TRY(hipGetLastError());
+  const int rows = n_freqs * n_blocks;   // upper bound: classes <= frequencies
+  const long work = (long)rows * N;
+  const int grid = (int)((work + 255) / 256 < 2048 ? (work + 255) / 256 : 2048);
+  hipLaunchKernelGGL(g_wipe_kernel, dim3(grid), dim3(256), 0, c->stream, d_if, iq, n_blocks,
+                     c->coh, (const double*)c->d_cfreq, (const int*)c->d_nclass,
+                     1.0 / c->cfg.samp_rate, N, (v2d*)c->d_in64);
+  HIP_TRY(hipGetLastError());
+  // transform only the class rows (the count is on the device: one small read
+  // back; this generic path is synchronous here anyway)
+  int n_cls = 0;
+  HIP_TRY(hipMemcpyAsync(&n_cls, c->d_nclass, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return g_dft_rows(c, (const v2d*)c->d_in64, N, n_cls * n_blocks, (v2d*)c->d_X64, c->rs64);
+}
+
+int g_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
+                const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
+                int dump_block) {
+  const int N = c->cfg.n_samples, M = c->gM;
+  const bool nc = mode == GNSSCORR_ACQ_NONCOHERENT;
+  const int n_units = n_groups * n_bins * (nc ? 1 : n_blocks);
+  for (int u0 = 0; u0 < n_units; u0 += c->g_chunk) {
+    const int nu = n_units - u0 < c->g_chunk ? n_units - u0 : c->g_chunk;
+    for (int b = 0; b < (nc ? n_blocks : 1); b++) {
+      v2d *A = (v2d*)c->d_gA, *B = (v2d*)c->d_gB, *D;
+      hipLaunchKernelGGL(g_corr_pre_kernel, dim3((M + kGThreads - 1) / kGThreads, nu),
+                         dim3(kGThreads), 0, c->stream, (const v2d*)c->d_X64,
+                         (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1, d_gcode, d_gfreq,
+                         n_bins, (const int2*)c->d_fmap64, u0, (const v2d*)c->d_chirp, N, M, A);
+      HIP_TRY(hipGetLastError());
+      int rc = g_fft(c, A, B, nu, &D);
+      if (rc) return rc;
+      v2d* E = D == A ? B : A;
+      hipLaunchKernelGGL(g_mulv_kernel, dim3((M + kGThreads - 1) / kGThreads, nu),
+                         dim3(kGThreads), 0, c->stream, D, (const v2d*)c->d_vf, M, E);
+      HIP_TRY(hipGetLastError());
+      rc = g_fft(c, E, D, nu, &D);
+      if (rc) return rc;
+      hipLaunchKernelGGL(g_power_kernel, dim3((N + kGThreads - 1) / kGThreads, nu),
+                         dim3(kGThreads), 0, c->stream, D, N, M, b > 0, c->d_gpw);
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
+                       (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats, d_dump,
+                       dump_block);
+    HIP_TRY(hipGetLastError());
+  }
+  return GNSSCORR_OK;
+}
+
+}  // namespace
+
 int acq64_plan_for(int n_samples) {
-  if (n_samples == PlanA::N) return 1;
-  if (n_samples == PlanB::N) return 2;
+  // GNSSCORR_ACQ_GENERIC=1: the Bluestein engine for every N (cross-checks)
+  const char* fg = getenv("GNSSCORR_ACQ_GENERIC");
+  const int force_generic = fg ? atoi(fg) : 0;
+  if (!force_generic && n_samples == PlanA::N) return 1;
+  if (!force_generic && n_samples == PlanB::N) return 2;
+  if (n_samples >= 64 && n_samples <= (1 << 19)) return 3;
   return 0;
 }
 
 int acq64_init(gnsscorr_acq_ctx* c) {
   c->plan64 = acq64_plan_for(c->cfg.n_samples);
   if (!c->plan64) {
-    gnsscorr_set_error("acq64: no fp64 plan for n_samples %d (supported: %d, %d)",
-                       c->cfg.n_samples, PlanA::N, PlanB::N);
+    gnsscorr_set_error("acq64: n_samples %d outside [64, %d] (compiled plans: %d, %d; "
+                       "Bluestein otherwise)", c->cfg.n_samples, 1 << 19, PlanA::N, PlanB::N);
     return GNSSCORR_EINVAL;
   }
   const int N = c->cfg.n_samples;
@@ -1143,6 +1481,7 @@ int acq64_init(gnsscorr_acq_ctx* c) {
   HIP_TRY(hipMemset(c->d_F64, 0, sizeof(double2) * (size_t)c->rs64 * c->cfg.max_codes));
   HIP_TRY(hipMalloc(&c->d_fmap64, sizeof(int2) * c->cfg.max_freqs));
   HIP_TRY(hipMalloc(&c->d_lead64, sizeof(int) * c->cfg.max_freqs));
+  if (c->plan64 == 3) return g_init(c);
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
   double2* tw = (double2*)malloc(sizeof(double2) * N);
   for (int j = 0; j < N; j++) {
@@ -1157,9 +1496,12 @@ int acq64_init(gnsscorr_acq_ctx* c) {
 }
 
 void acq64_free(gnsscorr_acq_ctx* c) {
-  void* bufs[] = {c->d_F64, c->d_X64, c->d_in64, c->d_twN, c->d_fmap64, c->d_lead64};
+  void* bufs[] = {c->d_F64, c->d_X64,   c->d_in64, c->d_twN, c->d_fmap64, c->d_lead64,
+                  c->d_chirp, c->d_vf, c->d_twM, c->d_gA,  c->d_gB,     c->d_gpw};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  c->d_chirp = c->d_vf = c->d_twM = c->d_gA = c->d_gB = nullptr;
+  c->d_gpw = nullptr;
   c->d_F64 = c->d_X64 = c->d_in64 = c->d_twN = nullptr;
   c->d_fmap64 = nullptr;
   c->d_lead64 = nullptr;
@@ -1205,6 +1547,7 @@ int acq64_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
   int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)n_codes * c->cfg.n_samples,
                     sizeof(double2));
   if (rc) return rc;
+  if (c->plan64 == 3) return g_set_codes(c, d_codes, n_codes);
   return c->plan64 == 1 ? set_codes_launch<PlanA>(c, d_codes, n_codes)
                         : set_codes_launch<PlanB>(c, d_codes, n_codes);
 }
@@ -1216,6 +1559,7 @@ int acq64_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks,
   if (rc) return rc;
   rc = acq_grow((void**)&c->d_X64, &c->cap_X64, rows * c->rs64, sizeof(double2));
   if (rc) return rc;
+  if (c->plan64 == 3) return g_spectra(c, d_if, iq, n_blocks, n_freqs, d_freqs);
   return c->plan64 == 1 ? spectra_launch<PlanA>(c, d_if, iq, n_blocks, n_freqs, d_freqs)
                         : spectra_launch<PlanB>(c, d_if, iq, n_blocks, n_freqs, d_freqs);
 }
@@ -1225,6 +1569,9 @@ int acq64_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, i
                     int dump_block) {
   const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;
   const int n_units = n_groups * n_bins * upr;
+  if (c->plan64 == 3)
+    return g_correlate(c, n_blocks, mode, n_groups, n_bins, d_gcode, d_gfreq, spc, d_dump,
+                       dump_block);
   return c->plan64 == 1 ? corr_launch<PlanA>(c, n_blocks, mode, n_units, n_bins, d_gcode, d_gfreq,
                                              spc, d_dump, dump_block)
                         : corr_launch<PlanB>(c, n_blocks, mode, n_units, n_bins, d_gcode, d_gfreq,

@@ -28,6 +28,15 @@ struct gnsscorr_acq_ctx {
   int2* d_fmap64 = nullptr;             // per frequency: {class, shift m mod N}
   int* d_lead64 = nullptr;              // classify scratch: per frequency, its class leader
   int rs64 = 0;                         // fp64 row stride (complex elements)
+  // generic-N fp64 plan (plan64 == 3, any other N): Bluestein with radix-16
+  // Stockham FFTs of length M = 16^P >= 2N - 1 (acq64.hip)
+  int gM = 0, gP = 0;
+  double2* d_chirp = nullptr;           // c_n = exp(-i pi n^2 / N), n < N
+  double2* d_vf = nullptr;              // FFT_M of the conjugate chirp (two-sided)
+  double2* d_twM = nullptr;             // W_M^t, t < M
+  double2 *d_gA = nullptr, *d_gB = nullptr;   // chunk x M work rows
+  double* d_gpw = nullptr;              // chunk x N power rows
+  int g_chunk = 0;                      // rows per chunk
   // ---- shared
   int n_codes = 0;
   int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra

@@ -204,4 +204,5 @@ def test_bad_precision_or_size_rejected(gpu):
     with pytest.raises(gpu.GnssCorrError):
         gpu.AcqCtx(16.0e6, 16000, precision=gpu.ACQ_F32)   # fp32 path: 16368 only
     with pytest.raises(gpu.GnssCorrError):
-        gpu.AcqCtx(16.1e6, 16100)                           # no fp64 plan for this N
+        gpu.AcqCtx(0.032e6, 32)                             # below the generic fp64 range
+    gpu.AcqCtx(16.1e6, 16100).close()                       # any other N: Bluestein (generic)
