@@ -803,6 +803,79 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
   }
 }
 
+// ---- forward transforms of prime-factor plans in two launches --------------------
+// Stage 1 (radix R1 over the G1 groups) in place: element n1*G1 + g of a row
+// becomes k1*G1 + g -- each thread reads and writes the same R1 positions.
+template <class P>
+__global__ __launch_bounds__(256) void acq64_fwd1_kernel(v2d* __restrict__ io,
+                                                         const int* __restrict__ n_cls_dev,
+                                                         int per_cls, int n_rows) {
+  const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int row = (int)(i / P::G1), g = (int)(i % P::G1);
+  if (row >= rows) return;
+  v2d* r = io + (long)row * P::N;
+  v2d v[P::R1];
+#pragma unroll
+  for (int n1 = 0; n1 < P::R1; n1++) v[n1] = r[n1 * P::G1 + g];
+  dft<P::R1>(v);
+#pragma unroll
+  for (int k1 = 0; k1 < P::R1; k1++) r[k1 * P::G1 + g] = v[k1];
+}
+
+// Stages 2 and 3 of one (row, k1): the G1 = R2 x R3 values k1*G1 + n2*R3 + n3
+// are an independent R2 x R3 prime-factor transform.  One output per thread
+// as direct DFT sums (R2, then R3 complex MACs) through LDS; the results go to
+// the plan's storage positions sbase(k1*R2 + k2) + soff(k3).
+constexpr int kFwd23Threads = 1024;
+template <class P>
+__global__ __launch_bounds__(kFwd23Threads) void acq64_fwd23_kernel(
+    const v2d* __restrict__ in, const int* __restrict__ n_cls_dev, int per_cls, int n_rows,
+    v2d* __restrict__ out, int rs) {
+  constexpr int R2 = P::R2, R3 = P::R3, G1 = P::G1;
+  static_assert(G1 <= kFwd23Threads, "one output per thread");
+  __shared__ v2d s_a[G1], s_b[G1];
+  __shared__ v2d w2[R2], w3[R3];
+  const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
+  const int row = blockIdx.x / P::R1, k1 = blockIdx.x % P::R1;
+  if (row >= rows) return;
+  const int t = threadIdx.x;
+  if (t < R2) w2[t] = (v2d){kTw<R2>.c[t], -kTw<R2>.s[t]};
+  if (t < R3) w3[t] = (v2d){kTw<R3>.c[t], -kTw<R3>.s[t]};
+  if (t < G1) s_a[t] = in[(long)row * P::N + k1 * G1 + t];
+  __syncthreads();
+  // (four partial sums: the latency of one dependent chain, not the FMA
+  // rate, bounds these single-wave-per-SIMD sums)
+  if (t < G1) {   // stage 2: output (k2, n3) = sum_n2 a[n2][n3] W_R2^(n2 k2)
+    const int k2 = t / R3, n3 = t % R3;
+    v2d acc[4] = {(v2d){0.0, 0.0}, (v2d){0.0, 0.0}, (v2d){0.0, 0.0}, (v2d){0.0, 0.0}};
+    // W^(n2 k2) by recurrence from one table read (a per-lane gather of the
+    // table at every step conflicts in LDS); error ~R2 ulp
+    const v2d wk = w2[k2];
+    v2d w = (v2d){1.0, 0.0};
+#pragma unroll
+    for (int n2 = 0; n2 < R2; n2++) {
+      acc[n2 & 3] += cmul(s_a[n2 * R3 + n3], w);
+      w = cmul(w, wk);
+    }
+    s_b[t] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+  __syncthreads();
+  if (t < G1) {   // stage 3: output (k2, k3) = sum_n3 b[k2][n3] W_R3^(n3 k3)
+    const int k2 = t / R3, k3 = t % R3;
+    v2d acc[4] = {(v2d){0.0, 0.0}, (v2d){0.0, 0.0}, (v2d){0.0, 0.0}, (v2d){0.0, 0.0}};
+    const v2d wk = w3[k3];
+    v2d w = (v2d){1.0, 0.0};
+#pragma unroll
+    for (int n3 = 0; n3 < R3; n3++) {
+      acc[n3 & 3] += cmul(s_b[k2 * R3 + n3], w);
+      w = cmul(w, wk);
+    }
+    out[(long)row * rs + P::sbase(k1 * R2 + k2) + P::soff(k3)] =
+        (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+}
+
 // ---- the correlation kernel -------------------------------------------------------
 // One workgroup = one unit: BEST_OF_BLOCKS -> (row, block); NONCOHERENT -> row,
 // |.|^2 summed over the blocks in registers.  fmap[fid] = {class, m}: the bin's
@@ -1095,8 +1168,21 @@ __global__ __launch_bounds__(1024) void acq64_classify_kernel(const double* __re
 template <class P>
 int fwd_launch(gnsscorr_acq_ctx* c, const v2d* in, const int* n_cls_dev, int per_cls,
                int n_rows, v2d* out) {
-  hipLaunchKernelGGL((acq64_fwd_kernel<P>), dim3(n_rows), dim3(P::TB), 0, c->stream, in, n_cls_dev,
-                     per_cls, n_rows, out, c->rs64, (const v2d*)c->d_twN);
+  if constexpr (P::PFA) {
+    // two launches spread over the whole GPU (a config-2 search has only 4
+    // rows: one workgroup per row would leave 252 CUs idle): stage 1 in place,
+    // then the 16 independent 1023-point (33 x 31) transforms of every row
+    v2d* io = const_cast<v2d*>(in);
+    const long groups = (long)n_rows * P::G1;
+    hipLaunchKernelGGL((acq64_fwd1_kernel<P>), dim3((groups + 255) / 256), dim3(256), 0,
+                       c->stream, io, n_cls_dev, per_cls, n_rows);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL((acq64_fwd23_kernel<P>), dim3(n_rows * P::R1), dim3(kFwd23Threads), 0,
+                       c->stream, (const v2d*)io, n_cls_dev, per_cls, n_rows, out, c->rs64);
+  } else {
+    hipLaunchKernelGGL((acq64_fwd_kernel<P>), dim3(n_rows), dim3(P::TB), 0, c->stream, in,
+                       n_cls_dev, per_cls, n_rows, out, c->rs64, (const v2d*)c->d_twN);
+  }
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
