@@ -56,16 +56,10 @@ __device__ __forceinline__ int xcd_channel(int b, int G) {
   return x * q + (x < r ? x : r) + slot;
 }
 
-__device__ __forceinline__ double flip(double v, uint32_t signmask) {
-  // multiply by +-1 exactly: xor the sign bit of the high dword
-  int2 b = *reinterpret_cast<int2*>(&v);
-  b.y ^= (int)signmask;
-  return *reinterpret_cast<double*>(&b);
-}
-
 // indices are in [0, L+1] for every state the loop produces (remCode in
-// [0, step)); the clamp only keeps a corrupted state inside the LDS table
-__device__ __forceinline__ int clampi(int i, int hi) { return i < 0 ? 0 : (i > hi ? hi : i); }
+// [0, step)); the clamp only keeps a corrupted state inside the LDS table, in
+// one instruction: a negative index wraps to a huge unsigned and lands on hi
+__device__ __forceinline__ int clampu(int i, int hi) { return (int)min((unsigned)i, (unsigned)hi); }
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -79,7 +73,7 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
     const uint32_t* __restrict__ codes, gnsscorr_sgt_chan* __restrict__ chans, int n_epochs,
     gnsscorr_sgt_epoch* __restrict__ out) {
 #pragma clang fp contract(off)
-  __shared__ uint32_t s_code[kPadLen];
+  __shared__ double s_sgn[kPadLen];   // the code as +-1.0: E/P/L accumulate with one fma
   __shared__ double s_part[2][kMaxWaves][6];
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
   const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -87,7 +81,9 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
   gnsscorr_sgt_chan c = chans[ch];
   const int L = p.code_length;
   const int row = p.system == 1 ? 0 : c.code_id;
-  for (int i = tid; i < L + 2; i += T) s_code[i] = codes[row * kPadLen + i];
+  for (int i = tid; i < L + 2; i += T) {
+    s_sgn[i] = codes[row * kPadLen + i] ? -1.0 : 1.0;   // sign-bit masks of the table
+  }
   __syncthreads();
 
   const int8_t* base = ifbuf + (int64_t)c.stream * stride;
@@ -111,17 +107,20 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
     const double aE = c.rem_code - p.spc, aL = c.rem_code + p.spc, aP = c.rem_code;
     const double A = (c.carr_freq * 2.0) * M_PI;        // (carrFreq * 2.0 * %pi)
     // carrier at the thread's first sample, rotation by T samples
-    // (sin/cos rather than sincos: its pointer outputs get promoted to 32 KB of LDS)
     const double th0 = A * ((double)tid / p.fs) + c.rem_carr, thw = A * ((double)T / p.fs);
-    double sn = sin(th0), cs = cos(th0);
-    const double sw = sin(thw), cw = cos(thw);
+    double sn, cs, sw, cw;
+    sincos(th0, &sn, &cs);   // one shared argument reduction per angle
+    sincos(thw, &sw, &cw);   // (sgt.o is built with promote-alloca-to-lds off)
     double ie = 0, ip = 0, il = 0, qe = 0, qp = 0, ql = 0;
     const int8_t* src = base + (FT == 2 ? 2 : 1) * c.pos;
+    // unrolled so the IF loads of several samples are in flight together (one
+    // load in flight per iteration left the loop waiting on memory latency)
+#pragma unroll 8
     for (int64_t k = tid; k < blk; k += T) {
       const double t = (double)k * step;
-      const uint32_t mE = s_code[clampi((int)ceil(aE + t), L + 1)];
-      const uint32_t mP = s_code[clampi((int)ceil(aP + t), L + 1)];
-      const uint32_t mL = s_code[clampi((int)ceil(aL + t), L + 1)];
+      const double gE = s_sgn[clampu((int)ceil(aE + t), L + 1)];
+      const double gP = s_sgn[clampu((int)ceil(aP + t), L + 1)];
+      const double gL = s_sgn[clampu((int)ceil(aL + t), L + 1)];
       double re, im;
       if (FT == 2) {
         const char2 v = *reinterpret_cast<const char2*>(src + 2 * k);
@@ -132,12 +131,14 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
         re = (double)src[k];
         im = 0.0;
       }
-      const double qb = cs * re - sn * im;   // real(carrsig .* rawSignal)
-      const double ib = cs * im + sn * re;   // imag(carrsig .* rawSignal)
-      ie += flip(ib, mE); ip += flip(ib, mP); il += flip(ib, mL);
-      qe += flip(qb, mE); qp += flip(qb, mP); ql += flip(qb, mL);
-      const double c2 = cs * cw - sn * sw;
-      sn = sn * cw + cs * sw;
+      // (explicit fma: the carrier and the sums only need fp64 accuracy; the
+      // code indices above stay uncontracted and bit-exact)
+      const double qb = fma(cs, re, -(sn * im));   // real(carrsig .* rawSignal)
+      const double ib = fma(cs, im, sn * re);      // imag(carrsig .* rawSignal)
+      ie = fma(ib, gE, ie); ip = fma(ib, gP, ip); il = fma(ib, gL, il);   // +-ib exactly
+      qe = fma(qb, gE, qe); qp = fma(qb, gP, qp); ql = fma(qb, gL, ql);
+      const double c2 = fma(cs, cw, -(sn * sw));
+      sn = fma(sn, cw, cs * sw);
       cs = c2;
     }
     ie = wave_sum(ie); ip = wave_sum(ip); il = wave_sum(il);
