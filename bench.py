@@ -469,6 +469,12 @@ def run_glo_coherent(dist, dev, steps, warmup):
 
 SDR_REC, SDR_SV, SDR_ROWS, SDR_N = 64, 32, 120, 2048
 SDR_CORR_CH = 4096
+# doAcqStrong int-op model per (sv, row): cmulsc 8/sample, 2048-pt int16 IFFT (11 ranks x
+# 1024 radix-2 butterflies x 12 ops), cmag + max 4/sample
+SDR_STRONG_OPS_ROW = 2048 * 8 + 11 * 1024 * 12 + 2048 * 4
+# Correlator::Accum bytes per channel-packet: its carrier-table row (2048 CPX x 4 B),
+# three code-bit rows (3 x 2048 bits) and its share of the packet (16 packets / 4096 ch)
+SDR_ACCUM_BYTES = 2048 * 4 + 3 * 2048 // 8 + 16 * 2048 * 4 / SDR_CORR_CH
 SDR_FE_BLOCKS = 2000         # GN3S 5-ms reads per front-end launch (10 s of 4 Msps 2-bit samples)
 SDR_CHAN_N, SDR_CHAN_MS = 8192, 1000   # Channel objects x 1-ms Channel::Accum calls per launch
 
@@ -727,6 +733,33 @@ def cpu_baseline_fullsky(budget_s=8.0):
     return dict(value=n * N_BINS * N * 10 / dt, unit="cell-ms/s", cores=1, kind="port",
                 sample=f"{n} GPS groups x {N_BINS} bins x 10 ms non-coherent (fp64 numpy "
                        f"restatement of acquisition.sci, oracle/acq_oracle.py), {dt:.1f} s")
+
+
+def cpu_baseline_glo_coh(budget_s=6.0):
+    """GLONASS default acquisition on the host: the fp64 restatement with the literal
+    5-ms (81 840-point) coherent transforms (oracle/acq_oracle.py, one core), one FCH
+    group of 121 bins at a time, as many as fit the budget."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import acq_oracle
+    nb = int(round(GLO_BAND_KHZ * 2 * GLO_COH)) + 1
+    IF = gc.ifgen(2 * GLO_COH * N, [dict(system=1, fch=0, code_phase=100.0, doppler=500.0,
+                                         cn0=44.0)], fs=FS, if_glo=1.0e6, seed=0x5EED000E)
+    code = acq_oracle.make_st_table_row(FS)[None]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        k = n % 14 - 7
+        freqs = 1.0e6 + k * 0.5625e6 - (GLO_BAND_KHZ / 2) * 1000 + (1000 / (2 * GLO_COH)) * \
+            np.arange(nb)
+        acq_oracle.acquire(IF, FS, code, freqs, np.arange(nb)[None], group_code=np.zeros(1, int),
+                           spc=32, coh=GLO_COH)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=n * nb * N / dt, unit="cells/s", cores=1, kind="port",
+                sample=f"{n} FCH groups x {nb} bins x 2 blocks of {GLO_COH} ms coherent (fp64 "
+                       f"numpy restatement with 81 840-point transforms, oracle/acq_oracle.py), "
+                       f"{dt:.1f} s")
 
 
 def host_info():
@@ -1006,9 +1039,19 @@ def main():
                           f"at 100 Hz) x 16368 code phases, 2 blocks of {GLO_COH} ms coherent, "
                           "16.368 Msps, IF resident in HBM; one search per GPU per step",
                 "planted_found": f"{gco['found']}/{gco['n_planted']}",
+                "dtype": "f64",
+                "roofline": {"bound": "valu", "kernel": "acq64 (whole search)",
+                             "achieved": cells * N_BLK * FLOP_PER_CELL_BLOCK
+                             / (gco["dt"] / gco["steps"]) / 1e12,
+                             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
+                             "frac": cells * N_BLK * FLOP_PER_CELL_BLOCK
+                             / (gco["dt"] / gco["steps"]) / 1e12 / PEAK_FP64_TFLOPS,
+                             "timing": "whole search per step (the 5-ms folding wipe-off and "
+                                       "forward spectra included)"},
             }
         if sdr:
             cells = SDR_REC * SDR_SV * SDR_ROWS * SDR_N
+            ops = SDR_REC * SDR_SV * SDR_ROWS * SDR_STRONG_OPS_ROW
             out["sdr_acquisition"] = {
                 "metric": "acquisition cells/sec (GPS-SDR int16 strong acquisition, bit-exact)",
                 "value": cells * sdr["steps"] * W / sdr["dt_acq"], "unit": "cells/s",
@@ -1016,6 +1059,11 @@ def main():
                           "120 rows (+-15 kHz: 30 x 1 kHz shifts x 4 sub-bins) x 2048 (doAcqStrong)",
                 "kernel_ms_per_launch": sdr["ms_acq"],
                 "cells_per_launch": cells,
+                "roofline": {"bound": "valu", "kernel": "sdr_strong_kernel",
+                             "achieved": ops / (sdr["ms_acq"] * 1e-3) / 1e12, "peak": PEAK_INT_TOPS,
+                             "unit": "Tops/s (int32 op model, DESIGN.md)",
+                             "frac": ops / (sdr["ms_acq"] * 1e-3) / 1e12 / PEAK_INT_TOPS,
+                             "traffic": pmc_traffic("sdr_strong_kernel")},
             }
             out["sdr_tracking"] = {
                 "metric": "1ms E/P/L correlations/sec (GPS-SDR Correlator::Accum, bit-exact)",
@@ -1023,6 +1071,14 @@ def main():
                 "config": f"{SDR_CORR_CH} channels x one 2048-sample packet per launch "
                           "(wipe-off row + 3 code rows from the HBM-resident pre-sampled tables)",
                 "kernel_ms_per_launch": sdr["ms_corr"],
+                "roofline": {"bound": "hbm", "kernel": "sdr_accum_kernel",
+                             "achieved": SDR_CORR_CH * SDR_ACCUM_BYTES / (sdr["ms_corr"] * 1e-3)
+                             / 1e9, "peak": PEAK_HBM_GBS,
+                             "unit": "GB/s (algorithmic: carrier row + code-bit rows + packet "
+                                     "share per channel)",
+                             "frac": SDR_CORR_CH * SDR_ACCUM_BYTES / (sdr["ms_corr"] * 1e-3) / 1e9
+                             / PEAK_HBM_GBS,
+                             "traffic": pmc_traffic("sdr_accum_kernel")},
             }
             for kind, m in sdr["mw"].items():
                 cells = SDR_SV * SDR_MW_ROWS[kind] * 10 * SDR_N
@@ -1076,6 +1132,8 @@ def main():
                 out["glonass_tracking"]["cpu_baseline"] = cpu_baseline_sgt()
             if sky:
                 out["fullsky"]["cpu_baseline"] = cpu_baseline_fullsky()
+            if gco:
+                out["glonass_acquisition_5ms"]["cpu_baseline"] = cpu_baseline_glo_coh()
             if sdr:
                 out["sdr_acquisition"]["cpu_baseline"] = cpu_baseline_sdr(sdr["bufs"])
                 for kind in sdr["mw"]:
