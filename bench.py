@@ -833,11 +833,15 @@ def cpu_baseline_track(budget_s=6.0):
     return base
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any."""
+def pmc_traffic(kernel, section=None):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any:
+    the pass over that bench section alone ("section/kernel") when recorded,
+    else the whole-bench pass (an average over every section using the kernel)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
+        if section and f"{section}/{kernel}" in d:
+            return d[f"{section}/{kernel}"]["hbm_bytes_per_launch"]
         return d.get(kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
@@ -889,7 +893,7 @@ def main():
             "roofline": {"bound": "valu", "kernel": ACQ64_KERNEL, "achieved": achieved,
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
                          "frac": achieved / PEAK_FP64_TFLOPS,
-                         "traffic": pmc_traffic(ACQ64_KERNEL),
+                         "traffic": pmc_traffic(ACQ64_KERNEL, "acq"),
                          "kernel_ms_per_launch": acq["corr_ms"],
                          "flop_per_launch": flop_launch},
             "search_latency_ms": acq["dt"] / a.steps * 1e3,
@@ -930,7 +934,7 @@ def main():
                              "frac": ops_launch / k_s / 1e12 / PEAK_INT_TOPS,
                              "hbm_algorithmic_GBs": bytes_launch / k_s / 1e9,
                              "hbm_frac": bytes_launch / k_s / 1e9 / PEAK_HBM_GBS,
-                             "traffic": pmc_traffic("osg_track_kernel"),
+                             "traffic": pmc_traffic("osg_track_kernel", "track"),
                              "kernel_ms_per_launch": trk["kern_ms"]},
                 "dumps_sane": trk["dumps_ok"],
                 "closed_loop": {
@@ -1027,7 +1031,7 @@ def main():
                              "timing": "whole search per step (forward spectra included): a "
                                        "lower bound on the correlation kernel's rate",
                              "traffic": pmc_traffic("acq64_corr_kernel<Plan<16368, 16, 33, 31, "
-                                                    "512, true>, 1, false>")},
+                                                    "512, true>, 1, false>", "fullsky")},
             }
         if gco:
             cells = 14 * gco["nb"] * N

@@ -4,7 +4,7 @@
 set -eu
 TAG=${1:-r1}
 O=gpurun_out/$TAG
-mkdir -p $O/pmc
+mkdir -p $O/pmc $O/pmc_acq $O/pmc_track $O/pmc_fullsky
 export TMPDIR=/tmp
 echo "== pytest -m gpu"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
@@ -29,4 +29,13 @@ for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
   echo "pmc pass $i ok"
 done
 python tools/pmc_summary.py $O/pmc $O/pmc_summary.json --traffic $O/pmc_traffic.json
+# HBM bytes per launch of the kernels several sections share, one section at a time
+for S in acq track fullsky; do
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
+      python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1
+  done
+  python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S
+  echo "pmc section $S ok"
+done
 echo "== done"

@@ -1,6 +1,12 @@
 """Summarise rocprofv3 --pmc passes (tools/prof_pmc.sh) per kernel.
 
 usage: python tools/pmc_summary.py <pmc dir> <out json> [--traffic profiles/pmc_traffic.json]
+                                   [--section NAME]
+
+With --section the passes profiled ONE bench section alone (tools/bench_part.py
+NAME): its kernels are merged into the traffic file as "NAME/<kernel>", so
+sections sharing a kernel instantiation (the fp64 search of config 2, the
+GLONASS 5-ms search and the full-sky sweep) each get their own bytes per launch.
 
 Per kernel (name up to the first '('): the mean of every counter over its
 dispatches.  HBM bytes per launch follow MI355X_MICROARCH.md "HBM [CDNA4]":
@@ -45,7 +51,19 @@ def main():
     json.dump(s, open(o, "w"), indent=1, sort_keys=True)
     if "--traffic" in sys.argv:
         t = sys.argv[sys.argv.index("--traffic") + 1]
+        sec = sys.argv[sys.argv.index("--section") + 1] if "--section" in sys.argv else None
         keep = {}
+        if sec:
+            try:
+                keep = json.load(open(t))
+            except (OSError, ValueError):
+                keep = {}
+            for k, m in s.items():
+                if "hbm_bytes_per_launch" in m:
+                    keep[f"{sec}/{k}"] = {"hbm_bytes_per_launch": m["hbm_bytes_per_launch"],
+                                          "source": os.path.relpath(o), "instance": k}
+            json.dump(keep, open(t, "w"), indent=1, sort_keys=True)
+            s = {}
         for k, m in s.items():
             base = k.split("<")[0]
             if "hbm_bytes_per_launch" in m:
@@ -56,8 +74,9 @@ def main():
                 if k != base:   # every template instantiation under its own name too
                     keep[k] = {"hbm_bytes_per_launch": m["hbm_bytes_per_launch"],
                                "source": os.path.relpath(o), "instance": k}
-        json.dump(keep, open(t, "w"), indent=1, sort_keys=True)
-    for k, m in sorted(s.items()):
+        if s:
+            json.dump(keep, open(t, "w"), indent=1, sort_keys=True)
+    for k, m in sorted(summarise(d).items()):
         print(k, {c: round(v, 3) for c, v in m.items() if c in
                   ("FETCH_SIZE", "WRITE_SIZE", "hbm_bytes_per_launch", "dispatches",
                    "valu_active_per_wave_cycle")})
