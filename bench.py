@@ -5,9 +5,12 @@ Primary line (`value`): acquisition cells/s on BASELINE config 2 -- a full
 32-PRN x 41-Doppler-bin cold-start search (acquisition.sci semantics: 1 ms
 coherent, two consecutive 1-ms blocks, keep the better), 16368 samples per
 code period, computed in fp64 like the reference (Scilab doubles; parity
-~1e-12 relative, tests/test_acq_gpu.py).  A step = one complete search of one
-2-ms IF record that is already resident in HBM (classes, wipe-off + FFT of the
-class rows, 2624 correlation IFFTs, peak/second-peak/metric for 32 PRNs).
+~1e-12 relative, tests/test_acq_gpu.py).  A step = complete searches of
+ACQ_RECORDS consecutive 2-ms IF records already resident in HBM, each exactly
+one acquisition.sci search (classes, wipe-off + FFT of the class rows, 2624
+correlation IFFTs, peak/second-peak/metric for 32 PRNs), run as one launch per
+stage (gnsscorr_acq_set_records): one record fills the GPU for 10.25 rounds of
+units, so a single search leaves most CUs idle in its last round.
 Weak scaling: every rank runs its own search on its own record each step (PRN
 x Doppler cells shard with no exchange step: no collective on the data path).
 The fp32 fast path is reported beside it as `acquisition_f32`.
@@ -37,6 +40,7 @@ import gnsscorr as gc  # noqa: E402
 FS = 16.368e6
 N = 16368
 N_PRN, N_BINS, N_BLK = 32, 41, 2
+ACQ_RECORDS = 4        # config-2 searches per launch (gnsscorr_acq_set_records, fp64)
 CELLS_PER_SEARCH = N_PRN * N_BINS * N          # 21,474,816
 # algorithmic FLOPs of one correlation cell per 1-ms block: radix-2-equivalent
 # IFFT 5*log2(N) + complex multiply 6 + |.|^2 3 + max 1  
@@ -94,25 +98,29 @@ class Dist:
             self.td.destroy_process_group()
 
 
-def acq_setup(dev, rank, precision=gc.ACQ_F64):
+def acq_setup(dev, rank, precision=gc.ACQ_F64, records=1):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     rng = np.random.default_rng(100 + rank)
     planted = rng.choice(np.arange(1, 33), 8, replace=False)
     sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
                  doppler=float(rng.uniform(-5000, 5000)), cn0=49.0, data_bits=1) for p in planted]
-    IF = gc.ifgen(N_BLK * N, sigs, fs=FS, seed=0x5EED0002 + rank)
+    # `records` consecutive 2-ms records of the same receiver stream
+    IF = gc.ifgen(records * N_BLK * N, sigs, fs=FS, seed=0x5EED0002 + rank)
     codes = np.stack([gc.sample_code(gc.ca_code(p), 1.023e6, FS, N) for p in range(1, 33)])
     freqs = 2.42e6 - 10000.0 + 500.0 * np.arange(N_BINS)           # acquisition.sci:101-104
-    ctx = gc.AcqCtx(FS, N, device=dev, max_freqs=N_BINS, max_blocks=N_BLK, max_codes=N_PRN,
-                    precision=precision)
+    ctx = gc.AcqCtx(FS, N, device=dev, max_freqs=N_BINS, max_blocks=N_BLK * records,
+                    max_codes=N_PRN, precision=precision)
     ctx.set_codes(codes)
+    if records > 1:
+        ctx.set_records(records)
     bufs = dict(
         d_if=gc.DevBuf.from_array(IF, dev), d_freqs=gc.DevBuf.from_array(freqs, dev),
         d_gcode=gc.DevBuf.from_array(np.arange(N_PRN, dtype=np.int32), dev),
         d_gfreq=gc.DevBuf.from_array(np.tile(np.arange(N_BINS, dtype=np.int32), N_PRN), dev),
-        d_rows=gc.DevBuf(N_PRN * N_BINS * gc.ACQ_ROW.itemsize, dev),
-        d_res=gc.DevBuf(N_PRN * gc.ACQ_RESULT.itemsize, dev))
-    return ctx, bufs, dict(IF=IF, codes=codes, freqs=freqs, planted=planted)
+        d_rows=gc.DevBuf(records * N_PRN * N_BINS * gc.ACQ_ROW.itemsize, dev),
+        d_res=gc.DevBuf(records * N_PRN * gc.ACQ_RESULT.itemsize, dev))
+    return ctx, bufs, dict(IF=IF[:2 * N_BLK * N], codes=codes, freqs=freqs, planted=planted,
+                           records=records)
 
 
 def acq_step(ctx, b, ev=None):
@@ -128,14 +136,17 @@ def acq_step(ctx, b, ev=None):
                    b["d_res"].ptr)
 
 
-def run_acq(dist, dev, steps, warmup, precision=gc.ACQ_F64):
-    ctx, b, meta = acq_setup(dev, dist.rank, precision)
+def run_acq(dist, dev, steps, warmup, precision=gc.ACQ_F64, records=None):
+    if records is None:
+        records = ACQ_RECORDS if precision == gc.ACQ_F64 else 1
+    ctx, b, meta = acq_setup(dev, dist.rank, precision, records)
     for _ in range(warmup):
         acq_step(ctx, b)
     ctx.sync()
-    # correctness guard: the planted PRNs must be found (cheap, outside timing)
-    res = b["d_res"].download(gc.ACQ_RESULT)
-    found = sum(1 for p in meta["planted"] if res[p - 1]["metric"] > 2.5)
+    # correctness guard: the planted PRNs must be found in every record (cheap,
+    # outside timing)
+    res = b["d_res"].download(gc.ACQ_RESULT).reshape(records, N_PRN)
+    found = sum(1 for r in range(records) for p in meta["planted"] if res[r][p - 1]["metric"] > 2.5)
     # kernel timing on every EV_EVERY-th step: an event record next to the
     # persistent correlation kernel costs a few us of stream gap
     ev_steps = list(range(0, steps, EV_EVERY))
@@ -151,8 +162,8 @@ def run_acq(dist, dev, steps, warmup, precision=gc.ACQ_F64):
     dist.barrier()
     dt = dist.max(t1 - t0)
     corr_ms = float(np.mean([a.elapsed_ms(z) for a, z in evs.values()]))
-    return dict(dt=dt, corr_ms=dist.max(corr_ms), found=found, n_planted=len(meta["planted"]),
-                meta=meta)
+    return dict(dt=dt, corr_ms=dist.max(corr_ms), found=found,
+                n_planted=len(meta["planted"]) * records, records=records, meta=meta)
 
 
 def run_track(dist, dev, steps, warmup):
@@ -875,9 +886,10 @@ def main():
 
     if dist.rank == 0:
         W = dist.world
-        cells = CELLS_PER_SEARCH * a.steps * W
+        R = acq["records"]
+        cells = CELLS_PER_SEARCH * a.steps * W * R
         value = cells / acq["dt"]
-        flop_launch = N_PRN * N_BINS * N_BLK * N * FLOP_PER_CELL_BLOCK
+        flop_launch = N_PRN * N_BINS * N_BLK * N * FLOP_PER_CELL_BLOCK * R
         achieved = flop_launch / (acq["corr_ms"] * 1e-3) / 1e12
         out = {
             "metric": METRIC, "value": value, "unit": "cells/s", "n_gpus": W,
@@ -886,22 +898,25 @@ def main():
             "data": "synthetic (deterministic 2-bit IQ with 8 planted GPS signals per rank)",
             "config": {"workload": "BASELINE config 2: 32-PRN x 41-bin cold-start acquisition, "
                                    "1 ms coherent, 2 blocks (acquisition.sci), 16.368 Msps, "
-                                   "fp64 as the reference computes it",
+                                   f"fp64 as the reference computes it; {R} consecutive 2-ms "
+                                   "records of one receiver per step, searched in one "
+                                   "correlation launch (gnsscorr_acq_set_records)",
                        "prns": N_PRN, "bins": N_BINS, "blocks": N_BLK, "samples_per_code": N,
-                       "cells_per_search": CELLS_PER_SEARCH,
-                       "parallelism": f"weak: one search per GPU per step x {W} GPUs"},
+                       "cells_per_search": CELLS_PER_SEARCH, "records_per_step": R,
+                       "parallelism": f"weak: {R} searches per GPU per step x {W} GPUs"},
             "roofline": {"bound": "valu", "kernel": ACQ64_KERNEL, "achieved": achieved,
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
                          "frac": achieved / PEAK_FP64_TFLOPS,
                          "traffic": pmc_traffic(ACQ64_KERNEL, "acq"),
                          "kernel_ms_per_launch": acq["corr_ms"],
                          "flop_per_launch": flop_launch},
-            "search_latency_ms": acq["dt"] / a.steps * 1e3,
+            "ms_per_search": acq["dt"] / a.steps / R * 1e3,
             "planted_found": f"{acq['found']}/{acq['n_planted']}",
             "ranks": rank_info,
         }
         if acq32:
-            a32 = flop_launch / (acq32["corr_ms"] * 1e-3) / 1e12
+            cells = CELLS_PER_SEARCH * a.steps * W
+            a32 = flop_launch / R / (acq32["corr_ms"] * 1e-3) / 1e12
             out["acquisition_f32"] = {
                 "metric": "acquisition cells/sec (config 2, single-precision fast path)",
                 "value": cells / acq32["dt"], "unit": "cells/s", "dtype": "f32",

@@ -1163,7 +1163,7 @@ __device__ __forceinline__ gnsscorr_acq_row combine_blocks(const gnsscorr_acq_ro
 
 // one wavefront per group (lane = 0..63); see acq_select_kernel
 __device__ void select_group(int g, int lane, const gnsscorr_acq_row* __restrict__ stats,
-                             int n_bins, int n_blocks, int mode,
+                             int n_bins, int n_blocks, int mode, int gpr,
                              const int* __restrict__ group_freq,
                              const double* __restrict__ freqs, gnsscorr_acq_row* __restrict__ rows,
                              gnsscorr_acq_result* __restrict__ res) {
@@ -1201,7 +1201,7 @@ __device__ void select_group(int g, int lane, const gnsscorr_acq_row* __restrict
     // winning row's own argmax (second peak then centred on the row's argmax)
     o.pad = cp != rb.argmax;
     o.pad2 = 0;
-    o.carr_freq = freqs[group_freq[(long)g * n_bins + bin]];
+    o.carr_freq = freqs[group_freq[(long)(g % gpr) * n_bins + bin]];   // g: rec * gpr + group
     res[g] = o;
   }
 }
@@ -1209,9 +1209,9 @@ __device__ void select_group(int g, int lane, const gnsscorr_acq_row* __restrict
 __global__ __launch_bounds__(64) void acq_select_kernel(
     const gnsscorr_acq_row* __restrict__ stats, int n_groups, int n_bins, int n_blocks, int mode,
     const int* __restrict__ group_freq, const double* __restrict__ freqs,
-    gnsscorr_acq_row* __restrict__ rows, gnsscorr_acq_result* __restrict__ res) {
-  select_group(blockIdx.x, threadIdx.x, stats, n_bins, n_blocks, mode, group_freq, freqs, rows,
-               res);
+    gnsscorr_acq_row* __restrict__ rows, gnsscorr_acq_result* __restrict__ res, int gpr) {
+  select_group(blockIdx.x, threadIdx.x, stats, n_bins, n_blocks, mode, gpr, group_freq, freqs,
+               rows, res);
 }
 
 // BEST_OF_BLOCKS statistics only (unit = (row, block)); launched with at most
@@ -1603,11 +1603,12 @@ static int forward_launch(gnsscorr_acq_ctx* c, const int8_t* src, int iq, int n_
 }
 
 static int check_search(gnsscorr_acq_ctx* c, int n_blocks, int n_freqs, int mode) {
-  if (n_blocks < 1 || n_blocks * c->coh > c->cfg.max_blocks || n_freqs < 1 ||
+  if (n_blocks < 1 || n_blocks * c->coh * c->recs > c->cfg.max_blocks || n_freqs < 1 ||
       n_freqs > c->cfg.max_freqs || c->n_codes < 1 ||
       (mode != GNSSCORR_ACQ_BEST_OF_BLOCKS && mode != GNSSCORR_ACQ_NONCOHERENT)) {
-    gnsscorr_set_error("gnsscorr_acq: bad arguments (blocks %d/%d, freqs %d/%d, codes %d)",
-                       n_blocks, c->cfg.max_blocks, n_freqs, c->cfg.max_freqs, c->n_codes);
+    gnsscorr_set_error("gnsscorr_acq: bad arguments (blocks %d x coherent %d x records %d / "
+                       "max_blocks %d, freqs %d/%d, codes %d)", n_blocks, c->coh, c->recs,
+                       c->cfg.max_blocks, n_freqs, c->cfg.max_freqs, c->n_codes);
     return GNSSCORR_EINVAL;
   }
   return GNSSCORR_OK;
@@ -1622,9 +1623,11 @@ static int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n
     return GNSSCORR_EINVAL;
   }
   if (c->prec == GNSSCORR_ACQ_F64) {
-    rc = acq64_spectra(c, d_if, iq, n_blocks, n_freqs, d_freqs);
+    // records are contiguous, so they are recs * n_blocks blocks of one IF
+    rc = acq64_spectra(c, d_if, iq, n_blocks * c->recs, n_freqs, d_freqs);
     if (rc) return rc;
     c->spec_blocks = n_blocks;
+    c->spec_recs = c->recs;
     c->spec_freqs = n_freqs;
     return GNSSCORR_OK;
   }
@@ -1659,9 +1662,11 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
     return GNSSCORR_EINVAL;
   }
   const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;  // work units per row
-  rc = ensure_order(c, n_groups, n_bins, upr);
+  const int nrec = c->prec == GNSSCORR_ACQ_F64 ? c->spec_recs : 1;
+  const int gall = n_groups * nrec;   // virtual groups rec * n_groups + g
+  rc = ensure_order(c, gall, n_bins, upr);
   if (rc) return rc;
-  rc = acq_grow((void**)&c->d_stats, &c->cap_stats, (size_t)n_groups * n_bins * n_blocks,
+  rc = acq_grow((void**)&c->d_stats, &c->cap_stats, (size_t)gall * n_bins * n_blocks,
             sizeof(gnsscorr_acq_row));
   if (rc) return rc;
   const int n_units = n_groups * n_bins * upr;
@@ -1688,6 +1693,7 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
   HIP_TRY(hipGetLastError());
   }
   c->stat_groups = n_groups;
+  c->stat_recs = nrec;
   c->stat_bins = n_bins;
   c->stat_blocks = n_blocks;
   c->stat_mode = mode;
@@ -1696,8 +1702,8 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
       gnsscorr_set_error("gnsscorr_acq_correlate: d_res needs d_rows and d_freqs");
       return GNSSCORR_EINVAL;
     }
-    hipLaunchKernelGGL(acq_select_kernel, dim3(n_groups), dim3(64), 0, c->stream, c->d_stats,
-                       n_groups, n_bins, n_blocks, mode, d_gfreq, d_freqs, d_rows, d_res);
+    hipLaunchKernelGGL(acq_select_kernel, dim3(gall), dim3(64), 0, c->stream, c->d_stats,
+                       gall, n_bins, n_blocks, mode, d_gfreq, d_freqs, d_rows, d_res, n_groups);
     HIP_TRY(hipGetLastError());
   }
   return GNSSCORR_OK;
@@ -1749,9 +1755,10 @@ extern "C" int gnsscorr_acq_select_dev(gnsscorr_acq_ctx* c, int n_groups, int n_
     return GNSSCORR_EINVAL;
   }
   HIP_TRY(hipSetDevice(c->cfg.device));
-  hipLaunchKernelGGL(acq_select_kernel, dim3(n_groups), dim3(64), 0, c->stream, c->d_stats,
-                     n_groups, n_bins, c->stat_blocks, c->stat_mode, d_group_freq, d_freqs, d_rows,
-                     d_res);
+  const int gall = n_groups * c->stat_recs;
+  hipLaunchKernelGGL(acq_select_kernel, dim3(gall), dim3(64), 0, c->stream, c->d_stats, gall,
+                     n_bins, c->stat_blocks, c->stat_mode, d_group_freq, d_freqs, d_rows, d_res,
+                     n_groups);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }
@@ -1773,10 +1780,10 @@ extern "C" int gnsscorr_acq_search_dev(gnsscorr_acq_ctx* c, const int8_t* d_if, 
 static int stage_host(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blocks, int n_freqs,
                       const double* h_freqs, int n_groups, int n_bins, const int32_t* h_gcode,
                       const int32_t* h_gfreq) {
-  if (n_blocks < 1 || n_blocks * c->coh > c->cfg.max_blocks || n_freqs < 1 ||
+  if (n_blocks < 1 || n_blocks * c->coh * c->recs > c->cfg.max_blocks || n_freqs < 1 ||
       n_freqs > c->cfg.max_freqs) {
-    gnsscorr_set_error("gnsscorr_acq_search: n_blocks (x coherent ms) / n_freqs outside the "
-                       "context capacity");
+    gnsscorr_set_error("gnsscorr_acq_search: n_blocks (x coherent ms x records) / n_freqs "
+                       "outside the context capacity");
     return GNSSCORR_EINVAL;
   }
   for (int g = 0; g < n_groups; g++) {
@@ -1794,12 +1801,15 @@ static int stage_host(gnsscorr_acq_ctx* c, const int8_t* h_if, int iq, int n_blo
   }
   const size_t R = (size_t)n_groups * n_bins;
   int rc;
-  if ((rc = acq_grow((void**)&c->d_rows, &c->cap_rows, R, sizeof(gnsscorr_acq_row)))) return rc;
-  if ((rc = acq_grow((void**)&c->d_res, &c->cap_res, n_groups, sizeof(gnsscorr_acq_result)))) return rc;
+  if ((rc = acq_grow((void**)&c->d_rows, &c->cap_rows, R * c->recs, sizeof(gnsscorr_acq_row))))
+    return rc;
+  if ((rc = acq_grow((void**)&c->d_res, &c->cap_res, (size_t)n_groups * c->recs,
+                     sizeof(gnsscorr_acq_result))))
+    return rc;
   if ((rc = acq_grow((void**)&c->d_gcode, &c->cap_gcode, n_groups, sizeof(int)))) return rc;
   if ((rc = acq_grow((void**)&c->d_gfreq, &c->cap_gfreq, R, sizeof(int)))) return rc;
   HIP_TRY(hipMemcpyAsync(c->d_if, h_if,
-                         (size_t)if_bytes((int64_t)n_blocks * c->coh * c->cfg.n_samples *
+                         (size_t)if_bytes((int64_t)c->recs * n_blocks * c->coh * c->cfg.n_samples *
                                               ((iq & GNSSCORR_IF_IQ) ? 2 : 1),
                                           iq & GNSSCORR_IF_PACKED2),
                          hipMemcpyHostToDevice, c->stream));
@@ -1828,10 +1838,11 @@ extern "C" int gnsscorr_acq_search(gnsscorr_acq_ctx* c, const int8_t* h_if, int 
                      c->d_gcode, c->d_gfreq, spc, c->d_rows, c->d_res, nullptr, -1);
   if (rc) return rc;
   if (h_rows)
-    HIP_TRY(hipMemcpyAsync(h_rows, c->d_rows, sizeof(gnsscorr_acq_row) * n_groups * n_bins,
+    HIP_TRY(hipMemcpyAsync(h_rows, c->d_rows,
+                           sizeof(gnsscorr_acq_row) * c->recs * n_groups * n_bins,
                            hipMemcpyDeviceToHost, c->stream));
   if (h_res)
-    HIP_TRY(hipMemcpyAsync(h_res, c->d_res, sizeof(gnsscorr_acq_result) * n_groups,
+    HIP_TRY(hipMemcpyAsync(h_res, c->d_res, sizeof(gnsscorr_acq_result) * c->recs * n_groups,
                            hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return GNSSCORR_OK;
@@ -1847,11 +1858,17 @@ extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, i
   }
   HIP_TRY(hipSetDevice(c->cfg.device));
   const int32_t gc = code, gf = 0;
+  const int recs = c->recs;   // one record, whatever set_records says
+  c->recs = 1;
   int rc = stage_host(c, h_if, iq, n_blocks, 1, &freq, 1, 1, &gc, &gf);
-  if (rc) return rc;
-  if (!c->d_dump) HIP_TRY(hipMalloc(&c->d_dump, sizeof(double) * c->cfg.n_samples));
-  rc = search_launch(c, c->d_if, iq, n_blocks, GNSSCORR_ACQ_BEST_OF_BLOCKS, 1, c->d_freqs, 1, 1,
-                     c->d_gcode, c->d_gfreq, 16, c->d_rows, nullptr, c->d_dump, block);
+  if (!rc && !c->d_dump && hipMalloc(&c->d_dump, sizeof(double) * c->cfg.n_samples) != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_acq_power_row: out of device memory");
+    rc = GNSSCORR_ENOMEM;
+  }
+  if (!rc)
+    rc = search_launch(c, c->d_if, iq, n_blocks, GNSSCORR_ACQ_BEST_OF_BLOCKS, 1, c->d_freqs, 1,
+                       1, c->d_gcode, c->d_gfreq, 16, c->d_rows, nullptr, c->d_dump, block);
+  c->recs = recs;
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(h_power, c->d_dump, sizeof(double) * c->cfg.n_samples,
                          hipMemcpyDeviceToHost, c->stream));
@@ -1865,6 +1882,21 @@ extern "C" int gnsscorr_acq_set_coherent(gnsscorr_acq_ctx* c, int coh_ms) {
     return GNSSCORR_EINVAL;
   }
   c->coh = coh_ms;
+  c->spec_blocks = 0;   // resident spectra were made with the previous setting
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_set_records(gnsscorr_acq_ctx* c, int n_records) {
+  if (!c || n_records < 1 || n_records > c->cfg.max_blocks) {
+    gnsscorr_set_error("gnsscorr_acq_set_records: need 1 <= n_records <= max_blocks");
+    return GNSSCORR_EINVAL;
+  }
+  if (n_records > 1 && (c->prec != GNSSCORR_ACQ_F64 || c->plan64 == 3)) {
+    gnsscorr_set_error("gnsscorr_acq_set_records: several records per search need the fp64 "
+                       "precision and a compiled plan (n_samples %d or %d)", 16368, 16000);
+    return GNSSCORR_EINVAL;
+  }
+  c->recs = n_records;
   c->spec_blocks = 0;   // resident spectra were made with the previous setting
   return GNSSCORR_OK;
 }

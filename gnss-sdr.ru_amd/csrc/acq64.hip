@@ -885,7 +885,8 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     const v2d* __restrict__ X, const v2d* __restrict__ F, int rs, int n_blocks,
     const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins, int spc,
     gnsscorr_acq_row* __restrict__ stats, double* __restrict__ dump, int dump_block,
-    const int* __restrict__ order, const int2* __restrict__ fmap, const v2d* __restrict__ twN) {
+    const int* __restrict__ order, const int2* __restrict__ fmap, const v2d* __restrict__ twN,
+    int gpr, int nbT) {
   constexpr int N = P::N, R1 = P::R1, R3 = P::R3, T = P::T, K3 = P::K3, L = P::L;
   constexpr bool kNC = MODE == GNSSCORR_ACQ_NONCOHERENT;
   __shared__ double lds[N];
@@ -901,7 +902,10 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   const int rowid = kNC ? unit : unit / n_blocks;
   const int blk0 = kNC ? 0 : unit % n_blocks;
   const int nblk = kNC ? n_blocks : 1;
-  const int g = rowid / n_bins, bin = rowid % n_bins;
+  // records (gnsscorr_acq_set_records): virtual group gv = rec * gpr + g reads
+  // blocks rec * n_blocks .. of the nbT resident blocks per class
+  const int gv = rowid / n_bins, bin = rowid % n_bins;
+  const int rec = gv / gpr, g = gv - rec * gpr;
   const int code = group_code[g];
   const int2 fm = fmap[group_freq[g * n_bins + bin]];
   const int m = fm.y;
@@ -912,7 +916,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
 
   for (int i = 0; i < nblk; i++) {
     const int blk = blk0 + i;
-    const v2d* Xb = X + ((long)fm.x * n_blocks + blk) * rs;
+    const v2d* Xb = X + ((long)fm.x * nbT + rec * n_blocks + blk) * rs;
     // the code row is the same for every block: keep the compiler from
     // hoisting its loads out of the block loop (they would stay live in
     // registers across the whole transform)
@@ -1190,13 +1194,14 @@ int fwd_launch(gnsscorr_acq_ctx* c, const v2d* in, const int* n_cls_dev, int per
 template <class P>
 int corr_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_units, int n_bins,
                 const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
-                int dump_block) {
+                int dump_block, int gpr) {
+  const int nbT = n_blocks * c->spec_recs;
 
 #define ACQ64_LAUNCH(M, D)                                                                  \
   hipLaunchKernelGGL((acq64_corr_kernel<P, M, D>), dim3(n_units), dim3(P::TB), 0, c->stream, \
                      (const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, d_gcode,   \
                      d_gfreq, n_bins, spc, c->d_stats, d_dump, dump_block, c->d_order,         \
-                     c->d_fmap64, (const v2d*)c->d_twN)
+                     c->d_fmap64, (const v2d*)c->d_twN, gpr, nbT)
   if (d_dump)
     ACQ64_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
   else if (mode == GNSSCORR_ACQ_NONCOHERENT)
@@ -1653,13 +1658,15 @@ int acq64_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks,
 int acq64_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
                     const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
                     int dump_block) {
+  // n_groups per record; the units of every record of the resident spectra run
+  // in one launch (virtual groups rec * n_groups + g)
   const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;
-  const int n_units = n_groups * n_bins * upr;
+  const int n_units = c->spec_recs * n_groups * n_bins * upr;
   if (c->plan64 == 3)
     return g_correlate(c, n_blocks, mode, n_groups, n_bins, d_gcode, d_gfreq, spc, d_dump,
                        dump_block);
   return c->plan64 == 1 ? corr_launch<PlanA>(c, n_blocks, mode, n_units, n_bins, d_gcode, d_gfreq,
-                                             spc, d_dump, dump_block)
+                                             spc, d_dump, dump_block, n_groups)
                         : corr_launch<PlanB>(c, n_blocks, mode, n_units, n_bins, d_gcode, d_gfreq,
-                                             spc, d_dump, dump_block);
+                                             spc, d_dump, dump_block, n_groups);
 }

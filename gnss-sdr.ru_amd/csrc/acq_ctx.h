@@ -48,9 +48,11 @@ struct gnsscorr_acq_ctx {
   int* d_nclass = nullptr;
   int n_cu = 256;                       // persistent grid of the pipelined kernel
   int coh = 1;                          // code periods per coherent block (set_coherent)
+  int recs = 1;                         // records per search (set_records, fp64 plans)
+  int spec_recs = 1;                    // records of the resident IF spectra
   gnsscorr_acq_row* d_stats = nullptr;  // per (row, block) statistics
   size_t cap_stats = 0;
-  int stat_groups = 0, stat_bins = 0, stat_blocks = 0, stat_mode = 0;
+  int stat_groups = 0, stat_bins = 0, stat_blocks = 0, stat_mode = 0, stat_recs = 1;
   // host-API staging
   int8_t* d_if = nullptr;
   double* d_freqs = nullptr;

@@ -162,6 +162,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
     "gnsscorr_acq_spectra_dev", "gnsscorr_acq_correlate_dev", "gnsscorr_acq_select_dev",
     "gnsscorr_acq_sync", "gnsscorr_acq_stream", "gnsscorr_acq_set_coherent",
+    "gnsscorr_acq_set_records",
     "gnsscorr_sgt_loop_coefs", "gnsscorr_sgt_init_chan", "gnsscorr_sgt_create",
     "gnsscorr_sgt_destroy", "gnsscorr_sgt_track_dev", "gnsscorr_sgt_track", "gnsscorr_sgt_sync",
     "gnsscorr_sgt_stream",
@@ -233,6 +234,7 @@ def lib() -> C.CDLL:
         "gnsscorr_acq_select_dev": (I, [P, I, I, P, P, P, P]),
         "gnsscorr_acq_sync": (I, [P]),
         "gnsscorr_acq_set_coherent": (I, [P, I]),
+        "gnsscorr_acq_set_records": (I, [P, I]),
         "gnsscorr_acq_stream": (P, [P]),
         "gnsscorr_sgt_loop_coefs": (None, [C.POINTER(SgtCfg)] + [C.POINTER(D)] * 5),
         "gnsscorr_sgt_init_chan": (I, [C.POINTER(SgtCfg), I, I, I64, I64, D, P]),
@@ -556,6 +558,7 @@ class AcqCtx:
         self.h = h
         self.n = n_samples
         self.fs = samp_rate
+        self.records = 1
 
     def close(self):
         if getattr(self, "h", None):
@@ -576,13 +579,22 @@ class AcqCtx:
         group_code = np.ascontiguousarray(group_code, np.int32)
         group_freq = np.ascontiguousarray(group_freq, np.int32).reshape(len(group_code), -1)
         G, B = group_freq.shape
-        rows = np.zeros(G * B, ACQ_ROW)
-        res = np.zeros(G, ACQ_RESULT)
+        R = self.records
+        rows = np.zeros(R * G * B, ACQ_ROW)
+        res = np.zeros(R * G, ACQ_RESULT)
         _check(lib().gnsscorr_acq_search(self.h, _ptr(if_samples), int(iq), n_blocks, mode,
                                          len(freqs), _ptr(freqs), G, B, _ptr(group_code),
                                          _ptr(group_freq), spc, _ptr(rows), _ptr(res)),
                "gnsscorr_acq_search")
-        return res, rows.reshape(G, B)
+        if R == 1:
+            return res, rows.reshape(G, B)
+        return res.reshape(R, G), rows.reshape(R, G, B)
+
+    def set_records(self, n_records: int):
+        """Records per search (fp64): n_records IF records end to end, searched
+        in one launch; search() then returns (R, G) results and (R, G, B) rows."""
+        _check(lib().gnsscorr_acq_set_records(self.h, int(n_records)), "gnsscorr_acq_set_records")
+        self.records = int(n_records)
 
     def set_coherent(self, coh_ms: int):
         """settings.acqCohIntegration: code periods per coherent block (default 1)."""
