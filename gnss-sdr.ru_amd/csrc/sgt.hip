@@ -67,8 +67,12 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-template <int FT, bool CLOSED>
-__global__ __launch_bounds__(1024) void sgt_track_kernel(
+// WAVE: one wavefront per channel (many-channel launches): the butterfly sums
+// leave the totals in every lane, so an epoch needs no LDS partials and no
+// barrier, and the loop filters run once per wave instead of once per wave of
+// a 4-16-wave workgroup.
+template <int FT, bool CLOSED, bool WAVE>
+__global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
     SgtParams p, const int8_t* __restrict__ ifbuf, int64_t stride, int64_t n_samples,
     const uint32_t* __restrict__ codes, gnsscorr_sgt_chan* __restrict__ chans, int n_epochs,
     gnsscorr_sgt_epoch* __restrict__ out) {
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
   __shared__ double s_sgn[kPadLen];   // the code as +-1.0: E/P/L accumulate with one fma
   __shared__ double s_part[2][kMaxWaves][6];
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
-  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = WAVE ? 64 : blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = T >> 6;
   gnsscorr_sgt_chan c = chans[ch];
   const int L = p.code_length;
@@ -98,12 +102,19 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
     }
     const double step = c.code_freq / p.fs;
     const double blk_d = ceil((dL - c.rem_code) / step);
-    const int64_t blk = (int64_t)blk_d;
-    if (c.pos + blk > n_samples) {  // tracking.sci:273-277: not enough samples
+    // tracking.sci:273-277: not enough samples (NaN or huge blksize from a
+    // corrupted state stops too, as does a blksize of 2^31 or more)
+    if (!(blk_d <= (double)(n_samples - c.pos) && blk_d < 2147483648.0)) {
       c.status = 1;
-      if (tid == 0) { gnsscorr_sgt_epoch z = {}; z.status = 1; z.blksize = (int32_t)blk; *rec = z; }
+      if (tid == 0) {
+        gnsscorr_sgt_epoch z = {};
+        z.status = 1;
+        z.blksize = blk_d >= 0.0 && blk_d < 2147483647.0 ? (int32_t)blk_d : -1;
+        *rec = z;
+      }
       continue;
     }
+    const int blk = (int)blk_d;
     const double aE = c.rem_code - p.spc, aL = c.rem_code + p.spc, aP = c.rem_code;
     const double A = (c.carr_freq * 2.0) * M_PI;        // (carrFreq * 2.0 * %pi)
     // carrier at the thread's first sample, rotation by T samples
@@ -113,22 +124,28 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
     sincos(thw, &sw, &cw);   // (sgt.o is built with promote-alloca-to-lds off)
     double ie = 0, ip = 0, il = 0, qe = 0, qp = 0, ql = 0;
     const int8_t* src = base + (FT == 2 ? 2 : 1) * c.pos;
-    // unrolled so the IF loads of several samples are in flight together (one
-    // load in flight per iteration left the loop waiting on memory latency)
-#pragma unroll 8
-    for (int64_t k = tid; k < blk; k += T) {
+    // I/Q byte order as bit-field offsets (switchIQ without a per-sample select)
+    const int sh_re = p.switch_iq ? 8 : 0, sh_im = 8 - sh_re;
+    // kU samples per thread per pass.  The IF words of pass n+1 are loaded
+    // while pass n is processed (with a plain unrolled loop the compiler kept
+    // one load in flight and waited on memory latency at every sample); the
+    // last, partial pass is guarded per sample.
+    constexpr int kU = 8;
+    auto load = [&](int k) -> int {
+      if (FT == 2) return *reinterpret_cast<const uint16_t*>(src + 2 * k);
+      return src[k];
+    };
+    auto sample = [&](int k, int w) {
       const double t = (double)k * step;
       const double gE = s_sgn[clampu((int)ceil(aE + t), L + 1)];
       const double gP = s_sgn[clampu((int)ceil(aP + t), L + 1)];
       const double gL = s_sgn[clampu((int)ceil(aL + t), L + 1)];
       double re, im;
       if (FT == 2) {
-        const char2 v = *reinterpret_cast<const char2*>(src + 2 * k);
-        re = (double)v.x;
-        im = (double)v.y;
-        if (p.switch_iq) { const double tmp = re; re = im; im = tmp; }
+        re = (double)(int)__builtin_amdgcn_sbfe(w, sh_re, 8);   // (the builtin is typed unsigned)
+        im = (double)(int)__builtin_amdgcn_sbfe(w, sh_im, 8);
       } else {
-        re = (double)src[k];
+        re = (double)w;
         im = 0.0;
       }
       // (explicit fma: the carrier and the sums only need fp64 accuracy; the
@@ -140,19 +157,52 @@ __global__ __launch_bounds__(1024) void sgt_track_kernel(
       const double c2 = fma(cs, cw, -(sn * sw));
       sn = fma(sn, cw, cs * sw);
       cs = c2;
+    };
+    const int n_full = blk / (kU * T);   // passes whose kU samples all exist for every thread
+    int k0 = tid;
+    int w[kU];
+    if (n_full > 0) {
+#pragma unroll
+      for (int u = 0; u < kU; u++) w[u] = load(k0 + u * T);
+    }
+    for (int n = 0; n < n_full; n++, k0 += kU * T) {
+      int cur[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) cur[u] = w[u];
+      if (n + 1 < n_full) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) w[u] = load(k0 + kU * T + u * T);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) sample(k0 + u * T, cur[u]);
+    }
+    // the remainder: fewer than kU * T samples
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int k = k0 + u * T;
+      w[u] = k < blk ? load(k) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int k = k0 + u * T;
+      if (k < blk) sample(k, w[u]);
     }
     ie = wave_sum(ie); ip = wave_sum(ip); il = wave_sum(il);
     qe = wave_sum(qe); qp = wave_sum(qp); ql = wave_sum(ql);
-    const int par = e & 1;
-    if (lane == 0) {
-      s_part[par][wave][0] = ie; s_part[par][wave][1] = ip; s_part[par][wave][2] = il;
-      s_part[par][wave][3] = qe; s_part[par][wave][4] = qp; s_part[par][wave][5] = ql;
-    }
-    __syncthreads();
-    double S[6] = {0, 0, 0, 0, 0, 0};
-    for (int w = 0; w < nw; w++)
+    double S[6] = {ie, ip, il, qe, qp, ql};
+    if constexpr (!WAVE) {
+      const int par = e & 1;
+      if (lane == 0) {
+        s_part[par][wave][0] = ie; s_part[par][wave][1] = ip; s_part[par][wave][2] = il;
+        s_part[par][wave][3] = qe; s_part[par][wave][4] = qp; s_part[par][wave][5] = ql;
+      }
+      __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 6; j++) S[j] += s_part[par][w][j];
+      for (int j = 0; j < 6; j++) S[j] = 0.0;
+      for (int w = 0; w < nw; w++)
+#pragma unroll
+        for (int j = 0; j < 6; j++) S[j] += s_part[par][w][j];
+    }
     const double I_E = S[0], I_P = S[1], I_L = S[2], Q_E = S[3], Q_P = S[4], Q_L = S[5];
 
     // carry-over (tracking.sci:301-313)
@@ -357,24 +407,34 @@ extern "C" int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx* c, const int8_t* d_if, i
     return GNSSCORR_EINVAL;
   }
   HIP_TRY(hipSetDevice(c->cfg.device));
-  // small channel counts: wide workgroups (latency); many channels: 256 threads
-  const int T = n_ch >= 512 ? 256 : (n_ch >= 128 ? 512 : 1024);
-  dim3 grid(n_ch), block(T);
-  if (c->cfg.file_type == 2) {
-    if (closed_loop)
-      hipLaunchKernelGGL((sgt_track_kernel<2, true>), grid, block, 0, c->stream, c->p, d_if,
-                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
-    else
-      hipLaunchKernelGGL((sgt_track_kernel<2, false>), grid, block, 0, c->stream, c->p, d_if,
-                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
-  } else {
-    if (closed_loop)
-      hipLaunchKernelGGL((sgt_track_kernel<1, true>), grid, block, 0, c->stream, c->p, d_if,
-                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
-    else
-      hipLaunchKernelGGL((sgt_track_kernel<1, false>), grid, block, 0, c->stream, c->p, d_if,
-                         stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);
+  // many channels: one wave per channel (throughput); fewer: 256-thread
+  // workgroups, which also give the lowest epoch latency for the 14-channel
+  // config-4 receiver (measured 9.3 us vs 9.4 / 11.6 us at 512 / 1024 threads,
+  // 14.9 us at 128); a handful of channels: 512.  GNSSCORR_SGT_THREADS
+  // overrides (64 = wave mode, 128..1024).
+  int T = n_ch >= 1024 ? 64 : (n_ch >= 8 ? 256 : 512);
+  if (const char* ov = getenv("GNSSCORR_SGT_THREADS")) {
+    const int v = atoi(ov);
+    if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) T = v;
   }
+  dim3 grid(n_ch), block(T);
+#define SGT_LAUNCH(FT, CL)                                                                     \
+  do {                                                                                         \
+    if (T == 64)                                                                               \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, true>), grid, block, 0, c->stream, c->p,   \
+                         d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
+    else                                                                                       \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, false>), grid, block, 0, c->stream, c->p,  \
+                         d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
+  } while (0)
+  if (c->cfg.file_type == 2) {
+    if (closed_loop) SGT_LAUNCH(2, true);
+    else SGT_LAUNCH(2, false);
+  } else {
+    if (closed_loop) SGT_LAUNCH(1, true);
+    else SGT_LAUNCH(1, false);
+  }
+#undef SGT_LAUNCH
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }

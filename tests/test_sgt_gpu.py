@@ -32,9 +32,13 @@ def _glo_start(cp_chips):
     return int(round((511 - cp_chips) / 0.511e6 * FS)) + 1
 
 
+@pytest.mark.parametrize("threads", [None, "64", "1024"])
 @pytest.mark.parametrize("system,file_type,switch", [(1, 2, 0), (1, 2, 1), (0, 2, 0), (1, 1, 0)])
-def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch):
+def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch, threads, monkeypatch):
+    """threads: launch shape override (GNSSCORR_SGT_THREADS; 64 = one wave per channel)."""
     gc = gpu
+    if threads:
+        monkeypatch.setenv("GNSSCORR_SGT_THREADS", threads)
     rng = np.random.default_rng(17 + system + 3 * file_type + 7 * switch)
     n = 200000
     IF = gc.ifgen(n, [], fs=FS, iq=file_type == 2, seed=21)
@@ -156,18 +160,20 @@ def test_out_of_data_stops_like_tracking_sci(gpu):
         assert ch["status"][i] == 1 and ch["n_epochs"][i] == k
 
 
-def test_many_channels_launch_shape(gpu):
-    """>= 512 channels switch to 256-thread workgroups: same results."""
+@pytest.mark.parametrize("reps", [40, 80])
+def test_many_channels_launch_shape(gpu, reps):
+    """>= 1024 channels switch to one wave per channel: the same closed-loop
+    results as the 14-channel (256-thread) launch."""
     gc = gpu
     IF, fchs, starts, acq = _glonass_scene(gc, 4)
     d_if = gc.DevBuf.from_array(IF)
     ctx = gc.SgtCtx(1)
     ch14 = ctx.init_chans(fchs, starts, acq)
-    big = np.tile(ch14, 40)                       # 560 channels
+    big = np.tile(ch14, reps)                     # 560 / 1120 channels
     small = ch14.copy()
-    e_big = ctx.track(d_if.ptr, 0, len(IF) // 2, big, 3)
-    e_small = ctx.track(d_if.ptr, 0, len(IF) // 2, small, 3)
-    for f in SUMS:
-        a = e_big[f].reshape(40, 14, 3)
-        assert _close(a, np.broadcast_to(e_small[f], a.shape), rtol=1e-12, atol=1e-9).all()
-    assert (e_big["blksize"].reshape(40, 14, 3) == e_small["blksize"]).all()
+    e_big = ctx.track(d_if.ptr, 0, len(IF) // 2, big, 3, closed_loop=True)
+    e_small = ctx.track(d_if.ptr, 0, len(IF) // 2, small, 3, closed_loop=True)
+    for f in S.FIELDS:
+        a = e_big[f].reshape(reps, 14, 3)
+        assert _close(a, np.broadcast_to(e_small[f], a.shape), rtol=1e-12, atol=1e-9).all(), f
+    assert (e_big["blksize"].reshape(reps, 14, 3) == e_small["blksize"]).all()
