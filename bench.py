@@ -876,7 +876,7 @@ def main():
     acq = run_acq(dist, dev, a.steps, a.warmup, gc.ACQ_F64)
     acq32 = None if a.skip_track else run_acq(dist, dev, a.steps, a.warmup, gc.ACQ_F32)
     rank_info = dist.gather(dict(rank=dist.rank, device=dev, pci_bus_id=gc.pci_bus_id(dev),
-                                 hip_runtime=gc.hip_runtime_path()))
+                                 hip_runtime=gc.hip_runtime()))
     trk = None if a.skip_track else run_track(dist, dev, max(a.steps, 20), a.warmup)
     tio = None if a.skip_track else run_track_io(dist, dev, max(a.steps, 20), a.warmup)
     sgt = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup)

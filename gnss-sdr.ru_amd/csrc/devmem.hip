@@ -1,6 +1,8 @@
 // devmem.hip -- device buffers, copies, events and a device-side synthetic IF
 // filler, so C hosts (and bench.py) can keep IF, commands and results resident
 // in HBM without any other GPU runtime in the process.
+#include <dlfcn.h>
+#include <stdio.h>
 #include <hip/hip_runtime.h>
 #include "gnsscorr_internal.h"
 
@@ -17,6 +19,23 @@
 extern "C" int gnsscorr_device_pci_bus_id(int device, char* buf, int len) {
   if (!buf || len < 13) return GNSSCORR_EINVAL;
   HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
+  return GNSSCORR_OK;
+}
+
+// The HIP runtime this library's calls actually bind to: dladdr of the
+// hipMalloc the library resolved (it is linked -z now, so every HIP symbol is
+// bound when the library is loaded, before another copy of the runtime -- e.g.
+// torch's -- can enter the global scope), and that runtime's version.
+extern "C" int gnsscorr_hip_runtime(char* path, int len, int* version) {
+  if (!path || len < 2 || !version) return GNSSCORR_EINVAL;
+  Dl_info info = {};
+  hipError_t (*const fn)(void**, size_t) = &hipMalloc;
+  if (!dladdr(reinterpret_cast<void*>(fn), &info) || !info.dli_fname) {
+    gnsscorr_set_error("gnsscorr_hip_runtime: dladdr(hipMalloc) failed");
+    return GNSSCORR_EDEVICE;
+  }
+  snprintf(path, (size_t)len, "%s", info.dli_fname);
+  HIP_TRY(hipRuntimeGetVersion(version));
   return GNSSCORR_OK;
 }
 

@@ -152,7 +152,7 @@ class SdrAcqCfg(C.Structure):
 # every symbol include/gnsscorr.h + include/gnsscorr_osg.h declare
 EXPORTED_FUNCTIONS = [
     "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
-    "gnsscorr_device_pci_bus_id",
+    "gnsscorr_device_pci_bus_id", "gnsscorr_hip_runtime",
     "gnsscorr_track_create", "gnsscorr_track_destroy", "gnsscorr_track_max_dumps",
     "gnsscorr_pack2", "gnsscorr_track_if_bytes",
     "gnsscorr_track", "gnsscorr_track_dev", "gnsscorr_track_next_tic",
@@ -210,6 +210,7 @@ def lib() -> C.CDLL:
         "gnsscorr_version": (C.c_char_p, []),
         "gnsscorr_device_count": (I, []),
         "gnsscorr_device_pci_bus_id": (I, [I, P, I]),
+        "gnsscorr_hip_runtime": (I, [P, I, P]),
         "gnsscorr_track_create": (I, [C.POINTER(P), C.POINTER(TrackCfg)]),
         "gnsscorr_track_destroy": (I, [P]),
         "gnsscorr_track_max_dumps": (I, [P]),
@@ -348,16 +349,21 @@ def pci_bus_id(device: int = 0) -> str:
     return buf.value.decode()
 
 
-def hip_runtime_path() -> str:
-    """The libamdhip64 this process mapped (the library binds the first one loaded)."""
+def hip_runtime() -> dict:
+    """The libamdhip64 libgnsscorr's HIP calls bind to (gnsscorr_hip_runtime), its
+    hipRuntimeGetVersion, and every libamdhip64 the process has mapped."""
+    buf = C.create_string_buffer(4096)
+    ver = C.c_int(0)
+    _check(lib().gnsscorr_hip_runtime(buf, 4096, C.byref(ver)), "gnsscorr_hip_runtime")
+    mapped = []
     try:
         with open("/proc/self/maps") as f:
             for line in f:
-                if "libamdhip64" in line:
-                    return line.split()[-1]
+                if "libamdhip64" in line and line.split()[-1] not in mapped:
+                    mapped.append(line.split()[-1])
     except OSError:
         pass
-    return ""
+    return dict(bound=os.path.realpath(buf.value.decode()), version=ver.value, mapped=mapped)
 
 
 # ---------------------------------------------------------------- device memory

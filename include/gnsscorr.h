@@ -41,6 +41,10 @@ const char *gnsscorr_version(void);
 int gnsscorr_device_count(void);
 /* PCI bus id ("0000:xx:00.0") of a device, for run records. */
 int gnsscorr_device_pci_bus_id(int device, char *buf, int len);
+/* Path of the libamdhip64 whose hipMalloc this library calls, and
+ * hipRuntimeGetVersion() of it (for run records: a host process may map a
+ * second HIP runtime, e.g. PyTorch's). */
+int gnsscorr_hip_runtime(char *path, int len, int *version);
 
 /* ======================================================================
  * IF sample formats.  Every batched entry point that takes IF samples has an
