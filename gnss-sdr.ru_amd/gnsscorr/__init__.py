@@ -21,7 +21,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgnsscorr.so")
+# GNSSCORR_LIB: an alternative build of the same library (A/B timing in tools/)
+LIB_PATH = os.environ.get("GNSSCORR_LIB") or os.path.join(_HERE, "libgnsscorr.so")
 
 # ---------------------------------------------------------------- structs
 NCO_CMD = np.dtype([("prn", "<i4"), ("carrier_incr", "<u4"), ("code_incr", "<u4"),
