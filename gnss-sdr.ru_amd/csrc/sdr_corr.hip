@@ -87,16 +87,28 @@ __global__ __launch_bounds__(kThreads) void sdr_accum_kernel(
     const int last = ((int)sh[k] + (nend - wave0) - 1) >> 5;
     cw[k] = (wave0 < nend && lane <= last) ? codebits[(bit0 >> 5) + lane] : 0u;
   }
-  for (int n0 = wave0; n0 < nend; n0 += 64) {
-    const int n = n0 + lane;
+  // all 16 steps' packet and carrier words are loaded before the first is
+  // used (a plain loop waited on memory latency at every step: one load pair
+  // in flight per wave)
+  constexpr int kSteps = 1024 / 64;
+  uint32_t av[kSteps], bv[kSteps];
+#pragma unroll
+  for (int st = 0; st < kSteps; st++) {
+    const int n = wave0 + st * 64 + lane;
+    av[st] = n < nend ? d[n] : 0u;
+    bv[st] = n < nend ? sn[n] : 0u;
+  }
+#pragma unroll
+  for (int st = 0; st < kSteps; st++) {
+    const int n = wave0 + st * 64 + lane;
     const bool live = n < nend;
-    const uint32_t a = live ? d[n] : 0u, b = live ? sn[n] : 0u;
+    const uint32_t a = av[st], b = bv[st];
     const int32_t ai = lo16(a), aq = hi16(a), bi = lo16(b), bq = hi16(b);
     const int32_t ti = (ai * bi - aq * bq + 8192) >> 14, tq = (ai * bq + aq * bi + 8192) >> 14;
     int32_t wi = saturate ? sat16(ti) : (int32_t)(int16_t)ti;
     int32_t wq = saturate ? sat16(tq) : (int32_t)(int16_t)tq;
     if (!live) wi = wq = 0;
-    const uint32_t rel = (uint32_t)(n - wave0);   // < 1024
+    const uint32_t rel = (uint32_t)(st * 64 + lane);   // n - wave0 < 1024
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       const uint32_t r = rel + sh[k];
