@@ -9,7 +9,7 @@ if [ -n "${AB_TESTS:-}" ]; then
   tail -1 gpurun_out/ab_tests.log
 fi
 for i in 1 2 3; do
-  for V in A B; do
+  for V in ${AB_VARIANTS:-A B}; do
     GNSSCORR_LIB=$PWD/gpurun_ab/lib_$V.so timeout -k 10 200 python -u tools/bench_part.py ${AB_PART:-acq} ${AB_STEPS:-60} > gpurun_out/ab_$V$i.log 2>&1
     python -c "
 import json, sys
