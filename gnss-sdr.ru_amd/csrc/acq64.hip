@@ -1172,11 +1172,16 @@ __global__ __launch_bounds__(1024) void acq64_classify_kernel(const double* __re
     fmap[i] = make_int2(cls, mN);
     if (l == i) cfreq[cls] = resid[i];
   }
-  if (threadIdx.x == 0) {
-    int cnt = 0;
-    for (int k = 0; k < n; k++) cnt += lead[k] == k;
-    *n_classes = cnt;
-  }
+  // class count: every thread counts its own entries (one serial thread over
+  // the whole table took ~100 us at full-sky sizes, a dependent load per entry)
+  __shared__ int s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) mine += lead[i] == i;
+  atomicAdd(&s_cnt, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) *n_classes = s_cnt;
 }
 
 // ---- launch helpers ---------------------------------------------------------------
