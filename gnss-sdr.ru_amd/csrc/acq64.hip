@@ -778,11 +778,11 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
   __shared__ v2d tw3[P::R3];
   const int t = threadIdx.x;
   init_tw3<P>(tw3);
-  // one row per workgroup; the grid is an upper bound of the rows
+  // rows grid-strided over a capped grid (n_rows is an upper bound of the
+  // rows when the class count is on the device); fft_core ends on a barrier
+  // after its last LDS read, so the next row may start writing at once
   const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
-  const int w = blockIdx.x;
-  if (w >= rows) return;
-  {
+  for (int w = blockIdx.x; w < rows; w += gridDim.x) {
     const v2d* src = in + (long)w * P::N;
     v2d v1[P::K1][P::R1];
 #pragma unroll
@@ -821,17 +821,20 @@ template <class P>
 __global__ __launch_bounds__(256) void acq64_fwd1_kernel(v2d* __restrict__ io,
                                                          const int* __restrict__ n_cls_dev,
                                                          int per_cls, int n_rows) {
+  // grid-stride: the launch is sized for the host's upper bound on the rows
+  // (classes <= frequencies), capped; the actual count is read here
   const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const int row = (int)(i / P::G1), g = (int)(i % P::G1);
-  if (row >= rows) return;
-  v2d* r = io + (long)row * P::N;
-  v2d v[P::R1];
+  const long total = (long)rows * P::G1;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int row = (int)(i / P::G1), g = (int)(i % P::G1);
+    v2d* r = io + (long)row * P::N;
+    v2d v[P::R1];
 #pragma unroll
-  for (int n1 = 0; n1 < P::R1; n1++) v[n1] = r[n1 * P::G1 + g];
-  dft<P::R1>(v);
+    for (int n1 = 0; n1 < P::R1; n1++) v[n1] = r[n1 * P::G1 + g];
+    dft<P::R1>(v);
 #pragma unroll
-  for (int k1 = 0; k1 < P::R1; k1++) r[k1 * P::G1 + g] = v[k1];
+    for (int k1 = 0; k1 < P::R1; k1++) r[k1 * P::G1 + g] = v[k1];
+  }
 }
 
 // Stages 2 and 3 of one (row, k1): the G1 = R2 x R3 values k1*G1 + n2*R3 + n3
@@ -847,12 +850,13 @@ __global__ __launch_bounds__(kFwd23Threads) void acq64_fwd23_kernel(
   static_assert(G1 <= kFwd23Threads, "one output per thread");
   __shared__ v2d s_a[G1], s_b[G1];
   __shared__ v2d w2[R2], w3[R3];
+  // grid-stride over (row, k1) (see acq64_fwd1_kernel)
   const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
-  const int row = blockIdx.x / P::R1, k1 = blockIdx.x % P::R1;
-  if (row >= rows) return;
   const int t = threadIdx.x;
   if (t < R2) w2[t] = (v2d){kTw<R2>.c[t], -kTw<R2>.s[t]};
   if (t < R3) w3[t] = (v2d){kTw<R3>.c[t], -kTw<R3>.s[t]};
+  for (int u = blockIdx.x; u < rows * P::R1; u += gridDim.x) {
+  const int row = u / P::R1, k1 = u % P::R1;
   if (t < G1) s_a[t] = in[(long)row * P::N + k1 * G1 + t];
   __syncthreads();
   // (four partial sums: the latency of one dependent chain, not the FMA
@@ -884,6 +888,8 @@ __global__ __launch_bounds__(kFwd23Threads) void acq64_fwd23_kernel(
     }
     out[(long)row * rs + P::sbase(k1 * R2 + k2) + P::soff(k3)] =
         (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+  __syncthreads();   // s_a / s_b are refilled by the next (row, k1)
   }
 }
 
@@ -1193,14 +1199,21 @@ int fwd_launch(gnsscorr_acq_ctx* c, const v2d* in, const int* n_cls_dev, int per
     // rows: one workgroup per row would leave 252 CUs idle): stage 1 in place,
     // then the 16 independent 1023-point (33 x 31) transforms of every row
     v2d* io = const_cast<v2d*>(in);
+    // n_rows is an upper bound when the class count is on the device (a
+    // full-sky GLONASS part: 574 frequencies x 10 blocks for 2 classes x 10):
+    // capped grids, grid-stride kernels (92 k mostly-empty workgroups cost
+    // ~190 us of launch alone)
     const long groups = (long)n_rows * P::G1;
-    hipLaunchKernelGGL((acq64_fwd1_kernel<P>), dim3((groups + 255) / 256), dim3(256), 0,
-                       c->stream, io, n_cls_dev, per_cls, n_rows);
+    const long g1 = (groups + 255) / 256, g23 = (long)n_rows * P::R1;
+    hipLaunchKernelGGL((acq64_fwd1_kernel<P>), dim3((unsigned)(g1 < 4096 ? g1 : 4096)), dim3(256),
+                       0, c->stream, io, n_cls_dev, per_cls, n_rows);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL((acq64_fwd23_kernel<P>), dim3(n_rows * P::R1), dim3(kFwd23Threads), 0,
-                       c->stream, (const v2d*)io, n_cls_dev, per_cls, n_rows, out, c->rs64);
+    hipLaunchKernelGGL((acq64_fwd23_kernel<P>), dim3((unsigned)(g23 < 2048 ? g23 : 2048)),
+                       dim3(kFwd23Threads), 0, c->stream, (const v2d*)io, n_cls_dev, per_cls,
+                       n_rows, out, c->rs64);
   } else {
-    hipLaunchKernelGGL((acq64_fwd_kernel<P>), dim3(n_rows), dim3(P::TB), 0, c->stream, in,
+    hipLaunchKernelGGL((acq64_fwd_kernel<P>), dim3(n_rows < 512 ? n_rows : 512), dim3(P::TB), 0,
+                       c->stream, in,
                        n_cls_dev, per_cls, n_rows, out, c->rs64, (const v2d*)c->d_twN);
   }
   HIP_TRY(hipGetLastError());
