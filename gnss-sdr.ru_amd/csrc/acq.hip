@@ -551,12 +551,16 @@ __global__ __launch_bounds__(1024) void acq_classify_kernel(const double* __rest
     F[i].z = cls;
     F[i].w = mN;
   }
-  if (threadIdx.x == 0) {
-    int cnt = 0;
-    for (int k = 0; k < n; k++) cnt += F[k].x == k;
-    *n_classes = cnt;
-  }
+  // class count: every thread counts its own entries (one thread walking the
+  // table was a dependent LDS/global load per entry)
+  __shared__ int s_cnt;
+  if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
+  int mine = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) mine += F[i].x == i;
+  atomicAdd(&s_cnt, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) *n_classes = s_cnt;
   // pass 3: class frequencies and the packed shift coordinates
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int4 v = F[i];
