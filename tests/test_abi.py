@@ -79,3 +79,27 @@ def test_pack2_layout(gc):
     assert np.array_equal(got, want)
     with pytest.raises(gc.GnssCorrError):
         gc.pack2(np.array([1, 0, 3], np.int8))     # 0 is not a 2-bit level
+
+
+def test_hip_runtime_binds_at_load_before_torch():
+    """The library's HIP calls reach the runtime it was built against even once
+    torch.distributed has mapped torch's own libamdhip64 (bench.py's N > 1 order:
+    libgnsscorr first, then torch).  A child process keeps this one's mappings
+    clean; no GPU is touched (hipRuntimeGetVersion needs no device)."""
+    import subprocess
+    import sys
+    code = (
+        "import sys, json; sys.path.insert(0, %r)\n"
+        "import gnsscorr as gc\n"
+        "gc.lib()\n"
+        "import torch.distributed\n"
+        "print(json.dumps(gc.hip_runtime()))\n" % os.path.join(ROOT, "gnss-sdr.ru_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import json
+    rt = json.loads(out.stdout.strip().splitlines()[-1])
+    assert "/torch/" not in rt["bound"], rt
+    assert "libamdhip64" in rt["bound"] and rt["version"] > 0, rt
+    L = C.CDLL(os.path.join(ROOT, "gnss-sdr.ru_amd", "gnsscorr", "libgnsscorr.so"))
+    assert hasattr(L, "gnsscorr_hip_runtime")
