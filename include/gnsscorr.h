@@ -399,7 +399,9 @@ typedef struct {          /* trackResults(ch).* for one epoch (tracking.sci:387-
   double  i_e, i_p, i_l, q_e, q_p, q_l;
   double  carr_freq, code_freq, absolute_sample;
   double  dll_discr, dll_discr_filt, pll_discr, pll_discr_filt;
-  int32_t blksize;
+  int32_t blksize;        /* samples of the epoch; on a stop record the blksize that did
+                             not fit, or -1 if it is not a representable count (NaN, or
+                             2^31 or more: a corrupted state, which also stops) */
   int32_t status;         /* 0 ok; 1 = this epoch was not processed (out of data) */
 } gnsscorr_sgt_epoch;     /* 112 bytes */
 
