@@ -109,7 +109,7 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
       if (tid == 0) {
         gnsscorr_sgt_epoch z = {};
         z.status = 1;
-        z.blksize = blk_d >= 0.0 && blk_d < 2147483647.0 ? (int32_t)blk_d : -1;
+        z.blksize = blk_d >= 0.0 && blk_d < 2147483648.0 ? (int32_t)blk_d : -1;
         *rec = z;
       }
       continue;
