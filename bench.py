@@ -631,6 +631,31 @@ def cpu_baseline_sdr(bufs, budget_s=5.0):
                        f"{dt:.1f} s")
 
 
+def cpu_baseline_sdr_accum(budget_s=3.0):
+    """Correlator::Accum on the host: the scalar C restatement (oracle/sdr_corr.c, sdrc_accum:
+    cmulsc >> 14 + E/P/L prn_accum_new) over one 2048-sample packet per call."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+    import sdr_oracle
+    o = sdr_oracle.OracleSdrCorr()
+    rng = np.random.default_rng(0x5EED0006)
+    data = rng.integers(-512, 512, (2048, 2), dtype=np.int16)
+    res = np.zeros(1, sdr_oracle.CORR)
+    sine = o.carrier.reshape(-1, 2)[: 2048]
+    rows = [np.ascontiguousarray(o.code.reshape(-1)[k * sdr_oracle.ROW:k * sdr_oracle.ROW + 2048])
+            for k in range(3)]
+    args = [ctypes.c_void_p(a.ctypes.data) for a in (data, sine, rows[0], rows[1], rows[2])]
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        o.L.sdrc_accum(*args, 2048, 0, ctypes.c_void_p(res.ctypes.data))
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="channel-ms/s", cores=1, kind="port",
+                sample=f"{n} Accum calls of 2048 samples (scalar C restatement oracle/sdr_corr.c, "
+                       f"pinned to the reference primitives; includes ctypes call overhead), "
+                       f"{dt:.1f} s")
+
+
 SDR_MW_ROWS = {"medium": 4 * 31, "weak": 8 * 30}      # +-15 kHz (acquisition.cpp:324, :452)
 SDR_MW_PASSES = {"medium": 1, "weak": 15}
 # integer-op model per row pass (DESIGN.md): ten cmulsc'd 2048-sample rows (8 ops/sample),
@@ -1158,6 +1183,7 @@ def main():
                 for kind in sdr["mw"]:
                     out[f"sdr_acquisition_{kind}"]["cpu_baseline"] = \
                         cpu_baseline_sdr_mw(sdr["long"], kind)
+                out["sdr_tracking"]["cpu_baseline"] = cpu_baseline_sdr_accum()
                 cb = cpu_baseline_sdr_channel(sdr["ch_corr"])
                 if cb:
                     out["sdr_channel"]["cpu_baseline"] = cb
