@@ -869,6 +869,16 @@ def cpu_baseline_track(budget_s=6.0):
     return base
 
 
+def pmc_executed_flop(kernel):
+    """fp64 flops the kernel executes per launch (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes) from
+    the committed PMC pass over the config-2 section (profiles/pmc_fp64_mix.json), if any."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_fp64_mix.json")))
+        return d[kernel]["SQ_INSTS_VALU_FLOPS_FP64"] * 64
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def pmc_traffic(kernel, section=None):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any:
     the pass over that bench section alone ("section/kernel") when recorded,
@@ -936,6 +946,13 @@ def main():
                          "kernel_ms_per_launch": acq["corr_ms"],
                          "flop_per_launch": flop_launch},
             "ms_per_search": acq["dt"] / a.steps / R * 1e3,
+            # the prime-factor transform executes more fp64 flops than the radix-2 model
+            # counts: its executed rate against the same peak (PMC, committed pass)
+            "executed_fp64": (lambda f: None if f is None or R != ACQ_RECORDS else {
+                "flop_per_launch": f, "tflops": f / (acq["corr_ms"] * 1e-3) / 1e12,
+                "frac": f / (acq["corr_ms"] * 1e-3) / 1e12 / PEAK_FP64_TFLOPS,
+                "source": "profiles/pmc_fp64_mix.json (SQ_INSTS_VALU_FLOPS_FP64 x 64)"})(
+                    pmc_executed_flop(ACQ64_KERNEL)),
             "planted_found": f"{acq['found']}/{acq['n_planted']}",
             "ranks": rank_info,
         }
