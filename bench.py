@@ -276,6 +276,7 @@ def run_track_io(dist, dev, steps, warmup):
         d_res = gc.DevBuf(K * C1 * gc.TRACK_RESULT.itemsize, dev)
         ctx = gc.TrackCtx(C1, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS,
                           packed=packed)
+        ctx.set_layout(True)   # every channel has its own stream (no effect on packed ones)
         dt, kms, res = _replay_timed(dist, dev, ctx, d_if, stride, ctx.if_bytes(TRACK_NS),
                                      d_cmds, d_res, C1, steps, warmup)
         out["cs1_packed2" if packed else "cs1_int8"] = dict(

@@ -155,6 +155,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
     "gnsscorr_device_pci_bus_id", "gnsscorr_hip_runtime",
     "gnsscorr_track_create", "gnsscorr_track_destroy", "gnsscorr_track_max_dumps",
+    "gnsscorr_track_set_layout",
     "gnsscorr_pack2", "gnsscorr_track_if_bytes",
     "gnsscorr_track", "gnsscorr_track_dev", "gnsscorr_track_next_tic",
     "gnsscorr_track_replay_dev", "gnsscorr_track_get_state", "gnsscorr_track_set_state",
@@ -214,6 +215,7 @@ def lib() -> C.CDLL:
         "gnsscorr_hip_runtime": (I, [P, I, P]),
         "gnsscorr_track_create": (I, [C.POINTER(P), C.POINTER(TrackCfg)]),
         "gnsscorr_track_destroy": (I, [P]),
+        "gnsscorr_track_set_layout": (I, [P, I]),
         "gnsscorr_track_max_dumps": (I, [P]),
         "gnsscorr_track": (I, [P, P, I64, I, I64, P, P, P, C.POINTER(I)]),
         "gnsscorr_track_dev": (I, [P, P, I64, I64, P, P, P, I64]),
@@ -495,6 +497,11 @@ class TrackCtx:
         _check(lib().gnsscorr_track_create(C.byref(h), C.byref(cfg)), "gnsscorr_track_create")
         self.h = h
         self.max_dumps = lib().gnsscorr_track_max_dumps(h)
+
+    def set_layout(self, one_stream_per_channel: bool):
+        """gnsscorr_track_set_layout: per-channel LDS staging of int8 C_s = 1 streams."""
+        _check(lib().gnsscorr_track_set_layout(self.h, int(bool(one_stream_per_channel))),
+               "gnsscorr_track_set_layout")
 
     def close(self):
         if getattr(self, "h", None):

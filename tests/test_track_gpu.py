@@ -105,6 +105,35 @@ def test_batched_many_channels_vs_oracle(gpu, oracle, nsamp):
             np.testing.assert_array_equal(st[key][c], ref_state[c][key][0], err_msg=f"{key} ch{c}")
 
 
+@pytest.mark.parametrize("per_channel_layout", [False, True])
+def test_one_stream_per_channel_vs_oracle(gpu, oracle, per_channel_layout):
+    """C_s = 1 (every channel its own int8 stream), with and without the
+    gnsscorr_track_set_layout hint (per-channel LDS staging): bit-exact either way."""
+    rng = np.random.default_rng(31)
+    C, nsamp, n_calls = 48, 16368, 2
+    streams = [S.synth_if(nsamp * n_calls, 300 + i, [(i % 32 + 1, 37 * i, 0, 3)]) for i in range(C)]
+    cmds = _random_cmds(rng, n_calls, C, C)
+    for k in range(n_calls):
+        cmds[k]["stream"] = np.arange(C)
+    ref, ref_nd, ref_state = _oracle_channels(oracle, streams, nsamp, cmds)
+    ctx = gpu.TrackCtx(C, iq=True, max_nsamp=nsamp)
+    ctx.set_layout(per_channel_layout)
+    stride = ((nsamp * n_calls * 2 + 15) // 16) * 16 // 2
+    buf = np.zeros(stride * 2 * C, np.int8)
+    for i, st in enumerate(streams):
+        buf[i * stride * 2: i * stride * 2 + len(st)] = st
+    for k in range(n_calls):
+        res, _ = ctx.track(buf[k * nsamp * 2:], nsamp, cmds[k], n_streams=C, stream_stride=stride)
+        got_nd = (res["n_dumps"] > 0).astype(np.int32)
+        np.testing.assert_array_equal(got_nd, ref_nd[k])
+        m = got_nd == 1
+        np.testing.assert_array_equal(res["dump"][m], ref[k][m])
+    st = ctx.get_state()
+    for c in range(C):
+        for key in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+            np.testing.assert_array_equal(st[key][c], ref_state[c][key][0], err_msg=f"{key} ch{c}")
+
+
 def test_chunking_invariance_full_size(gpu):
     """One 16368-sample call == two 8184-sample calls (4096 channels)."""
     rng = np.random.default_rng(3)
