@@ -347,15 +347,16 @@ def run_track_io(dist, dev, steps, warmup):
     return out
 
 
-def run_sgt(dist, dev, steps, warmup):
+def run_sgt(dist, dev, steps, warmup, fs=SGT_FS):
     """BASELINE config 4: GLONASS L1OF 14 FDMA channels, tracking.sci float loop on the GPU.
-    Throughput: SGT_RX records x 14 FCH; latency: one 14-channel receiver."""
+    Throughput: SGT_RX records x 14 FCH; latency: one 14-channel receiver.  fs: the
+    Scilab receiver's 16 MHz (initSettings.sci) or config 4's 16.368 Msps."""
     K = steps + warmup + 2
-    ns = int(SGT_FS * K / 1000)
+    ns = int(fs * K / 1000)
     stride = 2 * ns
     d_if = gc.DevBuf(SGT_RX * stride, dev)
     d_if.fill_if2(0x5EED0004 + dist.rank)
-    ctx = gc.SgtCtx(1, device=dev, samplingFreq=SGT_FS)
+    ctx = gc.SgtCtx(1, device=dev, samplingFreq=fs)
     rng = np.random.default_rng(44 + dist.rank)
     fch = np.tile(np.arange(-7, 7), SGT_RX)
     C = len(fch)
@@ -378,7 +379,8 @@ def run_sgt(dist, dev, steps, warmup):
     dt = dist.max(t1 - t0)
     kern_ms = dist.max(e0.elapsed_ms(e1))
     ep = d_ep.download(gc.SGT_EPOCH, C * steps).reshape(C, steps)
-    ok = bool((ep["status"] == 0).all() and (np.abs(ep["blksize"] - 16000) < 20).all())
+    ok = bool((ep["status"] == 0).all() and
+              (np.abs(ep["blksize"] - round(fs / 1000)) < 20).all())
     # config 4 as stated: one 14-channel receiver, epochs back to back
     ch14 = ctx.init_chans(np.arange(-7, 7), rng.integers(1, 16000, 14),
                           1e6 + 0.5625e6 * np.arange(-7, 7))
@@ -391,7 +393,7 @@ def run_sgt(dist, dev, steps, warmup):
     e1.record(ctx.stream)
     ctx.sync()
     lat_ms = e0.elapsed_ms(e1) / steps
-    return dict(dt=dt, kern_ms=kern_ms, channels=C, steps=steps, ok=ok, lat_ms=lat_ms)
+    return dict(dt=dt, kern_ms=kern_ms, channels=C, steps=steps, ok=ok, lat_ms=lat_ms, fs=fs)
 
 
 def run_fullsky(dist, dev, steps, warmup):
@@ -870,6 +872,13 @@ def cpu_baseline_track(budget_s=6.0):
     return base
 
 
+def acq_alg_bytes(records):
+    """Algorithmic HBM bytes of one config-2 correlation launch: every code spectrum
+    (32 rows) and class spectrum (2 classes x 2 blocks per record) read once, fp64
+    complex (16 B per element), plus the per-(row, block) statistics written."""
+    return (N_PRN + 4 * records) * N * 16 + records * N_PRN * N_BINS * N_BLK * 48
+
+
 def pmc_executed_flop(kernel):
     """fp64 flops the kernel executes per config-2 record (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes
     / records per launch of that pass) from the committed PMC pass over the config-2 section
@@ -879,6 +888,24 @@ def pmc_executed_flop(kernel):
         return d[kernel]["SQ_INSTS_VALU_FLOPS_FP64"] * 64 / d["_records_per_launch"]
     except (OSError, ValueError, KeyError):
         return None
+
+
+def pmc_run_bytes(section):
+    """HBM bytes of one whole run of a bench section (every per-run kernel), from the
+    committed per-section rocprofv3 --pmc pass (tools/pmc_summary.py --runs), if any."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+        return d[f"{section}/_run"]["hbm_bytes_per_run"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def hbm_fields(traffic_bytes, seconds):
+    """rocprof HBM bytes (PMC) over the measured time, against the 8 TB/s peak."""
+    if traffic_bytes is None or not seconds:
+        return {"hbm_GBs": None, "hbm_frac": None}
+    gbs = traffic_bytes / seconds / 1e9
+    return {"hbm_GBs": gbs, "hbm_frac": gbs / PEAK_HBM_GBS}
 
 
 def pmc_traffic(kernel, section=None):
@@ -919,6 +946,7 @@ def main():
     trk = None if a.skip_track else run_track(dist, dev, max(a.steps, 20), a.warmup)
     tio = None if a.skip_track else run_track_io(dist, dev, max(a.steps, 20), a.warmup)
     sgt = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup)
+    sgt_c4 = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup, FS)
     sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps // 5, 5), 2)
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
     gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps // 5, 5), 2)
@@ -948,7 +976,10 @@ def main():
                          "frac": achieved / PEAK_FP64_TFLOPS,
                          "traffic": pmc_traffic(ACQ64_KERNEL, "acq"),
                          "kernel_ms_per_launch": acq["corr_ms"],
-                         "flop_per_launch": flop_launch},
+                         "flop_per_launch": flop_launch,
+                         # rocprof HBM bytes of this kernel per launch / its measured duration
+                         **hbm_fields(pmc_traffic(ACQ64_KERNEL, "acq"), acq["corr_ms"] * 1e-3),
+                         "hbm_algorithmic_bytes_per_launch": acq_alg_bytes(R)},
             "ms_per_search": acq["dt"] / a.steps / R * 1e3,
             "single_search": {"ms_per_search": acq1["dt"] / max(a.steps, 20) * 1e3,
                               "corr_kernel_ms": acq1["corr_ms"],
@@ -1054,16 +1085,16 @@ def main():
                 "mean_us": r["mean_us"], "p50_us": r["p50_us"], "p99_us": r["p99_us"],
                 "max_us": r["max_us"], "budget_us": r["budget_us"],
                 "realtime": r["p99_us"] < r["budget_us"]}
-        if sgt:
+        def sgt_line(sgt):
             C = sgt["channels"]
             k_s = sgt["kern_ms"] * 1e-3
-            dp = C * sgt["steps"] * SGT_FS / 1000 * SGT_DP_PER_SAMPLE
-            out["glonass_tracking"] = {
+            dp = C * sgt["steps"] * sgt["fs"] / 1000 * SGT_DP_PER_SAMPLE
+            return {
                 "metric": "1ms E/P/L correlations/sec (GLONASS L1OF float loop, tracking.sci)",
                 "value": C * sgt["steps"] * W / sgt["dt"], "unit": "channel-ms/s",
                 "steps": sgt["steps"], "channels_per_gpu": C,
                 "config": f"BASELINE config 4 scaled out: {SGT_RX} records x 14 FCH, 511-chip ST, "
-                          f"{SGT_FS / 1e6:g} Msps int8 IQ, fp64 NCOs + FLL/PLL/DLL on the GPU",
+                          f"{sgt['fs'] / 1e6:g} Msps int8 IQ, fp64 NCOs + FLL/PLL/DLL on the GPU",
                 "config4_ms_per_epoch_14ch": sgt["lat_ms"],
                 "config4_realtime_factor": 1.0 / sgt["lat_ms"],
                 "realtime_channels_per_gpu": C * sgt["steps"] / sgt["kern_ms"],
@@ -1071,12 +1102,17 @@ def main():
                              "achieved": dp / k_s / 1e12, "peak": PEAK_FP64_TFLOPS,
                              "unit": f"TFLOP/s (fp64, {SGT_DP_PER_SAMPLE} ops/sample model)",
                              "frac": dp / k_s / 1e12 / PEAK_FP64_TFLOPS,
-                             "hbm_algorithmic_GBs": C * sgt["steps"] * SGT_FS / 1000 * 2 / 14
+                             "hbm_algorithmic_GBs": C * sgt["steps"] * sgt["fs"] / 1000 * 2 / 14
                              / k_s / 1e9,
                              "traffic": pmc_traffic("sgt_track_kernel"),
                              "kernel_ms_per_launch": sgt["kern_ms"]},
                 "epochs_sane": sgt["ok"],
             }
+        if sgt:
+            out["glonass_tracking"] = sgt_line(sgt)
+            if sgt_c4:
+                # config 4 at the rate SURVEY 8(d) states (32.03 samples per ST chip)
+                out["glonass_tracking"]["at_16368ksps"] = sgt_line(sgt_c4)
         if sky:
             sky_ms = sky["dt"] / sky["steps"] * 1e3
             sky_flop = sky["cells"] * FLOP_PER_CELL_BLOCK       # cell-ms x flop per cell-block
@@ -1096,6 +1132,10 @@ def main():
                              "frac": sky_flop / (sky_ms * 1e-3) / 1e12 / W / PEAK_FP64_TFLOPS,
                              "timing": "whole search per step (forward spectra included): a "
                                        "lower bound on the correlation kernel's rate",
+                             # HBM bytes of one whole search (PMC, every per-search kernel)
+                             # over the search time
+                             **hbm_fields(None if pmc_run_bytes("fullsky") is None else
+                                          pmc_run_bytes("fullsky") / W, sky_ms * 1e-3),
                              "traffic": pmc_traffic("acq64_corr_kernel<Plan<16368, 16, 33, 31, "
                                                     "512, true>, 1, false>", "fullsky")},
             }
@@ -1117,7 +1157,10 @@ def main():
                              "frac": cells * N_BLK * FLOP_PER_CELL_BLOCK
                              / (gco["dt"] / gco["steps"]) / 1e12 / PEAK_FP64_TFLOPS,
                              "timing": "whole search per step (the 5-ms folding wipe-off and "
-                                       "forward spectra included)"},
+                                       "forward spectra included)",
+                             "traffic_per_search": pmc_run_bytes("glo_coherent"),
+                             **hbm_fields(pmc_run_bytes("glo_coherent"),
+                                          gco["dt"] / gco["steps"])},
             }
         if sdr:
             cells = SDR_REC * SDR_SV * SDR_ROWS * SDR_N

@@ -1660,7 +1660,8 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
   int rc = check_search(c, n_blocks, c->spec_freqs > 0 ? c->spec_freqs : 1, mode);
   if (rc) return rc;
   if (n_groups < 1 || n_bins < 1 || spc < 1 || spc > c->cfg.n_samples / 2 ||
-      n_blocks != c->spec_blocks) {
+      n_blocks != c->spec_blocks ||
+      (c->prec == GNSSCORR_ACQ_F64 && c->spec_recs != c->recs)) {
     gnsscorr_set_error("gnsscorr_acq_correlate: bad arguments (groups %d, bins %d, spc %d, "
                        "blocks %d vs spectra %d)", n_groups, n_bins, spc, n_blocks, c->spec_blocks);
     return GNSSCORR_EINVAL;
@@ -1873,6 +1874,7 @@ extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, i
     rc = search_launch(c, c->d_if, iq, n_blocks, GNSSCORR_ACQ_BEST_OF_BLOCKS, 1, c->d_freqs, 1,
                        1, c->d_gcode, c->d_gfreq, 16, c->d_rows, nullptr, c->d_dump, block);
   c->recs = recs;
+  c->spec_blocks = 0;   // its one-record spectra must not serve a later multi-record correlate
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(h_power, c->d_dump, sizeof(double) * c->cfg.n_samples,
                          hipMemcpyDeviceToHost, c->stream));

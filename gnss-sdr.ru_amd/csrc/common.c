@@ -14,7 +14,7 @@ void gnsscorr_set_error(const char *fmt, ...)
 }
 
 const char *gnsscorr_last_error(void) { return g_err; }
-const char *gnsscorr_version(void) { return "gnsscorr 0.1.0 (gfx950)"; }
+const char *gnsscorr_version(void) { return "gnsscorr 0.2.0 (gfx950)"; }
 
 /* GNSSCORR_IF_PACKED2 packing (gnsscorr.h): level 2c-3 -> code c, element e in
  * bits 2*(e%4) of byte e/4 (the GN3S LUT, gps_source.cpp:692, inverted). */

@@ -686,6 +686,7 @@ struct gnsscorr_track_ctx {
   int stage_if = 1;   // GNSSCORR_TRACK_STAGE_IF=0: lanes read their IF runs from global memory
   int cpw_override = 0;   // GNSSCORR_TRACK_CPW: channels per workgroup
   int stage_perch = 0;    // GNSSCORR_TRACK_STAGE_PERCH=1: channels on different streams stage their own
+  size_t lds_max = 0;     // LDS bytes a workgroup may allocate (gnsscorr_device_lds_bytes)
 };
 
 extern "C" int gnsscorr_track_iq(const gnsscorr_track_ctx* ctx) { return ctx && (ctx->cfg.iq & GNSSCORR_IF_IQ); }
@@ -722,6 +723,7 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   if (rc) return rc;
   auto* c = new gnsscorr_track_ctx();
   c->cfg = *cfg;
+  c->lds_max = (size_t)gnsscorr_device_lds_bytes(cfg->device);
   c->max_dumps = cfg->max_nsamp / GNSSCORR_OSG_ROW + 2;
   c->tic_ref = (int64_t)(cfg->samp_rate * cfg->tic_period);
   c->tic = c->tic_ref;
@@ -835,7 +837,8 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   // cpw 4 33.4 us, 3 35.2, 2 34.1, 1 46.4); GNSSCORR_TRACK_CPW overrides.
   int cpw = min(kMaxCpw, kMaxThreads / threads);
   if (c->cpw_override > 0) cpw = min(cpw, c->cpw_override);
-  if (stage == 2 && lds_bytes(cpw) + 1024 > 160 * 1024) stage = 1;   // per-channel slots must fit
+  // per-channel slots must fit beside the static LDS (s_lo, s_stream: < 1 KiB)
+  if (stage == 2 && lds_bytes(cpw) + 1024 > c->lds_max) stage = 1;
   dim3 grid((C + cpw - 1) / cpw), block(threads * cpw);
   const size_t dyn = lds_bytes(cpw);
 #define TRACK_LAUNCH(IQ, PK, ST)                                                               \
@@ -979,6 +982,16 @@ extern "C" int gnsscorr_track_sync(gnsscorr_track_ctx* c) {
 }
 
 extern "C" void* gnsscorr_track_stream(gnsscorr_track_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int gnsscorr_device_lds_bytes(int device) {
+  int blk = 0, cu = 0;
+  if (hipDeviceGetAttribute(&blk, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess)
+    blk = 0;
+  if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) !=
+      hipSuccess)
+    cu = 0;
+  return blk > cu ? blk : cu;
+}
 
 extern "C" int gnsscorr_device_count(void) {
   int n = 0;

@@ -153,7 +153,7 @@ class SdrAcqCfg(C.Structure):
 # every symbol include/gnsscorr.h + include/gnsscorr_osg.h declare
 EXPORTED_FUNCTIONS = [
     "gnsscorr_last_error", "gnsscorr_version", "gnsscorr_device_count",
-    "gnsscorr_device_pci_bus_id", "gnsscorr_hip_runtime",
+    "gnsscorr_device_pci_bus_id", "gnsscorr_hip_runtime", "gnsscorr_device_lds_bytes",
     "gnsscorr_track_create", "gnsscorr_track_destroy", "gnsscorr_track_max_dumps",
     "gnsscorr_track_set_layout",
     "gnsscorr_pack2", "gnsscorr_track_if_bytes",
@@ -212,6 +212,7 @@ def lib() -> C.CDLL:
         "gnsscorr_version": (C.c_char_p, []),
         "gnsscorr_device_count": (I, []),
         "gnsscorr_device_pci_bus_id": (I, [I, P, I]),
+        "gnsscorr_device_lds_bytes": (I, [I]),
         "gnsscorr_hip_runtime": (I, [P, I, P]),
         "gnsscorr_track_create": (I, [C.POINTER(P), C.POINTER(TrackCfg)]),
         "gnsscorr_track_destroy": (I, [P]),
@@ -344,6 +345,11 @@ def pack2(levels) -> np.ndarray:
 
 def device_count() -> int:
     return int(lib().gnsscorr_device_count())
+
+
+def device_lds_bytes(device: int = 0) -> int:
+    """LDS bytes a workgroup may allocate on the device (gnsscorr_device_lds_bytes)."""
+    return int(lib().gnsscorr_device_lds_bytes(device))
 
 
 def pci_bus_id(device: int = 0) -> str:

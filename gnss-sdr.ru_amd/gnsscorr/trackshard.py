@@ -63,6 +63,9 @@ class TrackShard:
         self.bps = 2 if iq else 1                          # bytes per sample
         self.stride = (nsamp + 15) // 16 * 16             # samples per stream (16-B aligned)
         self.device = device
+        self.ctx = None
+        if not self.mine:       # more ranks than channels: this rank contributes an empty part
+            return
         self.ctx = TrackCtx(len(self.mine), iq=iq, device=device, max_nsamp=nsamp,
                             samp_rate=samp_rate)
         self.d_if = DevBuf(max(1, len(self.streams)) * self.stride * self.bps, device)
@@ -72,6 +75,8 @@ class TrackShard:
     def load(self, if_streams: np.ndarray):
         """if_streams: (n_rx, nsamp * bytes-per-sample) int8, one call of every
         receiver's IF; copies (H2D) the streams this rank reads."""
+        if self.ctx is None:
+            return
         buf = np.zeros((len(self.streams), self.stride * self.bps), np.int8)
         for i, s in enumerate(self.streams):
             row = np.asarray(if_streams[s], np.int8)[:self.nsamp * self.bps]
@@ -80,11 +85,15 @@ class TrackShard:
 
     def step(self, cmds_global: np.ndarray):
         """One Sim_GP2021_int call for this rank's channels (asynchronous)."""
+        if self.ctx is None:
+            return
         self.d_cmds.upload(local_cmds(cmds_global, self.mine, self.lstream))
         self.ctx.track_dev(self.d_if.ptr, self.stride, self.nsamp, self.d_cmds.ptr,
                            self.d_res.ptr)
 
     def results(self):
         """(global channel ids, TRACK_RESULT rows) of the last step."""
+        if self.ctx is None:
+            return [], np.zeros(0, TRACK_RESULT)
         self.ctx.sync()
         return self.mine, self.d_res.download(TRACK_RESULT, len(self.mine))

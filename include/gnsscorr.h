@@ -39,6 +39,10 @@ const char *gnsscorr_version(void);
 /* Number of visible HIP devices (0 on a CPU-only host; never initialises
  * more than hipGetDeviceCount does). */
 int gnsscorr_device_count(void);
+/* LDS bytes one workgroup may allocate on a device (the larger of HIP's
+ * per-block and per-CU attributes: 160 KiB on gfx950); 0 if it cannot be read.
+ * Kernels that size their LDS at launch (per-channel IF staging) check it. */
+int gnsscorr_device_lds_bytes(int device);
 /* PCI bus id ("0000:xx:00.0") of a device, for run records. */
 int gnsscorr_device_pci_bus_id(int device, char *buf, int len);
 /* Path of the libamdhip64 whose hipMalloc this library calls, and

@@ -140,3 +140,25 @@ def test_track_plan_partition_and_merge_checks():
         merge([([0, 1], np.zeros(2, gc.TRACK_RESULT))], 3)
     with pytest.raises(ValueError):
         plan(2, 12, 2, 5)
+
+
+def test_track_shard_more_ranks_than_channels():
+    """world > n_rx * n_ch: the surplus ranks hold no channels, build no context and
+    contribute an empty part; the merge is still complete (no GPU touched)."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gnss-sdr.ru_amd"))
+    import gnsscorr as gc
+    from gnsscorr.trackshard import TrackShard, merge, plan
+    world = 5
+    parts = [plan(1, 3, world, r) for r in range(world)]
+    assert [len(p[0]) for p in parts] == [1, 1, 1, 0, 0]
+    idle = TrackShard(1, 3, 16368, rank=4, world=world)
+    assert idle.ctx is None
+    idle.load(np.zeros((1, 2 * 16368), np.int8))
+    idle.step(np.zeros(3, gc.NCO_CMD))
+    ids, res = idle.results()
+    assert ids == [] and len(res) == 0
+    full = [(p[0], np.zeros(len(p[0]), gc.TRACK_RESULT)) for p in parts]
+    assert len(merge(full, 3)) == 3

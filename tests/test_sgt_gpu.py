@@ -20,6 +20,10 @@ import sgt_oracle as S
 
 pytestmark = pytest.mark.gpu
 FS = 16e6
+# initSettings.sci's 16 MHz, and BASELINE config 4's 16.368 Msps:
+# 32.03 samples per ST chip, so ceil(remCode +- spc + k*step) crosses chip
+# boundaries at non-integer sample positions (tracking.sci:281-302)
+RATES = [16e6, 16.368e6]
 SUMS = ("I_E", "I_P", "I_L", "Q_E", "Q_P", "Q_L")
 
 
@@ -28,23 +32,24 @@ def _close(a, b, rtol=1e-6, atol=1e-6):
     return np.abs(a - b) <= rtol * np.abs(b) + atol
 
 
-def _glo_start(cp_chips):
-    return int(round((511 - cp_chips) / 0.511e6 * FS)) + 1
+def _glo_start(cp_chips, fs=FS):
+    return int(round((511 - cp_chips) / 0.511e6 * fs)) + 1
 
 
+@pytest.mark.parametrize("fs", RATES)
 @pytest.mark.parametrize("threads", [None, "64", "1024"])
 @pytest.mark.parametrize("system,file_type,switch", [(1, 2, 0), (1, 2, 1), (0, 2, 0), (1, 1, 0)])
-def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch, threads, monkeypatch):
+def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch, threads, fs, monkeypatch):
     """threads: launch shape override (GNSSCORR_SGT_THREADS; 64 = one wave per channel)."""
     gc = gpu
     if threads:
         monkeypatch.setenv("GNSSCORR_SGT_THREADS", threads)
     rng = np.random.default_rng(17 + system + 3 * file_type + 7 * switch)
     n = 200000
-    IF = gc.ifgen(n, [], fs=FS, iq=file_type == 2, seed=21)
+    IF = gc.ifgen(n, [], fs=fs, iq=file_type == 2, seed=21)
     d_if = gc.DevBuf.from_array(IF)
-    ctx = gc.SgtCtx(system, fileType=file_type, switchIQ=switch)
-    s = S.settings(system, fileType=file_type, switchIQ=switch)
+    ctx = gc.SgtCtx(system, fileType=file_type, switchIQ=switch, samplingFreq=fs)
+    s = S.settings(system, fileType=file_type, switchIQ=switch, samplingFreq=fs)
     C = 96
     ids = rng.integers(-7, 7, C) if system == 1 else rng.integers(1, 33, C)
     ch = np.zeros(C, gc.SGT_CHAN)
@@ -52,7 +57,7 @@ def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch, threads,
     ch["pos"] = rng.integers(0, n - 20000, C)
     basis = s["codeFreqBasis"]
     ch["code_freq"] = basis + rng.uniform(-40, 40, C)
-    step = ch["code_freq"] / FS
+    step = ch["code_freq"] / fs
     ch["rem_code"] = rng.uniform(0, 1, C) * step
     ch["rem_carr"] = rng.uniform(-6.2, 6.2, C)
     ch["carr_freq"] = rng.uniform(-3e6, 3e6, C)
@@ -76,29 +81,31 @@ def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch, threads,
     assert (ch["code_freq"] == ch0["code_freq"]).all()
 
 
-def _glonass_scene(gc, n_ms):
+def _glonass_scene(gc, n_ms, fs=FS):
     rng = np.random.default_rng(5)
     fchs = np.arange(-7, 7)
     cps = rng.uniform(0, 511, 14)
     dops = rng.uniform(-3000, 3000, 14)
     sigs = [dict(system=1, fch=int(k), code_phase=float(c), doppler=float(d), cn0=48.0,
                  data_bits=1) for k, c, d in zip(fchs, cps, dops)]
-    IF = gc.ifgen(int(FS * (n_ms + 3) / 1000), sigs, fs=FS, if_glo=1e6, seed=77)
+    IF = gc.ifgen(int(fs * (n_ms + 3) / 1000), sigs, fs=fs, if_glo=1e6, seed=77)
     acq = 1e6 + 0.5625e6 * fchs + dops + rng.uniform(-15, 15, 14)
-    starts = [_glo_start(c) for c in cps]
+    starts = [_glo_start(c, fs) for c in cps]
     return IF, fchs, starts, acq
 
 
-def test_config4_glonass_14_fch_closed_loop(gpu):
-    """BASELINE config 4: 14 FDMA channels, 511-chip ST code, fp64 loop on the GPU."""
+@pytest.mark.parametrize("fs", RATES)
+def test_config4_glonass_14_fch_closed_loop(gpu, fs):
+    """BASELINE config 4: 14 FDMA channels, 511-chip ST code, fp64 loop on the GPU
+    (at 16.368 Msps too, the rate SURVEY 8(d) states for config 4)."""
     gc = gpu
     n_ms = 150
-    IF, fchs, starts, acq = _glonass_scene(gc, n_ms)
+    IF, fchs, starts, acq = _glonass_scene(gc, n_ms, fs)
     d_if = gc.DevBuf.from_array(IF)
-    ctx = gc.SgtCtx(1)
+    ctx = gc.SgtCtx(1, samplingFreq=fs)
     ch = ctx.init_chans(fchs, starts, acq)
     ep = ctx.track(d_if.ptr, 0, len(IF) // 2, ch, n_ms, closed_loop=True)
-    s = S.settings(1)
+    s = S.settings(1, samplingFreq=fs)
     for i in range(14):
         r = S.track(IF, s, int(fchs[i]), starts[i], float(acq[i]), n_ms)
         assert (ep["status"][i] == 0).all()

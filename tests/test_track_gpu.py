@@ -194,3 +194,9 @@ def test_track_rejects_bad_prn(gpu):
     cm["prn"][2] = 40
     with pytest.raises(gpu.GnssCorrError):
         ctx.track(np.zeros(2048, np.int8), 1024, cm)
+
+
+def test_device_lds_bytes(gpu):
+    """The LDS a workgroup may allocate, as the per-channel staging fit check reads it
+    (gnsscorr_device_lds_bytes): 160 KiB on gfx950."""
+    assert gpu.device_lds_bytes(0) >= 160 * 1024

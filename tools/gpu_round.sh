@@ -4,7 +4,7 @@
 set -eu
 TAG=${1:-r1}
 O=gpurun_out/$TAG
-mkdir -p $O/pmc $O/pmc_acq $O/pmc_track $O/pmc_fullsky
+mkdir -p $O/pmc $O/pmc_acq $O/pmc_track $O/pmc_fullsky $O/pmc_glo_coherent
 export TMPDIR=/tmp
 echo "== pytest -m gpu"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
@@ -12,12 +12,17 @@ tail -3 $O/pytest.log
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 tail -1 $O/smoke.log
-echo "== bench"
-timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
-cat $O/bench.json
+echo "== bench (the driver's command, wall-timed)"
+s0=$(date +%s.%N)
+timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+s1=$(date +%s.%N)
+python3 -c "print('wall_s', round($s1-$s0, 1))" | tee $O/bench.wall
+cut -c1-400 $O/bench.json
 echo "== rocprofv3 kernel-trace stats"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
   python3 bench.py --no-cpu-baseline > $O/prof.log 2>&1
+python3 tools/trace_by_grid.py $O/prof acq64_corr_kernel $O/acq64_trace_by_grid.json \
+  "rocprofv3 --kernel-trace of python3 bench.py --no-cpu-baseline ($TAG)"
 echo "== pmc"
 B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
 i=0
@@ -30,12 +35,12 @@ for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
 done
 python tools/pmc_summary.py $O/pmc $O/pmc_summary.json --traffic $O/pmc_traffic.json
 # HBM bytes per launch of the kernels several sections share, one section at a time
-for S in acq track fullsky; do
+for S in acq track fullsky glo_coherent; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
       python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1
   done
-  python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S
+  python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S --runs 13
   echo "pmc section $S ok"
 done
 echo "== done"

@@ -1,12 +1,15 @@
 """Summarise rocprofv3 --pmc passes (tools/prof_pmc.sh) per kernel.
 
 usage: python tools/pmc_summary.py <pmc dir> <out json> [--traffic profiles/pmc_traffic.json]
-                                   [--section NAME]
+                                   [--section NAME [--runs R]]
 
 With --section the passes profiled ONE bench section alone (tools/bench_part.py
 NAME): its kernels are merged into the traffic file as "NAME/<kernel>", so
 sections sharing a kernel instantiation (the fp64 search of config 2, the
 GLONASS 5-ms search and the full-sky sweep) each get their own bytes per launch.
+With --runs R (the section's warmup + timed runs), "NAME/_run" also records the
+HBM bytes of one whole run of the section: the kernels launched at least R
+times (per-run kernels, not setup), bytes per launch x launches / R.
 
 Per kernel (name up to the first '('): the mean of every counter over its
 dispatches.  HBM bytes per launch follow MI355X_MICROARCH.md "HBM [CDNA4]":
@@ -61,7 +64,15 @@ def main():
             for k, m in s.items():
                 if "hbm_bytes_per_launch" in m:
                     keep[f"{sec}/{k}"] = {"hbm_bytes_per_launch": m["hbm_bytes_per_launch"],
+                                          "dispatches": m["dispatches"],
                                           "source": os.path.relpath(o), "instance": k}
+            if "--runs" in sys.argv:
+                runs = int(sys.argv[sys.argv.index("--runs") + 1])
+                per = [(k, m["hbm_bytes_per_launch"] * m["dispatches"] / runs) for k, m in s.items()
+                       if "hbm_bytes_per_launch" in m and m["dispatches"] >= runs]
+                keep[f"{sec}/_run"] = {"hbm_bytes_per_run": sum(b for _, b in per), "runs": runs,
+                                       "kernels": sorted(k for k, _ in per),
+                                       "source": os.path.relpath(o)}
             json.dump(keep, open(t, "w"), indent=1, sort_keys=True)
             s = {}
         for k, m in s.items():
