@@ -91,11 +91,14 @@ __device__ __forceinline__ void bfly(uint32_t& A, uint32_t& B, uint2 w, bool sca
   short2_t a = __builtin_bit_cast(short2_t, A), b = __builtin_bit_cast(short2_t, B);
   if (scale) { a = a >> (short)1; b = b >> (short)1; }
   // VOP3P v_dot2 with the rounding constant in an SGPR: the compiler's
-  // v_dot2c form needs a v_mov into the accumulator per product
+  // v_dot2c form needs a v_mov into the accumulator per product.  volatile:
+  // an inline asm has no implicit EXEC operand, and a non-volatile one may be
+  // sunk or hoisted across the exec-mask writes of divergent branches
+  // (track.hip's mad24 note); a volatile one stays where the source puts it.
   int32_t rnd, bi, bq;
-  asm("s_mov_b32 %0, 0x2000" : "=s"(rnd));
-  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(bi) : "v"(b), "v"(w.x), "s"(rnd));
-  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(bq) : "v"(b), "v"(w.y), "s"(rnd));
+  asm volatile("s_mov_b32 %0, 0x2000" : "=s"(rnd));
+  asm volatile("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(bi) : "v"(b), "v"(w.x), "s"(rnd));
+  asm volatile("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(bq) : "v"(b), "v"(w.y), "s"(rnd));
   bi >>= 14;
   bq >>= 14;
   const short2_t t = __builtin_bit_cast(short2_t, pack((int16_t)bi, (int16_t)bq));

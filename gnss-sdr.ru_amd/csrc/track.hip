@@ -181,14 +181,16 @@ __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
   return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
 }
 
-// |segment sum| <= 64 samples x 512 < 2^23 and bits are -1/0/+1: the 24-bit
-// multiply-add is exact (int32 wrap on the accumulator, as the reference).
-// Written as v_mad_i32_i24 directly: left alone, the compiler fuses the
-// 24-bit multiply and the add into a 64-bit v_mad_u64_u32.
+// |segment sum| < 2^23 and bits are -1/0/+1: the 24-bit multiply is exact
+// (int32 wrap on the accumulator, as the reference).  __mul24 (llvm.amdgcn.mul.i24)
+// + add is selected as v_mad_i32_i24; a plain `c + a * b` becomes a 64-bit
+// v_mad_u64_u32.  This used to be an inline-asm v_mad_i32_i24: an INLINEASM
+// carries no implicit EXEC operand, so machine passes were free to move it
+// across the exec-mask writes of divergent branches, where it then wrote
+// lanes of a reused register that the branch had masked off -- the cause of
+// the wrong sums DESIGN.md recorded for reordered IF loads in round 2.
 __device__ __forceinline__ uint32_t mad24(int a, int b, uint32_t c) {
-  uint32_t d;
-  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
+  return c + (uint32_t)__mul24(a, b);
 }
 __device__ __forceinline__ void seg_flush(int si, int sq, int lb, int pb, int eb, Acc& cur) {
   cur.a[0] = mad24(lb, si, cur.a[0]);
@@ -281,10 +283,408 @@ __device__ __forceinline__ void corr_pair(uint32_t x, uint32_t& p0, uint32_t& kp
   }
 }
 
+// Epoch-segmented reduction of the per-thread sums and the per-channel epilogue
+// (one thread per channel): dumps, ms/bit counters, TIC latch, carrier cycles and
+// the new channel state (correlator.c:243-316).  Every thread of the workgroup
+// calls it (it holds a barrier).
+__device__ __forceinline__ void finish_call(const Chan& c, const gnsscorr_nco_cmd& cmd,
+                                            gnsscorr_chan_state st, int chn, bool have,
+                                            bool active, int tid, bool runs, int e0,
+                                            bool switched, const Acc& first, const Acc& cur,
+                                            int32_t* s_sum, uint32_t ndump, uint64_t Rtot,
+                                            int nsamp, int64_t tic_count,
+                                            gnsscorr_track_result* __restrict__ res,
+                                            gnsscorr_chan_state* __restrict__ state,
+                                            int32_t* __restrict__ all_dumps, int max_dumps) {
+  // ---- epoch-segmented reduction ------------------------------------------
+  // thread contributes (e0, switched ? first : cur) and (e0+1, cur) if switched
+  // (a wave never spans two thread groups: T is a multiple of 64)
+  const int e_hi_mine = e0 + (switched ? 1 : 0);
+  const int e_lo = wave_min(runs ? e0 : 0x7fffffff);
+  const int e_hi = wave_max(runs ? e_hi_mine : -1);
+  const int lane = threadIdx.x & 63;
+  for (int e = e_lo; e <= e_hi; e++) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      uint32_t v = 0;
+      if (e == e0) v += switched ? first.a[k] : cur.a[k];
+      if (switched && e == e0 + 1) v += cur.a[k];
+      const int s = wave_sum((int)v);
+      if (lane == 0) atomicAdd(&s_sum[e * 6 + k], s);
+    }
+  }
+  __syncthreads();
+  TRACK_PSTAMP(4);
+
+  // ---- per-channel epilogue (one thread per channel) ------------------------
+  if (tid != 0 || !have) return;
+  if (!active) {   // idle channel: only the epoch load (correlator.c:177-185)
+    gnsscorr_track_result r;
+    memset(&r, 0, sizeof r);
+    r.n_dumps = cmd.prn > 32 ? -1 : 0;
+    r.msbit_reg = st.msbit_reg;
+    res[chn] = r;
+    state[chn] = st;
+    return;
+  }
+  gnsscorr_track_result r;
+  memset(&r, 0, sizeof r);
+  r.n_dumps = (int)ndump;
+  int ms = st.ms_counter, bit = st.bit_counter, msbit = st.msbit_reg;
+
+  const bool tic_here = tic_count >= 0 && tic_count < nsamp;
+  uint32_t nd_tic = 0;
+  uint64_t Rt = 0;
+  if (tic_here) {
+    Rt = ((uint64_t)c.K0 + (uint64_t)(tic_count + 1) * c.kinc2) >> 32;
+    nd_tic = n_dumps_after(c, Rt);
+  }
+  int msbit_at_tic = msbit;
+  for (uint32_t d = 0; d < ndump; d++) {
+    uint32_t v[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++)
+      v[k] = (uint32_t)s_sum[d * 6 + k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
+    if (all_dumps && (int)d < max_dumps)
+      for (int k = 0; k < 6; k++) all_dumps[((int64_t)chn * max_dumps + d) * 6 + k] = (int32_t)v[k];
+    if (d + 1 == ndump)
+      for (int k = 0; k < 6; k++) r.dump[k] = (int32_t)v[k];
+    msbit_step(ms, bit);
+    msbit = ms + (bit << 8);
+    if (d + 1 == nd_tic) msbit_at_tic = msbit;
+  }
+  uint32_t nacc[6];
+  for (int k = 0; k < 6; k++)
+    nacc[k] = (uint32_t)s_sum[ndump * 6 + k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
+
+  const uint64_t Wtot = ((uint64_t)c.P0 + (uint64_t)nsamp * c.cinc) >> 32;
+  uint32_t cycle_end;
+  if (tic_here) {  // TIC latch after sample tic_count (correlator.c:286-303)
+    const uint64_t t1 = (uint64_t)tic_count + 1;
+    const uint64_t Wt = ((uint64_t)c.P0 + t1 * c.cinc) >> 32;
+    const uint32_t cyc = st.carrier_cycle + (uint32_t)Wt;
+    uint32_t hct, ldt, ept;
+    hc_after(c, Rt, hct, ldt, ept);
+    r.tic = 1;
+    r.tic_regs[0] = (int32_t)hct;
+    r.tic_regs[1] = (int32_t)(cyc & 0xffffu);
+    r.tic_regs[2] = (int32_t)((c.P0 + (uint32_t)t1 * c.cinc) >> 22);
+    r.tic_regs[3] = msbit_at_tic;
+    r.tic_regs[4] = (int32_t)((uint32_t)((uint64_t)c.K0 + t1 * c.kinc2) >> 22);
+    r.tic_regs[5] = (int32_t)(cyc >> 16);
+    cycle_end = (uint32_t)(Wtot - Wt);
+  } else {
+    cycle_end = st.carrier_cycle + (uint32_t)Wtot;
+  }
+  uint32_t hce, lde, epe;
+  hc_after(c, Rtot, hce, lde, epe);
+
+  r.msbit_reg = msbit;
+  res[chn] = r;
+
+  st.carrier_phase = c.P0 + (uint32_t)nsamp * c.cinc;
+  st.carrier_cycle = cycle_end;
+  st.code_phase = (uint32_t)((uint64_t)c.K0 + (uint64_t)nsamp * c.kinc2);
+  st.half_chip = hce;
+  for (int k = 0; k < 6; k++) st.acc[k] = (int32_t)nacc[k];
+  st.ms_counter = ms;
+  st.bit_counter = bit;
+  st.msbit_reg = msbit;
+  state[chn] = st;
+  TRACK_PSTAMP(5);
+}
+
 __device__ __forceinline__ int xcd_channel(int b, int G) {
   const int q = G >> 3, r = G & 7, x = b & 7, slot = b >> 3;
   return x * q + (x < r ? x : r) + slot;
 }
+
+// ============================================================================
+// osg_track2_kernel: branch-free segment sums for interleaved I,Q streams
+// (int8 or 2-bit packed).
+//
+// Why: in osg_track_kernel every lane walks its own 64-sample run and takes a
+// code-carry branch about once per 8 samples, at a different sample in every
+// lane, so a wave executes the carry path (segment flush, bit reload, epoch
+// switch) at nearly every sample pair: ~18 VALU + ~12 SALU instructions per
+// sample (PMC, round 2).  Here a lane's samples are cut into intervals of
+// three pairs (6 samples).  When a half-chip lasts at least 6 samples (kinc2 <=
+// 2^32 / 6, any fs >= 12.3 Msps) an interval holds at most one code carry, so
+// every pair is split branch-free into the part before the carry ("pre", LO
+// word masked by the carry position) and the whole pair ("tot"); at the end of
+// each interval -- the same instruction for every lane -- the pre sums are
+// flushed with the current E/P/L bits (correlator.c:213-241), the remainder
+// carries over into the next segment and the bits are reloaded once
+// (correlator.c:243-251).  The rare dump (epoch switch, correlator.c:251-281)
+// is the only branch.
+//
+// Sample -> lane map: wave w of a channel covers samples [4096 w, 4096 w + 4096)
+// as two pieces of 2048; lane l takes samples [2048 p + 32 l, +32) of piece p.
+// A piece is 64 lanes x 32 samples of CONTIGUOUS IF, so each wave load reads
+// 1 KiB of consecutive bytes: int8 pieces (4 KiB) are staged through a
+// wave-private LDS slot (no workgroup barrier), packed pieces (16 B per lane)
+// are loaded straight into registers and expanded with v_perm.  No IF is
+// shared between channels, so the receiver layout (12 channels per stream)
+// and one stream per channel run the same code with the same LDS footprint.
+//
+// Channels outside the fast path's conditions (kinc2 > 2^32/6, a half-chip
+// range beyond the staged E/P/L row, no dump possible) run the per-sample
+// reference recurrence (corr_sample) on the same staged words, wave-uniformly.
+// ============================================================================
+constexpr int kPieceLen = 32;                    // samples per lane per piece
+constexpr int kPieceSpan = 64 * kPieceLen;       // samples per wave per piece
+constexpr int kWaveSpan = 2 * kPieceSpan;        // samples per wave
+constexpr int kStage2Bytes = kPieceSpan * 2;     // int8 IQ bytes of one staged piece (4 KiB)
+constexpr uint32_t kFastKinc2 = 0xFFFFFFFFu / 6u;   // >= 6 samples per half-chip
+
+// hc_after without a 32-bit division (m < 2^24: fp32 reciprocal + one fix-up)
+__device__ __forceinline__ void hc_after_fast(const Chan& c, uint64_t r, float invD, uint32_t& hc,
+                                              uint32_t& ld, uint32_t& epoch) {
+  if (r < c.j1) {
+    epoch = 0;
+    hc = (uint32_t)((c.hc0 + r) & 0xFFFFu);
+    ld = hc;
+  } else {
+    const uint32_t m = (uint32_t)(r - c.j1);
+    uint32_t e = (uint32_t)((float)m * invD);
+    int q = (int)(m - e * c.D);
+    if (q < 0) { q += (int)c.D; e--; }
+    if (q >= (int)c.D) { q -= (int)c.D; e++; }
+    epoch = 1 + e;
+    hc = (uint32_t)q;
+    ld = q ? (uint32_t)q : (m == 0 ? (uint32_t)((c.hc0 + c.j1) & 0xFFFFu) : c.D);
+  }
+}
+
+// Lane state through its pieces.
+struct Seg {
+  uint32_t p0, kph, hc, ld;
+  int lb, pb, eb;
+  int ti, tq, pi, pq;          // interval sums: whole pairs / part before the carry
+  bool carried;               // a code carry in the current interval
+};
+
+// one pair of samples (IF word x) in the branch-free interval form; ONE: the
+// word holds a single (last) sample, so no carry after a second one
+template <bool ONE>
+__device__ __forceinline__ void pair2(uint32_t x, const Chan& c, Seg& g, const uint2* __restrict__ lo2) {
+  const uint32_t p1 = g.p0 + c.cinc;
+  const uint2 lo = lo2[(g.p0 >> 29) | ((p1 >> 26) & 0x38u)];
+  g.p0 = p1 + c.cinc;
+  const uint32_t k0 = g.kph + c.kinc2;
+  const bool c0 = k0 < g.kph;
+  uint32_t k1 = k0;
+  bool c1 = false;
+  if (!ONE) {
+    k1 = k0 + c.kinc2;
+    c1 = k1 < k0;
+  }
+  g.kph = k1;
+  uint32_t m = c0 ? 0xFFFFu : 0xFFFFFFFFu;   // carry after sample a: only a is "pre"
+  m = g.carried ? 0u : m;                    // after this interval's carry: nothing is
+  g.carried = g.carried | c0 | c1;
+  const uint32_t xm = x & m;
+  g.ti = dot4(x, lo.x, g.ti);
+  g.tq = dot4(x, lo.y, g.tq);
+  g.pi = dot4(xm, lo.x, g.pi);
+  g.pq = dot4(xm, lo.y, g.pq);
+}
+
+// end of an interval: flush the part before the carry with the current bits,
+// carry the rest into the next segment, step the half-chip (correlator.c:243-283)
+__device__ __forceinline__ void interval_end(const Chan& c, Seg& g, Acc& cur, Acc& first,
+                                             bool& switched, const uint8_t* __restrict__ row) {
+  seg_flush(g.pi, g.pq, g.lb, g.pb, g.eb, cur);
+  const int ri = g.ti - g.pi, rq = g.tq - g.pq;
+  g.ti = g.pi = ri;
+  g.tq = g.pq = rq;
+  const bool cy = g.carried;               // branch-free: one carry at most
+  g.hc += cy ? 1u : 0u;
+  g.ld = cy ? g.hc : g.ld;
+  g.carried = false;
+  // (a half-chip count already >= D -- slew lowered between calls -- dumps at
+  // the next carry, not before: the reference tests only after a step)
+  if (cy && g.hc >= c.D) {   // dump (correlator.c:251-281): rare, one lane per channel
+    // snapshot of the epoch's sums; cur keeps running over both epochs and the
+    // lane's share of the next epoch is cur - first (osg_track2_kernel's end)
+#pragma unroll
+    for (int k = 0; k < 6; k++) first.a[k] = cur.a[k];
+    switched = true;
+    g.hc = 0;          // the bits of half-chip 0 come from the pre-reset index ld
+  }
+  unpack8(row[g.ld], g.lb, g.pb, g.eb);
+}
+
+// The per-wave piece path (see the osg_track2 notes above): every lane's two
+// 32-sample pieces in the branch-free interval form (fast) or by the per-sample
+// recurrence; sums as (old epoch, new epoch) in (first, cur) when switched.
+// s_wave: this wave's 4 KiB LDS slot (int8 streams).
+template <bool PK>
+__device__ __forceinline__ void run_pieces(const int8_t* __restrict__ ifbuf, int64_t stream_stride,
+                                           int nsamp, int tid, const Chan& c, int stream,
+                                           bool active, bool fast, const uint8_t* s_pk8,
+                                           const uint2* s_lo, uint4* s_wave,
+                                           const uint32_t* __restrict__ pk, Acc& cur, Acc& first,
+                                           bool& switched, int& e0, bool& runs) {
+  const float invD = 1.0f / (float)c.D;
+  const int lane = (int)threadIdx.x & 63;
+  const int wbase = (tid >> 6) * kWaveSpan;               // first sample of this wave
+  runs = active && wbase + lane * kPieceLen < nsamp;
+  // element offset of the channel's stream
+  const int64_t e_stream = (int64_t)stream * stream_stride * 2;
+  Seg g;
+
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const int n_piece = wbase + p * kPieceSpan;            // first sample of the wave's piece
+    if (!active || n_piece >= nsamp) break;                // wave-uniform
+    const int n0 = n_piece + lane * kPieceLen;             // this lane's first sample
+    const int L = max(0, min(kPieceLen, nsamp - n0));      // this lane's valid samples
+    // ---- IF of the lane's piece: 16 sample-pair words in 4 chunks of 4
+    uint32_t pw[4] = {0u, 0u, 0u, 0u};   // packed: one 32-bit word (4 pairs) per chunk
+    if constexpr (PK) {
+      // 16 B per lane (8-byte aligned streams): two 8-byte loads of whole bytes
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(ifbuf) + ((e_stream + 2 * (int64_t)n0) >> 2);
+      if (L == kPieceLen) {
+        const uint2 u0 = reinterpret_cast<const uint2*>(b)[0];
+        const uint2 u1 = reinterpret_cast<const uint2*>(b)[1];
+        pw[0] = u0.x; pw[1] = u0.y; pw[2] = u1.x; pw[3] = u1.y;
+      } else {
+        for (int k = 0; 2 * k < L; k++) pw[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
+      }
+    } else {
+      // int8: the wave's 4 KiB piece through its LDS slot.  Chunk i (16 B) of the
+      // piece belongs to lane i >> 2; it is stored at lane * 64 + 16 * ((i ^ (lane >> 2)) & 3)
+      // so that the 16-byte reads of 16 consecutive lanes hit 64 distinct banks.
+      const int8_t* g8 = ifbuf + e_stream + 2 * (int64_t)n_piece;
+      const int valid = max(0, min(kPieceSpan, nsamp - n_piece));   // samples of the piece in the call
+      const int full_chunks = valid / 8;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = r * 64 + lane;
+        const int ow = i >> 2, sub = i & 3;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (i < full_chunks) {
+          v = reinterpret_cast<const uint4*>(g8)[i];
+        } else if (i * 8 < valid) {   // the partial chunk: whole words, then the odd sample
+          const int rem = valid - i * 8;   // 1..7 samples
+          const uint32_t* g32 = reinterpret_cast<const uint32_t*>(g8) + 4 * i;
+          uint32_t t[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int k = 0; k < 3; k++)
+            if (k < rem / 2) t[k] = g32[k];
+          const uint32_t odd = (rem & 1) ? (uint32_t)reinterpret_cast<const uint16_t*>(g32)[rem - 1] : 0u;
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (k == rem / 2) t[k] = odd;
+          v = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+        s_wave[ow * 4 + ((sub ^ (ow >> 2)) & 3)] = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // chunk j of the lane's piece as four pair words
+    auto chunk = [&](int j) -> uint4 {
+      if constexpr (PK) return if2_expand_word(pw[j]);
+      else return s_wave[lane * 4 + ((j ^ (lane >> 2)) & 3)];
+    };
+    if (L > 0) {
+      // ---- lane state at its first sample
+      const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
+      const uint64_t r0 = X >> 32;
+      g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
+      g.kph = (uint32_t)X;
+      if (fast) {
+        // closed form at the piece start; a dump between the lane's two pieces
+        // shows as a later epoch (at most one dump per lane: D >= 2046 half-chips)
+        uint32_t ep;
+        hc_after_fast(c, r0, invD, g.hc, g.ld, ep);
+        if (p == 0) {
+          e0 = (int)ep;
+        } else if ((int)ep > e0 + (switched ? 1 : 0)) {
+#pragma unroll
+          for (int k = 0; k < 6; k++) first.a[k] = cur.a[k];   // snapshot (see interval_end)
+          switched = true;
+        }
+        unpack8(s_pk8[g.ld], g.lb, g.pb, g.eb);
+        g.ti = g.tq = g.pi = g.pq = 0;
+        g.carried = false;
+        if (L == kPieceLen) {   // every lane but the last of a call
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint4 u = chunk(j);
+            const uint32_t words[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const int k = 4 * j + i;
+              pair2<false>(words[i], c, g, s_lo);
+              if (k % 3 == 2 || k == kPieceLen / 2 - 1) interval_end(c, g, cur, first, switched, s_pk8);
+            }
+          }
+        } else {
+          const int np = L >> 1;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint4 u = chunk(j);
+            const uint32_t words[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const int k = 4 * j + i;
+              if (k < np) pair2<false>(words[i], c, g, s_lo);
+              else if (k == np && (L & 1)) pair2<true>(words[i] & 0xFFFFu, c, g, s_lo);
+              if (k % 3 == 2 || k == kPieceLen / 2 - 1) interval_end(c, g, cur, first, switched, s_pk8);
+            }
+          }
+        }
+        // the samples after the piece's last carry: the open segment, with the
+        // bits in force after it
+        seg_flush(g.ti, g.tq, g.lb, g.pb, g.eb, cur);
+      } else {
+        // per-sample reference recurrence (correlator.c:200-283), table from global memory
+        uint32_t hc, ld, ep;
+        hc_after(c, r0, hc, ld, ep);
+        if (p == 0) {
+          e0 = (int)ep;
+        } else if ((int)ep > e0 + (switched ? 1 : 0)) {
+#pragma unroll
+          for (int k = 0; k < 6; k++) first.a[k] = cur.a[k];   // snapshot
+          switched = true;
+        }
+        const uint32_t tw = pk[c.base + (int)ld];
+        int lb = (int)(int8_t)(tw & 0xFFu), pb = (int)(int8_t)((tw >> 8) & 0xFFu),
+            eb = (int)(int8_t)((tw >> 16) & 0xFFu);
+        // corr_sample keeps (first, cur) as (old epoch, new epoch); the kernel
+        // keeps (snapshot, running total): convert around the call
+        if (switched)
+#pragma unroll
+          for (int k = 0; k < 6; k++) cur.a[k] -= first.a[k];
+        uint32_t phase = g.p0, kph = g.kph;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint4 u = chunk(j);
+          const uint32_t words[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int k = 4 * j + i;
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+              if (2 * k + h < L)
+                corr_sample<true>(sbyte((int)words[i], 2 * h), sbyte((int)words[i], 2 * h + 1), phase,
+                                  kph, c, hc, lb, pb, eb, cur, first, switched, pk);
+          }
+        }
+        if (switched)
+#pragma unroll
+          for (int k = 0; k < 6; k++) cur.a[k] += first.a[k];
+      }
+    }
+    if constexpr (!PK) __builtin_amdgcn_wave_barrier();   // the slot is refilled by the next piece
+  }
+  if (switched)   // (snapshot, running total) -> (old epoch, new epoch) for finish_call
+#pragma unroll
+    for (int k = 0; k < 6; k++) cur.a[k] -= first.a[k];
+}
+
 
 // One workgroup = cpw channels (cpw = 1024 / threads-per-channel, at most
 // kMaxCpw) x one call; thread group q = threadIdx.x / T runs channel
@@ -387,20 +787,21 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
       else if (v != sst) uni = false;
     }
   }
-  // stage_ok: 0 no staging; 1 a stream shared by the whole workgroup is
-  // staged once; 2 otherwise each channel stages its own stream in its own slot
+  // stage_ok: 0 no staging (lanes read their runs from global memory); 1 a
+  // stream shared by the whole workgroup is staged once in LDS and read by its
+  // cpw channels; channels of a workgroup on different streams (one stream
+  // per channel, receivers split over workgroups) take the per-wave piece
+  // path (run_pieces: coalesced 1 KiB wave loads, no workgroup barrier)
   const bool shared_stage = IQ && stage_ok && uni && sst >= 0;
-  const bool perch_stage = IQ && stage_ok == 2 && !shared_stage;
-  const bool stage = shared_stage || perch_stage;
-  const int slot_chunks = ((nsamp + kRun - 1) / kRun) * kPitch;
-  uint4* s_ifq = s_if + (perch_stage ? q * slot_chunks : 0);
+  const bool pieces = IQ && stage_ok == 1 && !shared_stage;   // 3: A/B, round-2 lane reads
+  const bool stage = shared_stage;
+  uint4* s_ifq = s_if;
   if (stage) {
     const int n_full = nsamp / kRun;
-    const int st_id = shared_stage ? sst : s_stream[q];
-    const int lt = shared_stage ? (int)threadIdx.x : tid;       // staging lane and width
-    const int nt = shared_stage ? (int)blockDim.x : T;
+    const int st_id = sst;
+    const int lt = (int)threadIdx.x;       // staging lane and width
+    const int nt = (int)blockDim.x;
     uint32_t* t32 = reinterpret_cast<uint32_t*>(s_ifq + n_full * kPitch);
-    if (st_id >= 0) {
     if constexpr (!PK) {
       // full 64-sample runs only; consecutive threads load consecutive 16-byte chunks
       const int4* g = reinterpret_cast<const int4*>(ifbuf + (int64_t)st_id * stream_stride * 2);
@@ -430,19 +831,26 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
       for (int wi = lt; wi < (nsamp - n_full * kRun) / 2; wi += nt)
         t32[wi] = if2_expand_byte(gb[n_full * (kRun / 2) + wi]);
     }
-    }
     __syncthreads();
   }
   TRACK_PSTAMP(2);
 
-  // ---- per-thread run of kRun samples --------------------------------------
   Acc cur, first;
 #pragma unroll
   for (int k = 0; k < 6; k++) { cur.a[k] = 0; first.a[k] = 0; }
   bool switched = false;
   int e0 = 0;
+  bool runs = false;
+  if (pieces) {
+    // the fast (branch-free) form needs the row in LDS and >= 6 samples per half-chip
+    const bool fast = pk_lds && c.kinc2 <= kFastKinc2;
+    const int wave = (int)threadIdx.x >> 6;
+    run_pieces<PK>(ifbuf, stream_stride, nsamp, tid, c, cmd.stream, active, fast, s_pk8, s_lo,
+                   s_if + wave * (kStage2Bytes / 16), pk, cur, first, switched, e0, runs);
+  } else {
+  // ---- per-thread run of kRun samples --------------------------------------
   const int n0 = tid * kRun;
-  const bool runs = active && n0 < nsamp;
+  runs = active && n0 < nsamp;
   if (runs) {
     const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
     uint32_t kph = (uint32_t)X;
@@ -566,104 +974,12 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
     }
   }
 
+  }   // per-thread runs
   TRACK_PSTAMP(3);
-  // ---- epoch-segmented reduction ------------------------------------------
-  // thread contributes (e0, switched ? first : cur) and (e0+1, cur) if switched
-  // (a wave never spans two thread groups: T is a multiple of 64)
-  const int e_hi_mine = e0 + (switched ? 1 : 0);
-  const int e_lo = wave_min(runs ? e0 : 0x7fffffff);
-  const int e_hi = wave_max(runs ? e_hi_mine : -1);
-  const int lane = threadIdx.x & 63;
-  for (int e = e_lo; e <= e_hi; e++) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      uint32_t v = 0;
-      if (e == e0) v += switched ? first.a[k] : cur.a[k];
-      if (switched && e == e0 + 1) v += cur.a[k];
-      const int s = wave_sum((int)v);
-      if (lane == 0) atomicAdd(&s_sum[e * 6 + k], s);
-    }
-  }
-  __syncthreads();
-  TRACK_PSTAMP(4);
-
-  // ---- per-channel epilogue (one thread per channel) ------------------------
-  if (tid != 0 || !have) return;
-  if (!active) {   // idle channel: only the epoch load (correlator.c:177-185)
-    gnsscorr_track_result r;
-    memset(&r, 0, sizeof r);
-    r.n_dumps = cmd.prn > 32 ? -1 : 0;
-    r.msbit_reg = st.msbit_reg;
-    res[chn] = r;
-    state[chn] = st;
-    return;
-  }
-  gnsscorr_track_result r;
-  memset(&r, 0, sizeof r);
-  r.n_dumps = (int)ndump;
-  int ms = st.ms_counter, bit = st.bit_counter, msbit = st.msbit_reg;
-
-  const bool tic_here = tic_count >= 0 && tic_count < nsamp;
-  uint32_t nd_tic = 0;
-  uint64_t Rt = 0;
-  if (tic_here) {
-    Rt = ((uint64_t)c.K0 + (uint64_t)(tic_count + 1) * c.kinc2) >> 32;
-    nd_tic = n_dumps_after(c, Rt);
-  }
-  int msbit_at_tic = msbit;
-  for (uint32_t d = 0; d < ndump; d++) {
-    uint32_t v[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++)
-      v[k] = (uint32_t)s_sum[d * 6 + k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
-    if (all_dumps && (int)d < max_dumps)
-      for (int k = 0; k < 6; k++) all_dumps[((int64_t)chn * max_dumps + d) * 6 + k] = (int32_t)v[k];
-    if (d + 1 == ndump)
-      for (int k = 0; k < 6; k++) r.dump[k] = (int32_t)v[k];
-    msbit_step(ms, bit);
-    msbit = ms + (bit << 8);
-    if (d + 1 == nd_tic) msbit_at_tic = msbit;
-  }
-  uint32_t nacc[6];
-  for (int k = 0; k < 6; k++)
-    nacc[k] = (uint32_t)s_sum[ndump * 6 + k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
-
-  const uint64_t Wtot = ((uint64_t)c.P0 + (uint64_t)nsamp * c.cinc) >> 32;
-  uint32_t cycle_end;
-  if (tic_here) {  // TIC latch after sample tic_count (correlator.c:286-303)
-    const uint64_t t1 = (uint64_t)tic_count + 1;
-    const uint64_t Wt = ((uint64_t)c.P0 + t1 * c.cinc) >> 32;
-    const uint32_t cyc = st.carrier_cycle + (uint32_t)Wt;
-    uint32_t hct, ldt, ept;
-    hc_after(c, Rt, hct, ldt, ept);
-    r.tic = 1;
-    r.tic_regs[0] = (int32_t)hct;
-    r.tic_regs[1] = (int32_t)(cyc & 0xffffu);
-    r.tic_regs[2] = (int32_t)((c.P0 + (uint32_t)t1 * c.cinc) >> 22);
-    r.tic_regs[3] = msbit_at_tic;
-    r.tic_regs[4] = (int32_t)((uint32_t)((uint64_t)c.K0 + t1 * c.kinc2) >> 22);
-    r.tic_regs[5] = (int32_t)(cyc >> 16);
-    cycle_end = (uint32_t)(Wtot - Wt);
-  } else {
-    cycle_end = st.carrier_cycle + (uint32_t)Wtot;
-  }
-  uint32_t hce, lde, epe;
-  hc_after(c, Rtot, hce, lde, epe);
-
-  r.msbit_reg = msbit;
-  res[chn] = r;
-
-  st.carrier_phase = c.P0 + (uint32_t)nsamp * c.cinc;
-  st.carrier_cycle = cycle_end;
-  st.code_phase = (uint32_t)((uint64_t)c.K0 + (uint64_t)nsamp * c.kinc2);
-  st.half_chip = hce;
-  for (int k = 0; k < 6; k++) st.acc[k] = (int32_t)nacc[k];
-  st.ms_counter = ms;
-  st.bit_counter = bit;
-  st.msbit_reg = msbit;
-  state[chn] = st;
-  TRACK_PSTAMP(5);
+  finish_call(c, cmd, st, chn, have, active, tid, runs, e0, switched, first, cur, s_sum, ndump, Rtot,
+              nsamp, tic_count, res, state, all_dumps, max_dumps);
 }
+
 
 }  // namespace
 
@@ -685,7 +1001,8 @@ struct gnsscorr_track_ctx {
   int64_t tic = 0, tic_ref = 0;
   int stage_if = 1;   // GNSSCORR_TRACK_STAGE_IF=0: lanes read their IF runs from global memory
   int cpw_override = 0;   // GNSSCORR_TRACK_CPW: channels per workgroup
-  int stage_perch = 0;    // GNSSCORR_TRACK_STAGE_PERCH=1: channels on different streams stage their own
+  int v1 = 0;             // GNSSCORR_TRACK_V1=1: workgroups whose channels read different
+                          // streams use the round-2 per-lane global reads, not the piece path (A/B)
   size_t lds_max = 0;     // LDS bytes a workgroup may allocate (gnsscorr_device_lds_bytes)
 };
 
@@ -729,7 +1046,7 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   c->tic = c->tic_ref;
   if (const char* e = getenv("GNSSCORR_TRACK_STAGE_IF")) c->stage_if = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_CPW")) c->cpw_override = atoi(e);
-  if (const char* e = getenv("GNSSCORR_TRACK_STAGE_PERCH")) c->stage_perch = atoi(e) != 0;
+  if (const char* e = getenv("GNSSCORR_TRACK_V1")) c->v1 = atoi(e) != 0;
   const int C = cfg->n_channels;
   auto fail = [&](int code) {
     gnsscorr_track_destroy(c);
@@ -765,19 +1082,15 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   return GNSSCORR_OK;
 }
 
-// Layout hint: 1 = every channel reads its own IF stream (C_s = 1).  For int8
-// streams the kernel then stages each channel's stream in its own LDS slot
-// (one workgroup per CU) instead of letting lanes read their 128-byte runs
-// from global memory, where eight 16-byte loads per lane touch 64 lines per
-// wave-instruction: 85 -> 64 us per 3072-channel call.  Packed streams and
-// receivers (channels sharing a stream) keep the default (per-channel slots
-// measured slower there: 48 -> 53 us packed, 33 -> 44 us for 256 x 12).
+// Layout hint (round 2: per-channel LDS staging for one stream per channel).
+// Since round 3 every workgroup picks its IF path itself -- the shared LDS
+// stage when its channels read one stream, the per-wave piece path otherwise --
+// so the hint is accepted and has no effect.
 extern "C" int gnsscorr_track_set_layout(gnsscorr_track_ctx* c, int one_stream_per_channel) {
   if (!c || one_stream_per_channel < 0 || one_stream_per_channel > 1) {
     gnsscorr_set_error("gnsscorr_track_set_layout: bad arguments");
     return GNSSCORR_EINVAL;
   }
-  c->stage_perch = one_stream_per_channel && !packed(c);
   return GNSSCORR_OK;
 }
 
@@ -820,16 +1133,19 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
     gnsscorr_set_error("IF base and stream stride must be %d-byte aligned", pk ? 8 : 16);
     return GNSSCORR_EINVAL;
   }
+  const int C = c->cfg.n_channels;
   int threads = (int)((nsamp + kRun - 1) / kRun);
   threads = (threads + 63) & ~63;
-  const int C = c->cfg.n_channels;
   const size_t stage_bytes = (size_t)((nsamp + kRun - 1) / kRun) * kPitch * 16;
   int stage = iq && c->stage_if && stage_bytes <= (size_t)kStageMaxBytes;
-  if (stage && c->stage_perch) stage = 2;
-  // dynamic LDS: epoch sums, E/P/L row bytes, staged IF (kernel layout)
+  if (stage && c->v1) stage = 3;
+  // dynamic LDS: epoch sums, E/P/L row bytes, then one region that holds either
+  // the workgroup's shared IF stage or the waves' 4 KiB piece slots
   auto lds_bytes = [&](int cpw) {
     const size_t sum_bytes = (size_t)((cpw * ((int)nsamp / GNSSCORR_OSG_ROW + 2) * 6 + 3) & ~3) * 4;
-    return sum_bytes + (iq ? (size_t)cpw * kPk8Stage + (stage ? stage_bytes * (stage == 2 ? cpw : 1) : 0) : 0);
+    const size_t slots = (size_t)(threads / 64) * cpw * kStage2Bytes;
+    return sum_bytes + (iq ? (size_t)cpw * kPk8Stage +
+                                 (stage ? (stage_bytes > slots ? stage_bytes : slots) : 0) : 0);
   };
   // Channels per workgroup: as many as fit 1024 threads (they share one staged
   // IF copy).  The 1.5-round tail at 3072 channels (768 workgroups, 512
@@ -837,8 +1153,8 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   // cpw 4 33.4 us, 3 35.2, 2 34.1, 1 46.4); GNSSCORR_TRACK_CPW overrides.
   int cpw = min(kMaxCpw, kMaxThreads / threads);
   if (c->cpw_override > 0) cpw = min(cpw, c->cpw_override);
-  // per-channel slots must fit beside the static LDS (s_lo, s_stream: < 1 KiB)
-  if (stage == 2 && lds_bytes(cpw) + 1024 > c->lds_max) stage = 1;
+  // the LDS must fit beside the static LDS (s_lo, s_stream: < 1 KiB)
+  while (cpw > 1 && lds_bytes(cpw) + 1024 > c->lds_max) cpw--;
   dim3 grid((C + cpw - 1) / cpw), block(threads * cpw);
   const size_t dyn = lds_bytes(cpw);
 #define TRACK_LAUNCH(IQ, PK, ST)                                                               \
