@@ -190,7 +190,13 @@ __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
 // lanes of a reused register that the branch had masked off -- the cause of
 // the wrong sums DESIGN.md recorded for reordered IF loads in round 2.
 __device__ __forceinline__ uint32_t mad24(int a, int b, uint32_t c) {
+#ifdef TRACK_ASM_MAD   // the round-2 form, kept only to reproduce the hazard (tools/gpu_mad.sh)
+  uint32_t d;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+#else
   return c + (uint32_t)__mul24(a, b);
+#endif
 }
 __device__ __forceinline__ void seg_flush(int si, int sq, int lb, int pb, int eb, Acc& cur) {
   cur.a[0] = mad24(lb, si, cur.a[0]);
@@ -909,12 +915,26 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
           // LDS) goes through the same loop with its missing pairs masked, so
           // it does not serialise behind the full runs of its wave.
           const uint4* run = stage ? &s_ifq[tid * kPitch] : reinterpret_cast<const uint4*>(src);
+#ifdef TRACK_LOAD4   // round 2's "four loads at a time" variant (tools/gpu_mad.sh)
+          if (!stage) {
+#pragma unroll 1
+            for (int j = 0; j < kVec; j += 4) {
+              const uint4 u0 = run[j], u1 = run[j + 1], u2 = run[j + 2], u3 = run[j + 3];
+              chunk(u0, j);
+              chunk(u1, j + 1);
+              chunk(u2, j + 2);
+              chunk(u3, j + 3);
+            }
+          } else
+#endif
+          {
           uint4 nx = run[0];
 #pragma unroll 1
           for (int j = 0; j < kVec; j++) {
             const uint4 u = nx;
             if (j + 1 < kVec) nx = run[j + 1];
             chunk(u, j);
+          }
           }
         } else if (PK && L == kRun) {
           // packed, unstaged (channels of a workgroup on different streams):
