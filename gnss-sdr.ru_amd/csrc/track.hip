@@ -56,7 +56,7 @@ constexpr int kMaxNsamp = kRun * kMaxThreads;
 constexpr uint64_t kNever = ~0ull;
 constexpr int kPitch = 9;             // 16-byte chunks per staged lane run (8 + 1 pad)
 constexpr int kStageMaxBytes = 48 * 1024;
-constexpr int kPk8Stage = 3072;       // LDS bytes of the E/P/L row (D <= 3071: slew <= 1025)
+constexpr int kPk8Stage = 3088;       // LDS bytes of the E/P/L row (D <= 3071: slew <= 1025) + 3 of misalignment
 constexpr int kMaxCpw = 4;            // channels per workgroup (32 waves/CU: two 1024-thread WGs)
 
 // 8-phase LO (correlator.c:203-204) as 4-bit two's-complement nibbles.
@@ -289,41 +289,17 @@ __device__ __forceinline__ void corr_pair(uint32_t x, uint32_t& p0, uint32_t& kp
   }
 }
 
-// Epoch-segmented reduction of the per-thread sums and the per-channel epilogue
-// (one thread per channel): dumps, ms/bit counters, TIC latch, carrier cycles and
-// the new channel state (correlator.c:243-316).  Every thread of the workgroup
-// calls it (it holds a barrier).
-__device__ __forceinline__ void finish_call(const Chan& c, const gnsscorr_nco_cmd& cmd,
-                                            gnsscorr_chan_state st, int chn, bool have,
-                                            bool active, int tid, bool runs, int e0,
-                                            bool switched, const Acc& first, const Acc& cur,
-                                            int32_t* s_sum, uint32_t ndump, uint64_t Rtot,
-                                            int nsamp, int64_t tic_count,
-                                            gnsscorr_track_result* __restrict__ res,
-                                            gnsscorr_chan_state* __restrict__ state,
-                                            int32_t* __restrict__ all_dumps, int max_dumps) {
-  // ---- epoch-segmented reduction ------------------------------------------
-  // thread contributes (e0, switched ? first : cur) and (e0+1, cur) if switched
-  // (a wave never spans two thread groups: T is a multiple of 64)
-  const int e_hi_mine = e0 + (switched ? 1 : 0);
-  const int e_lo = wave_min(runs ? e0 : 0x7fffffff);
-  const int e_hi = wave_max(runs ? e_hi_mine : -1);
-  const int lane = threadIdx.x & 63;
-  for (int e = e_lo; e <= e_hi; e++) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      uint32_t v = 0;
-      if (e == e0) v += switched ? first.a[k] : cur.a[k];
-      if (switched && e == e0 + 1) v += cur.a[k];
-      const int s = wave_sum((int)v);
-      if (lane == 0) atomicAdd(&s_sum[e * 6 + k], s);
-    }
-  }
-  __syncthreads();
-  TRACK_PSTAMP(4);
-
-  // ---- per-channel epilogue (one thread per channel) ------------------------
-  if (tid != 0 || !have) return;
+// Per-channel epilogue of a call (one thread): dumps, ms/bit counters, TIC latch,
+// carrier cycles and the new channel state (correlator.c:243-316).  sum(i):
+// the call's epoch sums, word i = epoch * 6 + k (LDS or global).
+template <typename SumAt>
+__device__ __forceinline__ void channel_epilogue(const Chan& c, const gnsscorr_nco_cmd& cmd,
+                                                 gnsscorr_chan_state st, int chn, bool active,
+                                                 uint32_t ndump, uint64_t Rtot, int nsamp,
+                                                 int64_t tic_count, SumAt sum,
+                                                 gnsscorr_track_result* __restrict__ res,
+                                                 gnsscorr_chan_state* __restrict__ state,
+                                                 int32_t* __restrict__ all_dumps, int max_dumps) {
   if (!active) {   // idle channel: only the epoch load (correlator.c:177-185)
     gnsscorr_track_result r;
     memset(&r, 0, sizeof r);
@@ -350,7 +326,7 @@ __device__ __forceinline__ void finish_call(const Chan& c, const gnsscorr_nco_cm
     uint32_t v[6];
 #pragma unroll
     for (int k = 0; k < 6; k++)
-      v[k] = (uint32_t)s_sum[d * 6 + k] + (d == 0 ? (uint32_t)st.acc[k] : 0u);
+      v[k] = sum(d * 6 + k) + (d == 0 ? (uint32_t)st.acc[k] : 0u);
     if (all_dumps && (int)d < max_dumps)
       for (int k = 0; k < 6; k++) all_dumps[((int64_t)chn * max_dumps + d) * 6 + k] = (int32_t)v[k];
     if (d + 1 == ndump)
@@ -361,7 +337,7 @@ __device__ __forceinline__ void finish_call(const Chan& c, const gnsscorr_nco_cm
   }
   uint32_t nacc[6];
   for (int k = 0; k < 6; k++)
-    nacc[k] = (uint32_t)s_sum[ndump * 6 + k] + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
+    nacc[k] = sum(ndump * 6 + k) + (ndump == 0 ? (uint32_t)st.acc[k] : 0u);
 
   const uint64_t Wtot = ((uint64_t)c.P0 + (uint64_t)nsamp * c.cinc) >> 32;
   uint32_t cycle_end;
@@ -397,6 +373,45 @@ __device__ __forceinline__ void finish_call(const Chan& c, const gnsscorr_nco_cm
   st.bit_counter = bit;
   st.msbit_reg = msbit;
   state[chn] = st;
+}
+
+// Epoch-segmented reduction of the per-thread sums and the per-channel epilogue
+// (one thread per channel): dumps, ms/bit counters, TIC latch, carrier cycles and
+// the new channel state (correlator.c:243-316).  Every thread of the workgroup
+// calls it (it holds a barrier).
+__device__ __forceinline__ void finish_call(const Chan& c, const gnsscorr_nco_cmd& cmd,
+                                            gnsscorr_chan_state st, int chn, bool have,
+                                            bool active, int tid, bool runs, int e0,
+                                            bool switched, const Acc& first, const Acc& cur,
+                                            int32_t* s_sum, uint32_t ndump, uint64_t Rtot,
+                                            int nsamp, int64_t tic_count,
+                                            gnsscorr_track_result* __restrict__ res,
+                                            gnsscorr_chan_state* __restrict__ state,
+                                            int32_t* __restrict__ all_dumps, int max_dumps) {
+  // ---- epoch-segmented reduction ------------------------------------------
+  // thread contributes (e0, switched ? first : cur) and (e0+1, cur) if switched
+  // (a wave never spans two thread groups: T is a multiple of 64)
+  const int e_hi_mine = e0 + (switched ? 1 : 0);
+  const int e_lo = wave_min(runs ? e0 : 0x7fffffff);
+  const int e_hi = wave_max(runs ? e_hi_mine : -1);
+  const int lane = threadIdx.x & 63;
+  for (int e = e_lo; e <= e_hi; e++) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      uint32_t v = 0;
+      if (e == e0) v += switched ? first.a[k] : cur.a[k];
+      if (switched && e == e0 + 1) v += cur.a[k];
+      const int s = wave_sum((int)v);
+      if (lane == 0) atomicAdd(&s_sum[e * 6 + k], s);
+    }
+  }
+  __syncthreads();
+  TRACK_PSTAMP(4);
+
+  // ---- per-channel epilogue (one thread per channel) ------------------------
+  if (tid != 0 || !have) return;
+  channel_epilogue(c, cmd, st, chn, active, ndump, Rtot, nsamp, tic_count,
+                   [&](int i) { return (uint32_t)s_sum[i]; }, res, state, all_dumps, max_dumps);
   TRACK_PSTAMP(5);
 }
 
@@ -780,9 +795,16 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   // stage that part of the channel's row in LDS so the reload at every code
   // carry is an LDS read, not a dependent global-memory round trip.
   const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
-  const bool pk_lds = IQ && active && c.j1 != kNever && pk_hi < (uint32_t)kPk8Stage;
-  if (pk_lds)
-    for (uint32_t i = tid; i <= pk_hi; i += T) s_pk8[i] = pk8[c.base + (int)i];
+  const bool pk_lds = IQ && active && c.j1 != kNever && pk_hi < 3072u;
+  if (pk_lds) {
+    // whole dwords of the row (the packed table is padded by 64 bytes): byte i of
+    // the staged row is s_pk8[i] with s_pk8 offset by the row's misalignment
+    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(pk8) + (c.base >> 2);
+    uint32_t* l32 = reinterpret_cast<uint32_t*>(s_pk8);
+    const int n32 = (int)((pk_hi + (uint32_t)(c.base & 3)) >> 2) + 1;
+    for (int i = tid; i < n32; i += T) l32[i] = g32[i];
+  }
+  s_pk8 += c.base & 3;
   __syncthreads();
   int sst = -1;
   bool uni = true;
@@ -1001,6 +1023,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
 }
 
 
+
 }  // namespace
 
 // ============================================================================
@@ -1074,7 +1097,7 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   };
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_pk, sizeof(uint32_t) * GNSSCORR_OSG_PK_LEN) != hipSuccess ||
-      hipMalloc(&c->d_pk8, GNSSCORR_OSG_PK_LEN) != hipSuccess ||
+      hipMalloc(&c->d_pk8, GNSSCORR_OSG_PK_LEN + 64) != hipSuccess ||   // +64: whole-dword row staging
       hipMalloc(&c->d_state, sizeof(gnsscorr_chan_state) * C) != hipSuccess ||
       hipMalloc(&c->d_cmds, sizeof(gnsscorr_nco_cmd) * C) != hipSuccess ||
       hipMalloc(&c->d_res, sizeof(gnsscorr_track_result) * C) != hipSuccess ||
@@ -1092,6 +1115,7 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
     for (int k = 0; k < 3; k++) b |= ((uint32_t)(int8_t)(pk[i] >> (8 * k)) & 3u) << (2 * k);
     reinterpret_cast<uint8_t*>(pk)[i] = (uint8_t)b;
   }
+  if (e == hipSuccess) e = hipMemset(c->d_pk8, 0, GNSSCORR_OSG_PK_LEN + 64);
   if (e == hipSuccess) e = hipMemcpy(c->d_pk8, pk, GNSSCORR_OSG_PK_LEN, hipMemcpyHostToDevice);
   free(pk);
   if (e != hipSuccess || hipMemset(c->d_state, 0, sizeof(gnsscorr_chan_state) * C) != hipSuccess) {

@@ -20,7 +20,8 @@ __device__ unsigned long long* g_stamps;
 #include "../gnss-sdr.ru_amd/csrc/track.hip"
 
 int main(int argc, char** argv) {
-  const int C = argc > 1 ? atoi(argv[1]) : 3072, NS = 16368, RX = (C + 11) / 12, K = 4;
+  const bool cs1 = argc > 2 && argv[2][0] == 'c';   // "cs1": one stream per channel
+  const int C = argc > 1 ? atoi(argv[1]) : 3072, NS = 16368, RX = cs1 ? C : (C + 11) / 12, K = 4;
   gnsscorr_track_cfg cfg = {};
   cfg.n_channels = C;
   cfg.max_nsamp = NS;
@@ -36,7 +37,7 @@ int main(int argc, char** argv) {
     gnsscorr_nco_cmd& m = cmd[k];
     memset(&m, 0, sizeof m);
     m.prn = 1 + (k % C) % 32;
-    m.stream = (k % C) / 12;
+    m.stream = cs1 ? (k % C) : (k % C) / 12;
     m.carrier_incr = 635008600u + (uint32_t)((rand() % 524000) - 262000) * 20u;
     m.code_incr = 6710886u * 40u + (uint32_t)(rand() % 20) - 10u;
     m.epoch_load = -1;
@@ -67,7 +68,7 @@ int main(int argc, char** argv) {
     starts.push_back((double)(a[0] - t0));
     life.push_back((double)(a[5] - a[0]));
   }
-  printf("C=%d kernel span %.1f us (stamp clock 100 MHz)\n", C, (t1 - t0) / 100.0);
+  printf("%s C=%d kernel span %.1f us (stamp clock 100 MHz)\n", cs1 ? "cs1" : "rx12", C, (t1 - t0) / 100.0);
   const char* nm[6] = {"", "cmd/state", "tables+barrier", "run (wave 0)", "reduce+barrier", "epilogue"};
   for (int i = 1; i < 6; i++) printf("  %-16s %7.2f us\n", nm[i], ph[i] / W / 100.0);
   printf("  run (wave 3)     %7.2f us\n", ph3w3 / W / 100.0);

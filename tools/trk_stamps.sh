@@ -5,4 +5,4 @@ set -e
 /opt/rocm/bin/hipcc --offload-arch=gfx950 /tmp/ts.o gnss-sdr.ru_amd/build/common.c.o \
   gnss-sdr.ru_amd/build/codes.c.o -o /tmp/trk_stamps
 timeout -k 10 60 /tmp/trk_stamps 3072
-timeout -k 10 60 /tmp/trk_stamps 12288
+timeout -k 10 60 /tmp/trk_stamps 3072 cs1
