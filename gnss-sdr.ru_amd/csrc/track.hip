@@ -630,7 +630,9 @@ __device__ __forceinline__ void run_pieces(const int8_t* __restrict__ ifbuf, int
         unpack8(s_pk8[g.ld], g.lb, g.pb, g.eb);
         g.ti = g.tq = g.pi = g.pq = 0;
         g.carried = false;
-        if (L == kPieceLen) {   // every lane but the last of a call
+        // one code path per wave: a wave with one partial lane (the call's last
+        // samples) runs the guarded loop for all its lanes instead of both loops
+        if (__all(L == kPieceLen)) {   // every wave but the last of a channel
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             const uint4 u = chunk(j);
