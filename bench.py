@@ -491,6 +491,8 @@ SDR_STRONG_OPS_ROW = 2048 * 8 + 11 * 1024 * 12 + 2048 * 4
 SDR_ACCUM_BYTES = 2048 * 4 + 3 * 2048 // 8 + 16 * 2048 * 4 / SDR_CORR_CH
 SDR_FE_BLOCKS = 2000         # GN3S 5-ms reads per front-end launch (10 s of 4 Msps 2-bit samples)
 SDR_CHAN_N, SDR_CHAN_MS = 8192, 1000   # Channel objects x 1-ms Channel::Accum calls per launch
+SDR_LOOP_RX, SDR_LOOP_REP, SDR_LOOP_PK = 8, 32, 100   # closed loop: 8 receivers' streams x 12
+                                                       # channels, replicated 32x; packets/launch
 
 
 def run_sdr(dist, dev, steps, warmup):
@@ -613,9 +615,86 @@ def run_sdr(dist, dev, steps, warmup):
     corr_ctx_k.sync()
     dt_ch = dist.max(time.perf_counter() - t0)
     ms_ch = e0.elapsed_ms(e1) / ch_steps
+    loop = run_sdr_loop(dist, dev, rng)
     return dict(dt_acq=dt_acq, ms_acq=ms_acq, dt_corr=dt_corr, ms_corr=ms_corr, steps=steps,
                 bufs=bufs, dt_fe=dt_fe, ms_fe=ms_fe, mw=mw, long=long, dt_ch=dt_ch, ms_ch=ms_ch,
-                ch_steps=ch_steps, ch_corr=corr1)
+                ch_steps=ch_steps, ch_corr=corr1, loop=loop)
+
+
+def sdr_loop_scene(rng, n_pk):
+    """SDR_LOOP_RX receivers' 2.048 Msps CPX streams (8 C/A signals each + noise, int16)
+    and 12 channels per receiver (8 on the signals, 4 on empty codes)."""
+    n = n_pk * SDR_N
+    t = np.arange(n) / 2.048e6
+    pk = np.zeros((n_pk, SDR_LOOP_RX, SDR_N, 2), np.int16)
+    chans = []
+    for r in range(SDR_LOOP_RX):
+        svs = rng.choice(32, 12, replace=False)
+        z = 2.0 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+        for j, sv in enumerate(svs):
+            cp0, dop = float(rng.uniform(0, 1023)), float(rng.integers(-16, 17) * 250)
+            if j < 8:
+                chips = gc.ca_code(int(sv) + 1).astype(np.float64)
+                cp = (cp0 + t * 1.023e6 * (1 + dop / 1575.42e6)) % 1023
+                z += 3.0 * chips[cp.astype(np.int64)] * np.exp(2j * np.pi * (38400.0 + dop) * t)
+                cs = int(round((1023 - cp0) * 2048 / 1023)) % 2048
+            else:
+                cs = int(rng.integers(0, 2048))
+            chans.append((r, int(sv), cs, int(dop)))
+        pk[:, r, :, 0] = np.clip(np.round(z.real), -127, 127).reshape(n_pk, SDR_N)
+        pk[:, r, :, 1] = np.clip(np.round(z.imag), -127, 127).reshape(n_pk, SDR_N)
+    return pk, chans
+
+
+def run_sdr_loop(dist, dev, rng):
+    """The device-resident GPS-SDR closed loop (gnsscorr_sdr_track_dev): Correlate's packet
+    schedule, UpdateState, DumpAccum and Channel::Accum per dump, SDR_LOOP_PK packets per
+    launch for SDR_LOOP_RX * 12 * SDR_LOOP_REP channels; consecutive launches continue the
+    same channels.  Work = dumps (1-ms correlations through the whole loop) counted from
+    the correlator states' dump counters of the channels still active at the end."""
+    pk, chans = sdr_loop_scene(rng, 2 * SDR_LOOP_PK)
+    ctx = gc.SdrCorrCtx(device=dev)
+    chans = chans * SDR_LOOP_REP
+    n = len(chans)
+    st = np.zeros(n, gc.SDR_CHAN)
+    ch = np.zeros(n, gc.SDR_CHANNEL)
+    for c, (r, sv, cs, dop) in enumerate(chans):
+        st[c] = ctx.init_chan(sv, cs, dop, 0.0)
+        ch[c] = ctx.channel_start(c, sv, dop, 1)
+    rx = np.array([c[0] for c in chans], np.int32)
+    half = SDR_LOOP_PK * SDR_LOOP_RX * SDR_N * 4
+    d_pk = gc.DevBuf.from_array(pk, dev)
+    d_rx, d_st, d_c, d_ch = (gc.DevBuf.from_array(a, dev) for a in
+                             (rx, st, np.zeros(n, gc.SDR_CORR), ch))
+    d_stat = gc.DevBuf.from_array(np.zeros(n, np.int32), dev)
+    d_ev = gc.DevBuf(4096 * gc.SDR_SUBFRAME.itemsize, dev)
+    d_ne = gc.DevBuf.from_array(np.zeros(1, np.int32), dev)
+
+    def launch(i):
+        ctx.track_dev(d_pk.ptr + (i % 2) * half, SDR_LOOP_PK, SDR_LOOP_RX, n, d_rx.ptr,
+                      d_st.ptr, d_c.ptr, d_ch.ptr, None, None, 0, None, d_stat.ptr, d_ev.ptr,
+                      4096, d_ne.ptr)
+
+    launch(0)
+    ctx.sync()
+    c0 = d_st.download(np.uint8).view(gc.SDR_CHAN)["count"].astype(np.int64)
+    k_steps = 4
+    e0, e1 = gc.Event(dev), gc.Event(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    e0.record(ctx.stream)
+    for i in range(k_steps):
+        launch(i + 1)
+    e1.record(ctx.stream)
+    ctx.sync()
+    dt = dist.max(time.perf_counter() - t0)
+    ms = e0.elapsed_ms(e1) / k_steps
+    s1 = d_st.download(np.uint8).view(gc.SDR_CHAN)
+    live = s1["active"] != 0
+    dumps = int((s1["count"].astype(np.int64) - c0)[live].sum())
+    status = d_stat.download(np.int32)
+    return dict(dt=dt, ms=ms, steps=k_steps, channels=n, live=int(live.sum()),
+                dumps=dumps, stopped=int((status != 0).sum()), pk=pk, chans=chans[:12])
 
 
 def cpu_baseline_sdr(bufs, budget_s=5.0):
@@ -665,6 +744,35 @@ SDR_MW_PASSES = {"medium": 1, "weak": 15}
 # ten 2048-point int16 IFFTs (11 x 1024 butterflies x 12 ops), 2048 columns x 10 post-DFT
 # bins x (10 complex MACs = 80 ops + |.|^2 3 + accumulate/compare 1)
 SDR_MW_OPS_PASS = 10 * SDR_N * 8 + 10 * 11 * 1024 * 12 + SDR_N * 10 * 84
+
+
+def cpu_baseline_sdr_loop(loop, budget_s=4.0):
+    """Correlator::Correlate on the host, scalar (oracle/sdr_corr.c: schedule, Accum,
+    UpdateState, DumpAccum) with its deterministic loop callback standing in for
+    Channel::Accum, over receiver 0's 12 channels, packet after packet."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sdr_oracle
+    o = sdr_oracle.OracleSdrCorr()
+    chans = loop["chans"]
+    st = np.zeros(len(chans), sdr_oracle.CHAN)
+    for c, (r, sv, cs, dop) in enumerate(chans):
+        st[c] = o.init_chan(sv, cs, dop, 0.0)
+    corr = np.zeros(len(chans), sdr_oracle.CORR)
+    pk = loop["pk"]
+    k = [0]
+
+    def run(calls):
+        c0 = st["count"].astype(np.int64)
+        for _ in range(calls):
+            o.correlate(pk[k[0] % len(pk), 0], st, corr)
+            k[0] += 1
+        return int((st["count"].astype(np.int64) - c0)[st["active"] != 0].sum())
+
+    dumps, dt, n = _timed(run, budget_s)
+    return dict(value=dumps / dt, unit="channel-ms/s", cores=1, kind="port",
+                sample=f"{n} packets x {len(chans)} channels of the scalar C restatement "
+                       "(oracle/sdr_corr.c: Correlate + Accum + UpdateState + DumpAccum; "
+                       "deterministic loop callback instead of Channel::Accum)")
 
 
 def cpu_baseline_sdr_mw(long, kind, budget_s=4.0):
@@ -1220,6 +1328,19 @@ def main():
                           "launch (one thread per channel), synthetic 50 bps navigation streams",
                 "kernel_ms_per_launch": sdr["ms_ch"],
             }
+            lp = sdr["loop"]
+            out["sdr_closed_loop"] = {
+                "metric": "closed-loop channel-ms/sec (GPS-SDR Correlate schedule + UpdateState + "
+                          "DumpAccum + Channel::Accum per dump, device-resident, bit-exact with "
+                          "the host-scheduled loop)",
+                "value": lp["dumps"] * W / lp["dt"], "unit": "channel-ms/s",
+                "config": f"{lp['channels']} channels ({SDR_LOOP_RX} receivers x 12, replicated "
+                          f"{SDR_LOOP_REP}x) x {SDR_LOOP_PK} consecutive 2048-sample packets per "
+                          "launch (gnsscorr_sdr_track_dev, one workgroup per channel)",
+                "kernel_ms_per_launch": lp["ms"],
+                "channels_live_at_end": lp["live"], "channels_stopped": lp["stopped"],
+                "realtime_channels_per_gpu": lp["dumps"] / lp["steps"] / lp["ms"],
+            }
             fe_in = SDR_FE_BLOCKS * gc.GN3S_BLOCK_IN
             fe_bytes = fe_in // 4 + SDR_FE_BLOCKS * gc.GN3S_BLOCK_OUT * 4
             out["sdr_frontend"] = {
@@ -1253,6 +1374,7 @@ def main():
                     out[f"sdr_acquisition_{kind}"]["cpu_baseline"] = \
                         cpu_baseline_sdr_mw(sdr["long"], kind)
                 out["sdr_tracking"]["cpu_baseline"] = cpu_baseline_sdr_accum()
+                out["sdr_closed_loop"]["cpu_baseline"] = cpu_baseline_sdr_loop(sdr["loop"])
                 cb = cpu_baseline_sdr_channel(sdr["ch_corr"])
                 if cb:
                     out["sdr_channel"]["cpu_baseline"] = cb

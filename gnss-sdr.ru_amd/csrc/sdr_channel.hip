@@ -24,6 +24,7 @@
 #include <math.h>
 #include <string.h>
 #include "gnsscorr_internal.h"
+#include "sdr_corr_state.h"
 
 #pragma clang fp contract(off)
 
@@ -493,6 +494,98 @@ __global__ __launch_bounds__(64) void sdr_channel_kernel(
   memcpy(&g, &s, offsetof(Chan, fft_buff));
 }
 
+// Device-resident closed loop: Correlator::Correlate (correlator.cpp:160-237)
+// over n_packets packets with UpdateState, DumpAccum (:452-525) and the
+// channel's Accum / ProcessFeedback (:530-555) at every dump -- the loop the
+// reference runs per packet on the host, here without leaving the device.
+// One 128-thread workgroup per channel: both waves run the Accum segments
+// (sdrc::accum_block, the kernel sdr_accum_kernel runs per job); thread 0
+// keeps the correlator state in LDS and runs the scalar bookkeeping and
+// Channel::Accum between segments.  The schedule is the host's
+// (gnsscorr_sdr_correlate): per packet at most 3 segments, at most 2 dumps.
+__global__ __launch_bounds__(sdrc::kThreads) void sdr_track_kernel(
+    const uint32_t* __restrict__ packets, int n_packets, int n_rx, const int32_t* __restrict__ rx,
+    gnsscorr_sdr_chan* __restrict__ states, gnsscorr_sdr_corr* __restrict__ corr,
+    Chan* __restrict__ chans, gnsscorr_sdr_feedback* __restrict__ fb_last,
+    gnsscorr_sdr_dump_rec* __restrict__ log, int log_per_ch, int32_t* __restrict__ n_log,
+    int32_t* __restrict__ status, gnsscorr_sdr_subframe* __restrict__ ev, int max_ev,
+    int32_t* __restrict__ n_ev, const uint32_t* __restrict__ carrier,
+    const uint32_t* __restrict__ codebits, int saturate, Twiddles tw) {
+  using namespace sdrc;
+  __shared__ gnsscorr_sdr_chan s_st;
+  __shared__ gnsscorr_sdr_corr s_c;
+  __shared__ int32_t red[kThreads / 64][6];
+  const int ch = blockIdx.x;
+  const bool t0 = threadIdx.x == 0;
+  Chan cs;   // thread 0's copy of the Channel object but its FFT buffer
+  gnsscorr_sdr_feedback f = {};
+  int32_t ndump = 0, stat = 0;
+  const int r = rx ? rx[ch] : 0;
+  if (t0) {
+    s_st = states[ch];
+    s_c = corr[ch];
+    memcpy(&cs, &chans[ch], offsetof(Chan, fft_buff));
+  }
+  if (r < 0 || r >= n_rx) stat = -1;
+  __syncthreads();
+  Events e = {ev, max_ev, n_ev, ch, 0};
+  for (int p = 0; p < n_packets && stat == 0 && s_st.active; p++) {
+    const uint32_t* pkt = packets + ((size_t)p * n_rx + r) * kN;
+    int off = 0, left = kN, dumps = 0;
+    for (int phase = 0; phase < 3; phase++) {
+      const bool dump = dumps < 2 && s_st.rollover <= (uint32_t)left;
+      const int samps = dump ? (int)s_st.rollover : left;
+      if (samps > 0) {
+        const gnsscorr_sdr_accum_job j = make_job(s_st, 0, off, samps);
+        if (!job_in_range(j, 1)) {   // uniform: every thread sees the same state
+          stat = 1 + p;
+          break;
+        }
+        // ends with a barrier: every thread has read s_st before thread 0 writes it
+        const gnsscorr_sdr_corr a = accum_block(j, pkt, carrier, codebits, saturate, red);
+        if (t0) {
+          for (int k = 0; k < 3; k++) {
+            s_c.i[k] = (int32_t)((uint32_t)s_c.i[k] + (uint32_t)a.i[k]);
+            s_c.q[k] = (int32_t)((uint32_t)s_c.q[k] + (uint32_t)a.q[k]);
+          }
+          update_state(&s_st, samps);
+        }
+      } else {
+        __syncthreads();
+      }
+      off += samps;
+      left -= samps;
+      if (dump) {
+        if (t0) {
+          rotate(&s_st, &s_c);
+          e.ms = p;
+          accum(cs, chans[ch].fft_buff, tw, s_c, &f, e);
+          if (ndump < log_per_ch) {
+            gnsscorr_sdr_dump_rec& d = log[(size_t)ch * log_per_ch + ndump];
+            d.packet = p;
+            d.phase = phase;
+            d.corr = s_c;
+            d.fb = f;
+          }
+          after_feedback(&s_st, &s_c, f);
+        }
+        ndump++;
+        dumps++;
+      }
+      __syncthreads();
+      if (!dump || !s_st.active) break;
+    }
+  }
+  if (t0) {
+    states[ch] = s_st;
+    corr[ch] = s_c;
+    memcpy(&chans[ch], &cs, offsetof(Chan, fft_buff));
+    if (fb_last && ndump > 0) fb_last[ch] = f;
+    if (n_log) n_log[ch] = ndump;
+    status[ch] = stat;
+  }
+}
+
 Twiddles make_twiddles() {   // fft.cpp:121-149 for N = 512
   Twiddles t;
   const double pi = 3.14159265358979323846264338327;
@@ -547,6 +640,36 @@ extern "C" int gnsscorr_sdr_channel_accum_dev(gnsscorr_sdr_corr_ctx* ctx, int n_
   static const Twiddles tw = make_twiddles();
   hipLaunchKernelGGL(sdr_channel_kernel, dim3((n_ch + 63) / 64), dim3(64), 0, s, n_ch, n_ms,
                      d_corr, d_ch, d_fb, d_fb_last, d_events, max_events, d_n_events, tw);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sdr_track_dev(gnsscorr_sdr_corr_ctx* ctx, const int16_t* d_packets,
+                                      int n_packets, int n_rx, int n_ch, const int32_t* d_rx,
+                                      gnsscorr_sdr_chan* d_states, gnsscorr_sdr_corr* d_corr,
+                                      gnsscorr_sdr_channel* d_ch, gnsscorr_sdr_feedback* d_fb_last,
+                                      gnsscorr_sdr_dump_rec* d_log, int log_per_ch,
+                                      int32_t* d_n_log, int32_t* d_status,
+                                      gnsscorr_sdr_subframe* d_events, int max_events,
+                                      int32_t* d_n_events) {
+  if (!ctx || n_packets < 0 || n_rx < 1 || n_ch < 0 || (n_packets > 0 && !d_packets) ||
+      (n_ch > 0 && (!d_states || !d_corr || !d_ch || !d_status || !d_n_events)) ||
+      log_per_ch < 0 || (log_per_ch > 0 && !d_log) || max_events < 0 ||
+      (max_events > 0 && !d_events)) {
+    gnsscorr_set_error("gnsscorr_sdr_track_dev: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  if (n_ch == 0) return GNSSCORR_OK;
+  HIP_TRY(hipSetDevice(gnsscorr_sdr_corr_device(ctx)));
+  hipStream_t s = (hipStream_t)gnsscorr_sdr_corr_stream(ctx);
+  const uint32_t *carrier, *codebits;
+  int saturate;
+  gnsscorr_sdr_corr_tables(ctx, &carrier, &codebits, &saturate);
+  static const Twiddles tw = make_twiddles();
+  hipLaunchKernelGGL(sdr_track_kernel, dim3(n_ch), dim3(sdrc::kThreads), 0, s,
+                     (const uint32_t*)d_packets, n_packets, n_rx, d_rx, d_states, d_corr, d_ch,
+                     d_fb_last, d_log, log_per_ch, d_n_log, d_status, d_events, max_events,
+                     d_n_events, carrier, codebits, saturate, tw);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }

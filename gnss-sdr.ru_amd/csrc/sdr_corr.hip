@@ -25,6 +25,7 @@
 #include <string.h>
 #include <vector>
 #include "gnsscorr_internal.h"
+#include "sdr_corr_state.h"
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -38,23 +39,7 @@
 
 namespace {
 
-constexpr int kN = 2048;                 // SAMPS_MS
-constexpr int kRow = 2 * kN;             // pre-sampled row length
-constexpr int kIF = 38400;               // IF_FREQUENCY (signaldef.h:34)
-constexpr int kCarrSpacing = 10;         // CARRIER_SPACING (config.h:82)
-constexpr int kCarrBins = 1500;          // CARRIER_BINS = 15000 / 10
-constexpr int kSBins = 2 * kCarrBins + 1;
-constexpr int kCodeBins = 50;            // CODE_BINS (config.h:81)
-constexpr int kCBins = 2 * kCodeBins + 1;
-constexpr int kSV = 32;                  // MAX_SV
-constexpr int kThreads = 128;
-constexpr double kInvFs = 4.882812500000000e-7;   // INVERSE_SAMPLE_FREQUENCY
-
-__device__ __forceinline__ int16_t lo16(uint32_t v) { return (int16_t)(v & 0xFFFFu); }
-__device__ __forceinline__ int16_t hi16(uint32_t v) { return (int16_t)(v >> 16); }
-__device__ __forceinline__ int32_t sat16(int32_t v) {
-  return v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
-}
+using namespace sdrc;
 
 __global__ __launch_bounds__(kThreads) void sdr_accum_kernel(
     const uint32_t* __restrict__ packets, const gnsscorr_sdr_accum_job* __restrict__ jobs,
@@ -62,164 +47,20 @@ __global__ __launch_bounds__(kThreads) void sdr_accum_kernel(
     gnsscorr_sdr_corr* __restrict__ out) {
   __shared__ int32_t red[kThreads / 64][6];
   const gnsscorr_sdr_accum_job j = jobs[blockIdx.x];
-  const uint32_t* d = packets + (size_t)j.packet * kN + j.data_off;
-  const uint32_t* sn = carrier + (size_t)j.sbin * kRow + j.soff;
-  size_t cb[3];
-#pragma unroll
-  for (int k = 0; k < 3; k++) cb[k] = ((size_t)j.sv * kCBins + j.cbin[k]) * kRow + j.coff[k];
-  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-  // Wave w covers the contiguous samples [1024 w, 1024 w + 1024) of the job,
-  // 64 per step.  The code bits it needs per arm lie in the 33 words from
-  // (cb + 1024 w) >> 5: lane l holds word l of that range (one coalesced load
-  // per arm for the whole job), and each sample's bit comes from its word's
-  // lane by ds_bpermute.
-  static_assert(kThreads == 128 && kN == 2048, "two waves of 1024 samples");
-  const int lane = threadIdx.x & 63, wave0 = (threadIdx.x >> 6) * 1024;
-  const int nend = min(j.samps, wave0 + 1024);
-  uint32_t cw[3];
-  uint32_t sh[3];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const size_t bit0 = cb[k] + (size_t)wave0;
-    sh[k] = (uint32_t)bit0 & 31u;
-    // words 0..32 cover bits up to sh + 1023; a lane loads only a word the
-    // wave's samples reach (an idle wave loads nothing)
-    const int last = ((int)sh[k] + (nend - wave0) - 1) >> 5;
-    cw[k] = (wave0 < nend && lane <= last) ? codebits[(bit0 >> 5) + lane] : 0u;
-  }
-  // all 16 steps' packet and carrier words are loaded before the first is
-  // used (a plain loop waited on memory latency at every step: one load pair
-  // in flight per wave)
-  constexpr int kSteps = 1024 / 64;
-  uint32_t av[kSteps], bv[kSteps];
-#pragma unroll
-  for (int st = 0; st < kSteps; st++) {
-    const int n = wave0 + st * 64 + lane;
-    av[st] = n < nend ? d[n] : 0u;
-    bv[st] = n < nend ? sn[n] : 0u;
-  }
-#pragma unroll
-  for (int st = 0; st < kSteps; st++) {
-    const int n = wave0 + st * 64 + lane;
-    const bool live = n < nend;
-    const uint32_t a = av[st], b = bv[st];
-    const int32_t ai = lo16(a), aq = hi16(a), bi = lo16(b), bq = hi16(b);
-    const int32_t ti = (ai * bi - aq * bq + 8192) >> 14, tq = (ai * bq + aq * bi + 8192) >> 14;
-    int32_t wi = saturate ? sat16(ti) : (int32_t)(int16_t)ti;
-    int32_t wq = saturate ? sat16(tq) : (int32_t)(int16_t)tq;
-    if (!live) wi = wq = 0;
-    const uint32_t rel = (uint32_t)(st * 64 + lane);   // n - wave0 < 1024
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const uint32_t r = rel + sh[k];
-      const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r >> 5) << 2), (int)cw[k]);
-      const int32_t m = (int32_t)((word >> (r & 31u)) & 1u) - 1;   // 0: +code, -1: -code
-      acc[2 * k] += (uint32_t)((wi ^ m) - m);       // A.i * code  (+-1)
-      acc[2 * k + 1] += (uint32_t)((wq ^ m) - m);   // A.q * code
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 6; k++)
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) acc[k] += (uint32_t)__shfl_xor((int)acc[k], o, 64);
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < 6; k++) red[threadIdx.x >> 6][k] = (int32_t)acc[k];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    gnsscorr_sdr_corr r;
-    for (int k = 0; k < 3; k++) {
-      uint32_t si = 0, sq = 0;
-      for (int w = 0; w < kThreads / 64; w++) {
-        si += (uint32_t)red[w][2 * k];
-        sq += (uint32_t)red[w][2 * k + 1];
-      }
-      r.i[k] = (int32_t)si;
-      r.q[k] = (int32_t)sq;
-    }
-    out[blockIdx.x] = r;
-  }
+  const gnsscorr_sdr_corr r =
+      accum_block(j, packets + (size_t)j.packet * kN, carrier, codebits, saturate, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = r;
 }
 
-// ---- host restatement of the Correlator bookkeeping -------------------------
-uint32_t code_bin(double phase) {
-  int32_t b = (int32_t)floor(phase * kCodeBins + 0.5) + kCodeBins / 2;
-  if (b < 0) b = 0;
-  if (b > 2 * kCodeBins) b = 2 * kCodeBins;
-  return (uint32_t)b;
-}
-
-uint32_t carrier_bin(double nco) {
-  int32_t b = (int32_t)floor((nco - kIF) / kCarrSpacing + 0.5) + kCarrBins;
-  if (b < 0) b = 0;
-  if (b > 2 * kCarrBins) b = 2 * kCarrBins;
-  return (uint32_t)b;
-}
-
-void update_state(gnsscorr_sdr_chan* s, int32_t samps) {   // correlator.cpp:369-422
-  s->code_phase += samps * s->code_nco * kInvFs;
-  s->carrier_phase += samps * s->carrier_nco * kInvFs;
-  s->code_phase_mod += samps * s->code_nco * kInvFs;
-  s->carrier_phase_mod += samps * s->carrier_nco * kInvFs;
-  const uint32_t inc = s->code_phase_mod >= 2.0 * 1023.0 ? 2u : (s->code_phase_mod >= 1023.0 ? 1u : 0u);
-  if (inc) {
-    s->epoch_1ms += inc;
-    if (s->epoch_1ms >= 20) {
-      s->epoch_1ms %= 20;
-      if (++s->epoch_20ms >= 300) {
-        s->epoch_20ms = 0;
-        s->z_count += 6;
-        if (s->z_count > 604800.0) s->z_count = 0;
-      }
-    }
-  }
-  s->carrier_phase_mod = fmod(s->carrier_phase_mod, 1.0);
-  s->code_phase_mod = fmod(s->code_phase_mod, 1023);
-  s->rollover -= (uint32_t)samps;
-  s->soff += samps;
-  for (int k = 0; k < 3; k++) s->coff[k] += samps;
-  s->scount += (uint32_t)samps;
-}
-
-void rebin(gnsscorr_sdr_chan* s) {   // tail of DumpAccum, correlator.cpp:497-524
-  const double r = ceil(((double)1023 - s->code_phase_mod) * 2048000.0 / s->code_nco);
-  s->rollover = isfinite(r) ? (uint32_t)(int32_t)r : 0x80000000u;   // (int32)inf on x86
-  s->cbin[0] = code_bin(s->code_phase_mod + 0.5);
-  s->cbin[1] = code_bin(s->code_phase_mod + 0.0);
-  s->cbin[2] = code_bin(s->code_phase_mod - 0.5);
-  s->coff[0] = s->coff[1] = s->coff[2] = 0;
-  s->sbin = carrier_bin(s->carrier_nco);
-  s->soff = 0;
-  s->scount = 0;
-}
-
+// DumpAccum, correlator.cpp:452-525, with the channel callback between the
+// rotation and ProcessFeedback
 void dump(gnsscorr_sdr_chan* s, gnsscorr_sdr_corr* c, int ch, gnsscorr_sdr_dump_fn cb,
-          void* user) {   // DumpAccum, correlator.cpp:452-496
-  // f1 in uint32 arithmetic as the reference (sbin is uint32): wraps below the centre bin
-  const double f1 = (double)((s->sbin - (uint32_t)kCarrBins) * (uint32_t)kCarrSpacing + (uint32_t)kIF);
-  const double fix = 3.141592653589793 * (s->carrier_nco - f1) * (double)s->scount * kInvFs;
-  double ang = s->carrier_phase_prev * 6.283185307179586 + fix;
-  ang = -ang;
-  const double ca = cos(ang), sa = sin(ang);
-  s->carrier_phase_prev = s->carrier_phase_mod;
-  for (int k = 0; k < 3; k++) {
-    const double tI = c->i[k], tQ = c->q[k];
-    c->i[k] = (int32_t)floor(ca * tI - sa * tQ);
-    c->q[k] = (int32_t)floor(sa * tI + ca * tQ);
-  }
+          void* user) {
+  rotate(s, c);
   gnsscorr_sdr_feedback f;
   memset(&f, 0, sizeof f);
   if (cb) cb(user, ch, s, c, &f);
-  s->carrier_nco = f.carrier_nco;   // ProcessFeedback, correlator.cpp:530-555
-  s->code_nco = f.code_nco;
-  s->navigate = f.navigate;
-  if (f.reset_1ms) s->epoch_1ms = 0;
-  if (f.reset_20ms) s->epoch_20ms = 60;
-  if (f.set_z_count) s->z_count = f.z_count;
-  if (f.kill) memset(s, 0, sizeof *s);
-  s->count++;
-  memset(c, 0, sizeof *c);
-  rebin(s);
+  after_feedback(s, c, f);
 }
 
 }  // namespace
@@ -334,23 +175,6 @@ extern "C" int gnsscorr_sdr_init_chan(gnsscorr_sdr_chan* s, int sv, int acq_code
   return GNSSCORR_OK;
 }
 
-static bool job_in_range(const gnsscorr_sdr_accum_job& j, int n_packets) {
-  if (j.samps < 0 || j.samps > kN || j.data_off < 0 || j.data_off + j.samps > kN ||
-      j.packet < 0 || j.packet >= n_packets || j.sv < 0 || j.sv >= kSV || j.sbin < 0 ||
-      j.sbin >= kSBins)
-    return false;
-  // the reference reads rows through raw pointers: allow running into the next
-  // row, but not past the whole table
-  const long long send = (long long)j.sbin * kRow + j.soff + j.samps;
-  if (j.soff < 0 || send > (long long)kSBins * kRow) return false;
-  for (int k = 0; k < 3; k++) {
-    if (j.cbin[k] < 0 || j.cbin[k] >= kCBins || j.coff[k] < 0) return false;
-    const long long cend = ((long long)j.sv * kCBins + j.cbin[k]) * kRow + j.coff[k] + j.samps;
-    if (cend > (long long)kSV * kCBins * kRow) return false;
-  }
-  return true;
-}
-
 extern "C" int gnsscorr_sdr_accum_dev(gnsscorr_sdr_corr_ctx* c, const int16_t* d_packets,
                                       int n_jobs, const gnsscorr_sdr_accum_job* d_jobs,
                                       gnsscorr_sdr_corr* d_out) {
@@ -426,13 +250,7 @@ extern "C" int gnsscorr_sdr_correlate(gnsscorr_sdr_corr_ctx* c, const int16_t* h
       job_of[ch] = -1;
       if (samps > 0) {
         gnsscorr_sdr_accum_job& j = c->h_jobs[nj];
-        j.packet = h_rx ? h_rx[ch] : 0;
-        j.data_off = off[ch];
-        j.samps = samps;
-        j.sv = (int32_t)s->sv;
-        j.sbin = (int32_t)s->sbin;
-        j.soff = s->soff;
-        for (int k = 0; k < 3; k++) { j.cbin[k] = (int32_t)s->cbin[k]; j.coff[k] = s->coff[k]; }
+        j = make_job(*s, h_rx ? h_rx[ch] : 0, off[ch], samps);
         if (!job_in_range(j, n_packets)) {
           gnsscorr_set_error("gnsscorr_sdr_correlate: channel %d state out of the tables "
                              "(sv %d sbin %d soff %d)", ch, j.sv, j.sbin, j.soff);
@@ -476,6 +294,13 @@ extern "C" int gnsscorr_sdr_correlate(gnsscorr_sdr_corr_ctx* c, const int16_t* h
     if (!more) break;
   }
   return GNSSCORR_OK;
+}
+
+extern "C" void gnsscorr_sdr_corr_tables(const gnsscorr_sdr_corr_ctx* c, const uint32_t** carrier,
+                                         const uint32_t** codebits, int* saturate) {
+  *carrier = c->d_carrier;
+  *codebits = c->d_codebits;
+  *saturate = c->cfg.saturate;
 }
 
 extern "C" int gnsscorr_sdr_corr_sync(gnsscorr_sdr_corr_ctx* c) {

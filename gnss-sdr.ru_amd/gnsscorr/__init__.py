@@ -106,6 +106,9 @@ SDR_FEEDBACK = np.dtype([("carrier_nco", "<f8"), ("code_nco", "<f8"), ("kill", "
                          ("reset_1ms", "<u4"), ("reset_20ms", "<u4"), ("set_z_count", "<u4"),
                          ("z_count", "<u4"), ("length", "<u4"), ("navigate", "<u4"),
                          ("pad", "<u4")])
+SDR_DUMP_REC = np.dtype([("packet", "<i4"), ("phase", "<i4"), ("corr", SDR_CORR),
+                         ("fb", SDR_FEEDBACK)])
+assert SDR_DUMP_REC.itemsize == 80
 assert SDR_CHANNEL_CORE.itemsize == 584 and SDR_CHANNEL.itemsize == 2632
 assert SDR_SUBFRAME.itemsize == 64 and SDR_FEEDBACK.itemsize == 48
 SDR_ACQ_STRONG, SDR_ACQ_MEDIUM, SDR_ACQ_WEAK = 0, 1, 2   # ACQ_TYPE_* (acquisition.cpp:584-599)
@@ -170,7 +173,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_sgt_stream",
     "gnsscorr_sdr_prn_codes", "gnsscorr_sdr_sine_gen", "gnsscorr_sdr_acq_create",
     "gnsscorr_sdr_acq_destroy", "gnsscorr_sdr_acq_strong", "gnsscorr_sdr_acq_strong_dev",
-    "gnsscorr_sdr_channel_start", "gnsscorr_sdr_channel_accum_dev",
+    "gnsscorr_sdr_channel_start", "gnsscorr_sdr_channel_accum_dev", "gnsscorr_sdr_track_dev",
     "gnsscorr_sdr_acq_sync", "gnsscorr_sdr_acq_stream", "gnsscorr_sdr_acq_prep_dev",
     "gnsscorr_sdr_acq_search_dev", "gnsscorr_sdr_acq_acquire",
     "gnsscorr_sdr_corr_create", "gnsscorr_sdr_corr_destroy", "gnsscorr_sdr_init_chan",
@@ -259,6 +262,7 @@ def lib() -> C.CDLL:
         "gnsscorr_sdr_acq_prep_dev": (I, [P, I, P, I]),
         "gnsscorr_sdr_channel_start": (I, [P, I, I, I, I]),
         "gnsscorr_sdr_channel_accum_dev": (I, [P, I, I, P, P, P, P, P, I, P]),
+        "gnsscorr_sdr_track_dev": (I, [P, P, I, I, I, P, P, P, P, P, P, I, P, P, P, I, P]),
         "gnsscorr_sdr_acq_search_dev": (I, [P, I, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_acquire": (I, [P, I, P, I, I, P, I, I, P]),
         "gnsscorr_sdr_acq_stream": (P, [P]),
@@ -988,6 +992,58 @@ class SdrCorrCtx:
         else:
             fb = d_last.download(np.uint8).view(SDR_FEEDBACK)
         return fb, ev, n
+
+    def track_dev(self, d_packets, n_packets, n_rx, n_ch, d_rx, d_states, d_corr, d_chans,
+                  d_fb_last, d_log, log_per_ch, d_n_log, d_status, d_events, max_events,
+                  d_n_events):
+        _check(lib().gnsscorr_sdr_track_dev(self.h, d_packets, n_packets, n_rx, n_ch, d_rx,
+                                            d_states, d_corr, d_chans, d_fb_last, d_log,
+                                            log_per_ch, d_n_log, d_status, d_events, max_events,
+                                            d_n_events), "gnsscorr_sdr_track_dev")
+
+    def track(self, packets, states, corr, chans, rx=None, log_per_ch=0, max_events=4096):
+        """The closed loop on the device: packets (n_packets, n_rx, 2048, 2) int16;
+        states SDR_CHAN[n_ch], corr SDR_CORR[n_ch], chans SDR_CHANNEL[n_ch] updated in
+        place (chans[c] steers states[c]).  Returns dict(fb_last, log SDR_DUMP_REC
+        [n_ch, log_per_ch], n_log, status, events sorted by (ms = packet, chan)).
+        Raises when a channel's state left the tables (status != 0)."""
+        pk = np.ascontiguousarray(packets, np.int16)
+        n_packets, n_rx = pk.shape[0], pk.shape[1]
+        assert pk.shape[2:] == (2048, 2), pk.shape
+        n_ch = len(states)
+        assert states.dtype == SDR_CHAN and corr.dtype == SDR_CORR and chans.dtype == SDR_CHANNEL
+        assert len(corr) == n_ch and len(chans) == n_ch
+        dev = self.device
+        d_pk = DevBuf.from_array(pk, dev)
+        d_rx = None if rx is None else DevBuf.from_array(np.ascontiguousarray(rx, np.int32), dev)
+        d_st, d_c, d_ch = (DevBuf.from_array(a, dev) for a in (states, corr, chans))
+        d_last = DevBuf.from_array(np.zeros(n_ch, SDR_FEEDBACK), dev)
+        d_log = DevBuf(max(n_ch * log_per_ch, 1) * SDR_DUMP_REC.itemsize, dev)
+        d_nlog = DevBuf.from_array(np.zeros(n_ch, np.int32), dev)
+        d_stat = DevBuf.from_array(np.zeros(n_ch, np.int32), dev)
+        d_ev = DevBuf(max(max_events, 1) * SDR_SUBFRAME.itemsize, dev)
+        d_n = DevBuf.from_array(np.zeros(1, np.int32), dev)
+        self.track_dev(d_pk.ptr, n_packets, n_rx, n_ch, None if d_rx is None else d_rx.ptr,
+                       d_st.ptr, d_c.ptr, d_ch.ptr, d_last.ptr, d_log.ptr, log_per_ch,
+                       d_nlog.ptr, d_stat.ptr, d_ev.ptr, max_events, d_n.ptr)
+        self.sync()
+        status = d_stat.download(np.int32)[:n_ch]
+        states[:] = d_st.download(np.uint8).view(SDR_CHAN)
+        corr[:] = d_c.download(np.uint8).view(SDR_CORR)
+        chans[:] = d_ch.download(np.uint8).view(SDR_CHANNEL)
+        if np.any(status != 0):
+            c = int(np.flatnonzero(status)[0])
+            raise GnssCorrError(f"sdr track: channel {c} stopped (status {int(status[c])}: "
+                                "-1 bad receiver index, 1+p state out of the tables at packet p)")
+        n = int(d_n.download(np.int32)[0])
+        if n > max_events:
+            raise GnssCorrError(f"sdr track: {n} subframes exceed max_events={max_events}")
+        ev = d_ev.download(np.uint8).view(SDR_SUBFRAME)[:n]
+        ev = ev[np.lexsort((ev["chan"], ev["ms"]))]
+        log = d_log.download(np.uint8).view(SDR_DUMP_REC)[:n_ch * log_per_ch]
+        return dict(fb_last=d_last.download(np.uint8).view(SDR_FEEDBACK),
+                    log=log.reshape(n_ch, log_per_ch), n_log=d_nlog.download(np.int32)[:n_ch],
+                    status=status, events=ev)
 
     def accum_dev(self, d_packets, n_jobs, d_jobs, d_out):
         _check(lib().gnsscorr_sdr_accum_dev(self.h, d_packets, n_jobs, d_jobs, d_out),

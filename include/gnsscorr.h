@@ -640,6 +640,35 @@ int gnsscorr_sdr_channel_accum_dev(gnsscorr_sdr_corr_ctx *ctx, int n_ch, int n_m
                                    gnsscorr_sdr_subframe *d_events, int max_events,
                                    int32_t *d_n_events);
 
+/* Device-resident closed loop: Correlator::Correlate
+ * (correlator.cpp:160-237) over n_packets consecutive packets, with
+ * UpdateState, DumpAccum and Channel::Accum + ProcessFeedback (:452-555) at
+ * every dump, without a host round trip -- channel c's Channel object d_ch[c]
+ * steers correlator d_states[c].  One workgroup per channel.
+ * d_packets: n_packets x n_rx x 2048 CPX (packet-major); channel c reads
+ * receiver d_rx[c] (NULL: 0).  d_states / d_corr / d_ch: n_ch entries,
+ * updated in place.  d_fb_last[c] (optional): the last dump's feedback.
+ * d_log (optional): log_per_ch records per channel (channel-major), the first
+ * log_per_ch dumps; d_n_log[c] (optional) counts all of channel c's dumps.
+ * d_status[c]: 0; 1 + p when the state left the tables at packet p (the
+ * channel stops there -- the host path returns GNSSCORR_EINVAL instead);
+ * -1 for a receiver index outside 0..n_rx-1.  Subframe events as in
+ * gnsscorr_sdr_channel_accum_dev with ms = the packet index.  Bit-identical
+ * to gnsscorr_sdr_correlate packet by packet with gnsscorr_sdr_channel_accum_dev
+ * as the dump callback.  Async on the context stream. */
+typedef struct {
+  int32_t packet, phase;          /* packet index and segment phase (0..2) of the dump */
+  gnsscorr_sdr_corr corr;         /* rotated correlations handed to Channel::Accum    */
+  gnsscorr_sdr_feedback fb;       /* the NCO_Command_S it returned                    */
+} gnsscorr_sdr_dump_rec;          /* 80 bytes */
+int gnsscorr_sdr_track_dev(gnsscorr_sdr_corr_ctx *ctx, const int16_t *d_packets, int n_packets,
+                           int n_rx, int n_ch, const int32_t *d_rx, gnsscorr_sdr_chan *d_states,
+                           gnsscorr_sdr_corr *d_corr, gnsscorr_sdr_channel *d_ch,
+                           gnsscorr_sdr_feedback *d_fb_last, gnsscorr_sdr_dump_rec *d_log,
+                           int log_per_ch, int32_t *d_n_log, int32_t *d_status,
+                           gnsscorr_sdr_subframe *d_events, int max_events,
+                           int32_t *d_n_events);
+
 /* ======================================================================
  * GPS-SDR sample front end, bit-exact with
  *   GPS_Source::Read_GN3S   objects/gps_source.cpp:684-767 (2-bit LUT {-3,-1,1,3},
