@@ -479,7 +479,7 @@ __device__ __forceinline__ void lds_read_fence() { __builtin_amdgcn_sched_barrie
 struct NoHook {
   __device__ void operator()() const {}
 };
-template <class P, class Hook = NoHook, bool kStage3 = true>
+template <class P, class Hook = NoHook, bool kStage3 = true, bool kPinStage1 = false>
 __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
                                          const v2d* __restrict__ twN, int t,
                                          v2d (&v1)[P::K1][P::R1], v2d (&v3)[P::K3][P::R3],
@@ -494,6 +494,15 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       const int g = P::group1(t, j);
       if (g >= 0) twiddle_run<R1>(v1[j], twN[g]);
     }
+  }
+  if constexpr (kPinStage1) {
+    // stage 1 completes before the hook: its results pass through empty asm
+    // statements, the hook's loads stay behind a compiler memory barrier
+#pragma unroll
+    for (int j = 0; j < P::K1; j++)
+#pragma unroll
+      for (int k = 0; k < R1; k++) asm volatile("" : "+v"(v1[j][k].x), "+v"(v1[j][k].y));
+    asm volatile("" ::: "memory");
   }
   before_exchange();   // the caller may still use the LDS up to here
   // ---- exchange 1: re then im
@@ -906,11 +915,18 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     int gpr, int nbT) {
   constexpr int N = P::N, R1 = P::R1, R3 = P::R3, T = P::T, K3 = P::K3, L = P::L;
   constexpr bool kNC = MODE == GNSSCORR_ACQ_NONCOHERENT;
-  __shared__ double lds[N];
+  // non-coherent: a thread's first kE running sums live in the LDS left over
+  // beside the exchange plane for the whole row (the others are parked in the
+  // plane between blocks, see start_sums)
+  constexpr int kLdsOther = N * 8 + P::LS * 16 + R3 * 16 + P::NW * 20 + 256;
+  constexpr int kE0 = kNC ? (163840 - kLdsOther) / (8 * T) : 0;
+  constexpr int kE = kE0 < K3 * R3 ? kE0 : K3 * R3;
+  __shared__ double lds[N + kE * T];   // the exchange plane, then s_extra
   __shared__ v2d side[P::LS];
   __shared__ v2d tw3[R3];
   __shared__ double s_v[P::NW], s_m[P::NW];
   __shared__ int s_k[P::NW];
+  double* const s_extra = lds + N;
   const int t = threadIdx.x;
   const bool act = t < T;
   init_tw3<P>(tw3);
@@ -1003,24 +1019,44 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
       }
     }
     v2d v3[K3][R3], vl[2] = {(v2d){0.0, 0.0}, (v2d){0.0, 0.0}};
-    // non-coherent: the running sums start at zero in the first block (the
-    // compiler spills them around the load phase, where registers are scarcest)
+    // non-coherent: the running sums are parked in the LDS between blocks
+    // (stored after a block's stage 3, when the exchange plane is idle) and
+    // come back after this block's stage 1, just before the exchange needs the
+    // plane: they are not live across the load phase, whose in-flight X / F
+    // loads take the registers (held in registers, they were spilled there).
     auto start_sums = [&]() {
       if constexpr (kNC) {
-        if (i == 0) {
+        // branch-free (a branch here lets the compiler sink stage 1 below the
+        // reads, back into the load phase); at i == 0 the plane's content is
+        // read but not used
+        const bool first = i == 0;
+        const int tt = min(t, T - 1);
 #pragma unroll
-          for (int j = 0; j < K3; j++)
+        for (int j = 0; j < K3; j++)
 #pragma unroll
-            for (int k = 0; k < R3; k++) pw[j][k] = 0.0;
-          pwl[0] = P::lvalid(t, 0) ? 0.0 : -1.0;
-          pwl[1] = P::lvalid(t, 1) ? 0.0 : -1.0;
-        }
+          for (int k = 0; k < R3; k++) {
+            if (j * R3 + k < kE) continue;   // in s_extra: read just before stage 3
+            const double v = lds[(j * R3 + k) * T + tt];
+            pw[j][k] = first ? 0.0 : v;
+          }
+        pwl[0] = first ? (P::lvalid(t, 0) ? 0.0 : -1.0) : pwl[0];
+        pwl[1] = first ? (P::lvalid(t, 1) ? 0.0 : -1.0) : pwl[1];
+        __syncthreads();   // exchange 1 overwrites the parked sums
       }
     };
     // |.|^2 / N^2 (|ifft(Y)|^2 = |fft(conj Y)|^2 / N^2); a prime radix-R3
     // stage is fused with the powers
     constexpr bool kFuse = is_prime(R3);
-    fft_core<P, decltype(start_sums), !kFuse>(lds, side, tw3, twN, t, v1, v3, vl, start_sums);
+    fft_core<P, decltype(start_sums), !kFuse, kNC>(lds, side, tw3, twN, t, v1, v3, vl,
+                                                   start_sums);
+    if constexpr (kE > 0) {
+      const int tt = min(t, T - 1);
+#pragma unroll
+      for (int f = 0; f < kE; f++) {
+        const double v = s_extra[f * T + tt];
+        pw[f / R3][f % R3] = i == 0 ? 0.0 : v;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < K3; j++) {
       if constexpr (kFuse) {
@@ -1064,7 +1100,20 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
           }
       }
     }
-
+    if constexpr (kNC) {
+      // park the sums (exchange 2's reads ended with a barrier: the plane is idle)
+      static_assert(K3 * R3 * T <= N, "parked sums fit the exchange plane");
+      if (i + 1 < nblk && act) {
+#pragma unroll
+        for (int j = 0; j < K3; j++)
+#pragma unroll
+          for (int k = 0; k < R3; k++) {
+            const int f = j * R3 + k;
+            if (f < kE) s_extra[f * T + t] = pw[j][k];
+            else lds[f * T + t] = pw[j][k];
+          }
+      }
+    }
   }
   // ---- row statistics.  Per stage-3 group, the thread's outputs lie
   // SPACING = N/R3 samples apart, so an exclusion window narrower than that
