@@ -23,6 +23,7 @@
 //
 // Roofline: fp64 VALU (~27 DP ops per sample); HBM is 2 B/sample.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -77,7 +78,9 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
     const uint32_t* __restrict__ codes, gnsscorr_sgt_chan* __restrict__ chans, int n_epochs,
     gnsscorr_sgt_epoch* __restrict__ out) {
 #pragma clang fp contract(off)
-  __shared__ double s_sgn[kPadLen];   // the code as +-1.0: E/P/L accumulate with one fma
+  // the code as +-1.0 (E/P/L accumulate with one fma), L + 2 entries: dynamic,
+  // so a 511-chip GLONASS table takes 4.1 KB, not the 1023-chip maximum
+  extern __shared__ double s_sgn[];
   __shared__ double s_part[2][kMaxWaves][6];
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
   const int T = WAVE ? 64 : blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -135,11 +138,23 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
       if (FT == 2) return *reinterpret_cast<const uint16_t*>(src + 2 * k);
       return src[k];
     };
+    // Every code index lies in [0, L+1] (the padded table) when remCode >= spc - 1
+    // (aE > -1) and spc < 0.99: blksize = ceil((L - remCode)/step) keeps
+    // (blksize-1)*step below L - remCode up to rounding, so aL + t < L + 1.  The
+    // loop keeps remCode in [0, step); only a state set from outside can fail
+    // the test, and then the indices are clamped into the table (kClamp).
+    const bool in_table = c.rem_code >= p.spc - 1.0 && p.spc >= 0.0 && p.spc < 0.99;
+    auto run = [&](auto clamp_tag) {
+    constexpr bool kClamp = decltype(clamp_tag)::value;
+    auto index = [&](double x) {
+      const int i = (int)ceil(x);
+      return kClamp ? clampu(i, L + 1) : i;
+    };
     auto sample = [&](int k, int w) {
       const double t = (double)k * step;
-      const double gE = s_sgn[clampu((int)ceil(aE + t), L + 1)];
-      const double gP = s_sgn[clampu((int)ceil(aP + t), L + 1)];
-      const double gL = s_sgn[clampu((int)ceil(aL + t), L + 1)];
+      const double gE = s_sgn[index(aE + t)];
+      const double gP = s_sgn[index(aP + t)];
+      const double gL = s_sgn[index(aL + t)];
       double re, im;
       if (FT == 2) {
         re = (double)(int)__builtin_amdgcn_sbfe(w, sh_re, 8);   // (the builtin is typed unsigned)
@@ -187,6 +202,11 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
       const int k = k0 + u * T;
       if (k < blk) sample(k, w[u]);
     }
+    };
+    if (in_table)
+      run(std::false_type{});
+    else
+      run(std::true_type{});
     ie = wave_sum(ie); ip = wave_sum(ip); il = wave_sum(il);
     qe = wave_sum(qe); qp = wave_sum(qp); ql = wave_sum(ql);
     double S[6] = {ie, ip, il, qe, qp, ql};
@@ -418,13 +438,14 @@ extern "C" int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx* c, const int8_t* d_if, i
     if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) T = v;
   }
   dim3 grid(n_ch), block(T);
+  const size_t tab = (size_t)(c->p.code_length + 2) * sizeof(double);   // s_sgn
 #define SGT_LAUNCH(FT, CL)                                                                     \
   do {                                                                                         \
     if (T == 64)                                                                               \
-      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, true>), grid, block, 0, c->stream, c->p,   \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, true>), grid, block, tab, c->stream, c->p, \
                          d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
     else                                                                                       \
-      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, false>), grid, block, 0, c->stream, c->p,  \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, false>), grid, block, tab, c->stream, c->p, \
                          d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
   } while (0)
   if (c->cfg.file_type == 2) {
