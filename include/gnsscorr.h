@@ -127,10 +127,11 @@ typedef struct {
 
 int gnsscorr_track_create(gnsscorr_track_ctx **out, const gnsscorr_track_cfg *cfg);
 int gnsscorr_track_destroy(gnsscorr_track_ctx *ctx);
-/* Layout hint: one_stream_per_channel = 1 when no two channels of the context
- * share an IF stream (C_s = 1); int8 streams are then staged per channel in
- * LDS (faster there, slower for receivers whose channels share a stream).
- * 0 restores the default.  Results are identical either way. */
+/* Layout hint (kept for source compatibility, since 0.2.0 a validated no-op):
+ * the kernel picks the load path per workgroup from the channels' streams --
+ * receivers (channels sharing a stream) stage the stream once in LDS, channels
+ * on distinct streams take the per-wave piece path -- so no hint is needed.
+ * Returns GNSSCORR_EINVAL for a NULL context or a value other than 0 / 1. */
 int gnsscorr_track_set_layout(gnsscorr_track_ctx *ctx, int one_stream_per_channel);
 /* Max dumps one call can produce: floor(max_nsamp/2046)+2.  The optional
  * all-dumps buffer of gnsscorr_track() is n_channels * this * 6 int32. */
