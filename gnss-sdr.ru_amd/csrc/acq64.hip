@@ -1297,33 +1297,36 @@ int corr_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_units, int n_
 // Generic N (any other samplesPerCode, e.g. acquisition.sci at fs = 5 or 38.192 MHz):
 // the same fp64 pipeline with every length-N DFT done by Bluestein's chirp-z
 // identity  X_k = c_k sum_n (a_n c_n) conj(c_{k-n}),  c_n = exp(-i pi n^2 / N),
-// i.e. a cyclic convolution of length M = 16^P >= 2N - 1 through two radix-16
-// Stockham FFTs in global memory.  A fallback for sizes without a compiled
-// plan: correct to fp64 rounding, not tuned.
+// i.e. a cyclic convolution of length M = 2^q >= 2N - 1 (radix-16 Stockham
+// passes in global memory, the last one radix 2, 4 or 8 when q is not a
+// multiple of 4).  A fallback for sizes without a compiled plan: correct to
+// fp64 rounding, not tuned.
 // ==================================================================================
 namespace {
 
 constexpr int kGThreads = 256;
 
-// one radix-16 Stockham pass (autosort), forward: Ns = 16^p
+// one radix-R Stockham pass (autosort), forward: Ns = product of the earlier
+// passes' radices
+template <int R>
 __global__ __launch_bounds__(kGThreads) void g_fft_pass(const v2d* __restrict__ in,
                                                         v2d* __restrict__ out, int M, int Ns,
                                                         const v2d* __restrict__ twM) {
-  const int j = blockIdx.x * kGThreads + threadIdx.x;   // < M / 16
+  const int j = blockIdx.x * kGThreads + threadIdx.x;   // < M / R
   const long row = (long)blockIdx.y * M;
-  if (j >= M / 16) return;
+  if (j >= M / R) return;
   const int k = j & (Ns - 1);
-  const int tstep = k * (M / (16 * Ns));                  // twiddle W_M^(r * tstep)
-  v2d v[16];
+  const int tstep = k * (M / (R * Ns));                   // twiddle W_M^(r * tstep)
+  v2d v[R];
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const v2d x = in[row + j + r * (M / 16)];
+  for (int r = 0; r < R; r++) {
+    const v2d x = in[row + j + r * (M / R)];
     v[r] = r == 0 ? x : cmul(x, twM[(r * tstep) & (M - 1)]);
   }
-  dft<16>(v);
-  const int d = (j / Ns) * Ns * 16 + k;
+  dft<R>(v);
+  const int d = (j / Ns) * Ns * R + k;
 #pragma unroll
-  for (int r = 0; r < 16; r++) out[row + d + r * Ns] = v[r];
+  for (int r = 0; r < R; r++) out[row + d + r * Ns] = v[r];
 }
 
 // A[row] = (a_n c_n | 0...) from natural rows a (stride src_rs)
@@ -1473,10 +1476,21 @@ __global__ __launch_bounds__(256) void g_codes_kernel(const int8_t* __restrict__
 int g_fft(gnsscorr_acq_ctx* c, v2d* A, v2d* B, int rows, v2d** res) {
   const int M = c->gM;
   v2d *in = A, *out = B;
-  for (int p = 0, Ns = 1; p < c->gP; p++, Ns *= 16) {
-    hipLaunchKernelGGL(g_fft_pass, dim3((M / 16 + kGThreads - 1) / kGThreads, rows),
-                       dim3(kGThreads), 0, c->stream, in, out, M, Ns, (const v2d*)c->d_twM);
+  int Ns = 1;
+  while (Ns < M) {
+    const int R = M / Ns >= 16 ? 16 : M / Ns;   // radix-16 passes, then one of 2, 4 or 8
+    const dim3 grid((M / R + kGThreads - 1) / kGThreads, rows);
+    const v2d* tw = (const v2d*)c->d_twM;
+    if (R == 16)
+      hipLaunchKernelGGL(g_fft_pass<16>, grid, dim3(kGThreads), 0, c->stream, in, out, M, Ns, tw);
+    else if (R == 8)
+      hipLaunchKernelGGL(g_fft_pass<8>, grid, dim3(kGThreads), 0, c->stream, in, out, M, Ns, tw);
+    else if (R == 4)
+      hipLaunchKernelGGL(g_fft_pass<4>, grid, dim3(kGThreads), 0, c->stream, in, out, M, Ns, tw);
+    else
+      hipLaunchKernelGGL(g_fft_pass<2>, grid, dim3(kGThreads), 0, c->stream, in, out, M, Ns, tw);
     HIP_TRY(hipGetLastError());
+    Ns *= R;
     v2d* t = in;
     in = out;
     out = t;
@@ -1512,8 +1526,9 @@ int g_dft_rows(gnsscorr_acq_ctx* c, const v2d* a, int src_rs, int rows, v2d* out
 
 int g_init(gnsscorr_acq_ctx* c) {
   const long N = c->cfg.n_samples;
-  int M = 16, P = 1;
-  while (M < 2 * N - 1) { M *= 16; P++; }
+  int M = 16, P = 0;   // P: passes (radix 16, the last possibly 2 / 4 / 8)
+  while (M < 2 * N - 1) M *= 2;
+  for (int m = 1; m < M; m *= 16) P++;
   c->gM = M;
   c->gP = P;
   // chunk: ~64 MiB per work buffer

@@ -478,10 +478,13 @@ __global__ __launch_bounds__(64) void sdr_channel_kernel(
     gnsscorr_sdr_feedback* __restrict__ fb, gnsscorr_sdr_feedback* __restrict__ fb_last,
     gnsscorr_sdr_subframe* __restrict__ ev, int max_ev, int32_t* __restrict__ n_ev,
     Twiddles tw) {
+  // each thread's copy of its Channel object but the FFT buffer, in LDS (not
+  // scratch: the serial channel code is a chain of dependent field accesses)
+  __shared__ __attribute__((aligned(16))) unsigned char s_obj[64][offsetof(Chan, fft_buff)];
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= n_ch) return;
   Chan& g = chans[ch];
-  Chan s;   // private copy of everything but the FFT buffer
+  Chan& s = *reinterpret_cast<Chan*>(s_obj[threadIdx.x]);   // fields before fft_buff only
   memcpy(&s, &g, offsetof(Chan, fft_buff));
   Events e = {ev, max_ev, n_ev, ch, 0};
   gnsscorr_sdr_feedback f = {};
@@ -517,7 +520,9 @@ __global__ __launch_bounds__(sdrc::kThreads) void sdr_track_kernel(
   __shared__ int32_t red[kThreads / 64][6];
   const int ch = blockIdx.x;
   const bool t0 = threadIdx.x == 0;
-  Chan cs;   // thread 0's copy of the Channel object but its FFT buffer
+  __shared__ Chan cs;   // thread 0's copy of the Channel object (its FFT buffer unused: the
+                        // one in HBM is used); LDS, not scratch: the serial channel
+                        // code is a chain of dependent field accesses
   gnsscorr_sdr_feedback f = {};
   int32_t ndump = 0, stat = 0;
   const int r = rx ? rx[ch] : 0;

@@ -822,8 +822,10 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   // cpw channels; channels of a workgroup on different streams (one stream
   // per channel, receivers split over workgroups) take the per-wave piece
   // path (run_pieces: coalesced 1 KiB wave loads, no workgroup barrier)
-  const bool shared_stage = IQ && stage_ok && uni && sst >= 0;
-  const bool pieces = IQ && stage_ok == 1 && !shared_stage;   // 3: A/B, round-2 lane reads
+  // (stage_ok 3: A/B, round-2 lane reads for mixed streams; 4: A/B, the piece
+  // path for every workgroup)
+  const bool shared_stage = IQ && stage_ok && stage_ok != 4 && uni && sst >= 0;
+  const bool pieces = IQ && (stage_ok == 1 || stage_ok == 4) && !shared_stage;
   const bool stage = shared_stage;
   uint4* s_ifq = s_if;
   if (stage) {
@@ -1046,6 +1048,7 @@ struct gnsscorr_track_ctx {
   int64_t tic = 0, tic_ref = 0;
   int stage_if = 1;   // GNSSCORR_TRACK_STAGE_IF=0: lanes read their IF runs from global memory
   int cpw_override = 0;   // GNSSCORR_TRACK_CPW: channels per workgroup
+  int pieces_all = 0;     // GNSSCORR_TRACK_PIECES=1: the piece path for receivers too (A/B)
   int v1 = 0;             // GNSSCORR_TRACK_V1=1: workgroups whose channels read different
                           // streams use the round-2 per-lane global reads, not the piece path (A/B)
   size_t lds_max = 0;     // LDS bytes a workgroup may allocate (gnsscorr_device_lds_bytes)
@@ -1092,6 +1095,7 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   if (const char* e = getenv("GNSSCORR_TRACK_STAGE_IF")) c->stage_if = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_CPW")) c->cpw_override = atoi(e);
   if (const char* e = getenv("GNSSCORR_TRACK_V1")) c->v1 = atoi(e) != 0;
+  if (const char* e = getenv("GNSSCORR_TRACK_PIECES")) c->pieces_all = atoi(e) != 0;
   const int C = cfg->n_channels;
   auto fail = [&](int code) {
     gnsscorr_track_destroy(c);
@@ -1185,6 +1189,7 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   const size_t stage_bytes = (size_t)((nsamp + kRun - 1) / kRun) * kPitch * 16;
   int stage = iq && c->stage_if && stage_bytes <= (size_t)kStageMaxBytes;
   if (stage && c->v1) stage = 3;
+  if (stage && c->pieces_all) stage = 4;
   // dynamic LDS: epoch sums, E/P/L row bytes, then one region that holds either
   // the workgroup's shared IF stage or the waves' 4 KiB piece slots
   auto lds_bytes = [&](int cpw) {

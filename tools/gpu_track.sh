@@ -11,10 +11,11 @@ echo "== tracking parity tests"
   tests/test_track_gpu.py tests/test_packed_gpu.py tests/test_e2e_gpu.py tests/test_osg_loops_gpu.py \
   tests/test_trackshard_gpu.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 [ -n "${SKIP_TESTS:-}" ] || tail -2 $O/pytest.log
-for V in 0 1 0 1; do
-  echo "== bench track / track_io, GNSSCORR_TRACK_V$V=1 (V0: default)"
-  env GNSSCORR_TRACK_V$V=1 timeout -k 10 200 python3 tools/bench_part.py track 20 > $O/track_v$V.json
-  env GNSSCORR_TRACK_V$V=1 timeout -k 10 200 python3 tools/bench_part.py track_io 20 > $O/track_io_v$V.json
+# TRK_VARIANTS: GNSSCORR_TRACK_<name>=1 per run (V0: no such switch, the default)
+for V in ${TRK_VARIANTS:-V0 V1 V0 V1}; do
+  echo "== bench track / track_io, GNSSCORR_TRACK_$V=1 (V0: default)"
+  env GNSSCORR_TRACK_$V=1 timeout -k 10 200 python3 tools/bench_part.py track 20 > $O/track_v$V.json
+  env GNSSCORR_TRACK_$V=1 timeout -k 10 200 python3 tools/bench_part.py track_io 20 > $O/track_io_v$V.json
   python3 - $O/track_v$V.json $O/track_io_v$V.json <<'PY'
 import json, sys
 a = json.load(open(sys.argv[1])); b = json.load(open(sys.argv[2]))
