@@ -173,10 +173,11 @@ def run_acq_generic(dist, dev, steps, warmup, fs=GENERIC_FS):
     """Config 2's search at a rate without a compiled plan: the fp64 Bluestein engine
     (every length-N DFT as a cyclic convolution of length 2^q >= 2N - 1)."""
     n = int(round(fs / 1000.0))
+    spc = int(round(fs / 1.023e6))   # samplesPerCodeChip (GPS/L1/acquisition.sci:147), the exclusion window
     rng = np.random.default_rng(300 + dist.rank)
     planted = rng.choice(np.arange(1, 33), 8, replace=False)
     sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
-                 doppler=float(rng.uniform(-5000, 5000)), cn0=52.0, data_bits=1) for p in planted]
+                 doppler=float(rng.uniform(-5000, 5000)), cn0=49.0, data_bits=1) for p in planted]
     IF = gc.ifgen(N_BLK * n, sigs, fs=fs, seed=0x5EED0030 + dist.rank)
     codes = np.stack([gc.sample_code(gc.ca_code(p), 1.023e6, fs, n) for p in range(1, 33)])
     freqs = 2.42e6 - 10000.0 + 500.0 * np.arange(N_BINS)
@@ -191,7 +192,7 @@ def run_acq_generic(dist, dev, steps, warmup, fs=GENERIC_FS):
     def step():
         ctx.spectra_dev(b["d_if"].ptr, N_BLK, N_BINS, b["d_freqs"].ptr)
         ctx.correlate_dev(N_BLK, b["d_freqs"].ptr, N_PRN, N_BINS, b["d_gcode"].ptr,
-                          b["d_gfreq"].ptr)
+                          b["d_gfreq"].ptr, spc=spc)
         ctx.select_dev(N_PRN, N_BINS, b["d_freqs"].ptr, b["d_gfreq"].ptr, b["d_rows"].ptr,
                        b["d_res"].ptr)
 
