@@ -41,15 +41,95 @@ namespace {
 
 using namespace sdrc;
 
+// One Accum job per workgroup.  The same computation as sdrc::accum_block (the
+// device-resident loop's segment, sdr_channel.hip), written out here: through
+// the shared function the compiler schedules more loads in flight for this
+// kernel (73 instead of 50 VGPRs, 6 instead of 8 waves per SIMD), and 4096 jobs
+// take 17.5 instead of 15.2 us (same-box A/B).  test_sdr_track_gpu.py checks the
+// two bit for bit (the loop against the host schedule, which launches this).
 __global__ __launch_bounds__(kThreads) void sdr_accum_kernel(
     const uint32_t* __restrict__ packets, const gnsscorr_sdr_accum_job* __restrict__ jobs,
     const uint32_t* __restrict__ carrier, const uint32_t* __restrict__ codebits, int saturate,
     gnsscorr_sdr_corr* __restrict__ out) {
   __shared__ int32_t red[kThreads / 64][6];
   const gnsscorr_sdr_accum_job j = jobs[blockIdx.x];
-  const gnsscorr_sdr_corr r =
-      accum_block(j, packets + (size_t)j.packet * kN, carrier, codebits, saturate, red);
-  if (threadIdx.x == 0) out[blockIdx.x] = r;
+  const uint32_t* d = packets + (size_t)j.packet * kN + j.data_off;
+  const uint32_t* sn = carrier + (size_t)j.sbin * kRow + j.soff;
+  size_t cb[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) cb[k] = ((size_t)j.sv * kCBins + j.cbin[k]) * kRow + j.coff[k];
+  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+  // Wave w covers the contiguous samples [1024 w, 1024 w + 1024) of the job,
+  // 64 per step.  The code bits it needs per arm lie in the 33 words from
+  // (cb + 1024 w) >> 5: lane l holds word l of that range (one coalesced load
+  // per arm for the whole job), and each sample's bit comes from its word's
+  // lane by ds_bpermute.
+  static_assert(kThreads == 128 && kN == 2048, "two waves of 1024 samples");
+  const int lane = threadIdx.x & 63, wave0 = (threadIdx.x >> 6) * 1024;
+  const int nend = min(j.samps, wave0 + 1024);
+  uint32_t cw[3];
+  uint32_t sh[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const size_t bit0 = cb[k] + (size_t)wave0;
+    sh[k] = (uint32_t)bit0 & 31u;
+    // words 0..32 cover bits up to sh + 1023; a lane loads only a word the
+    // wave's samples reach (an idle wave loads nothing)
+    const int last = ((int)sh[k] + (nend - wave0) - 1) >> 5;
+    cw[k] = (wave0 < nend && lane <= last) ? codebits[(bit0 >> 5) + lane] : 0u;
+  }
+  // all 16 steps' packet and carrier words are loaded before the first is
+  // used (a plain loop waited on memory latency at every step: one load pair
+  // in flight per wave)
+  constexpr int kSteps = 1024 / 64;
+  uint32_t av[kSteps], bv[kSteps];
+#pragma unroll
+  for (int st = 0; st < kSteps; st++) {
+    const int n = wave0 + st * 64 + lane;
+    av[st] = n < nend ? d[n] : 0u;
+    bv[st] = n < nend ? sn[n] : 0u;
+  }
+#pragma unroll
+  for (int st = 0; st < kSteps; st++) {
+    const int n = wave0 + st * 64 + lane;
+    const bool live = n < nend;
+    const uint32_t a = av[st], b = bv[st];
+    const int32_t ai = lo16(a), aq = hi16(a), bi = lo16(b), bq = hi16(b);
+    const int32_t ti = (ai * bi - aq * bq + 8192) >> 14, tq = (ai * bq + aq * bi + 8192) >> 14;
+    int32_t wi = saturate ? sat16(ti) : (int32_t)(int16_t)ti;
+    int32_t wq = saturate ? sat16(tq) : (int32_t)(int16_t)tq;
+    if (!live) wi = wq = 0;
+    const uint32_t rel = (uint32_t)(st * 64 + lane);   // n - wave0 < 1024
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const uint32_t r = rel + sh[k];
+      const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r >> 5) << 2), (int)cw[k]);
+      const int32_t m = (int32_t)((word >> (r & 31u)) & 1u) - 1;   // 0: +code, -1: -code
+      acc[2 * k] += (uint32_t)((wi ^ m) - m);       // A.i * code  (+-1)
+      acc[2 * k + 1] += (uint32_t)((wq ^ m) - m);   // A.q * code
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc[k] += (uint32_t)__shfl_xor((int)acc[k], o, 64);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 6; k++) red[threadIdx.x >> 6][k] = (int32_t)acc[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gnsscorr_sdr_corr r;
+    for (int k = 0; k < 3; k++) {
+      uint32_t si = 0, sq = 0;
+      for (int w = 0; w < kThreads / 64; w++) {
+        si += (uint32_t)red[w][2 * k];
+        sq += (uint32_t)red[w][2 * k + 1];
+      }
+      r.i[k] = (int32_t)si;
+      r.q[k] = (int32_t)sq;
+    }
+    out[blockIdx.x] = r;
+  }
 }
 
 // DumpAccum, correlator.cpp:452-525, with the channel callback between the

@@ -35,9 +35,9 @@ constexpr int kSV = 32;                  // MAX_SV
 constexpr int kThreads = 128;            // one Accum job per 128-thread workgroup
 constexpr double kInvFs = 4.882812500000000e-7;   // INVERSE_SAMPLE_FREQUENCY
 
-__host__ __device__ inline int16_t lo16(uint32_t v) { return (int16_t)(v & 0xFFFFu); }
-__host__ __device__ inline int16_t hi16(uint32_t v) { return (int16_t)(v >> 16); }
-__host__ __device__ inline int32_t sat16(int32_t v) {
+__host__ __device__ __forceinline__ int16_t lo16(uint32_t v) { return (int16_t)(v & 0xFFFFu); }
+__host__ __device__ __forceinline__ int16_t hi16(uint32_t v) { return (int16_t)(v >> 16); }
+__host__ __device__ __forceinline__ int32_t sat16(int32_t v) {
   return v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
 }
 
@@ -161,14 +161,16 @@ __host__ __device__ inline bool job_in_range(const gnsscorr_sdr_accum_job& j, in
 
 // Correlator::Accum of one job by a 128-thread workgroup (sse_cmulsc >> 14 of the
 // packet by the carrier row, then the E/P/L code bits; int32 wrapping sums).
-// d: the job's packet (2048 CPX); red: 2 x 6 int32 of LDS.  Every thread returns
-// the six sums.  Wave w covers the contiguous samples [1024 w, 1024 w + 1024)
+// d: the job's packet (2048 CPX); red: 2 x 6 int32 of LDS.  kAll: every thread
+// returns the six sums and red may be reused right after (the device loop);
+// otherwise only thread 0's result is defined (no trailing barrier).  Wave w covers the contiguous samples [1024 w, 1024 w + 1024)
 // of the job, 64 per step; the code bits it needs per arm lie in the 33 words
 // from (cb + 1024 w) >> 5: lane l holds word l of that range (one coalesced load
 // per arm for the whole job) and each sample's bit comes from its word's lane
 // by ds_bpermute.  All 16 steps' packet and carrier words are loaded before
 // the first is used (a plain loop waited on memory latency at every step).
-__device__ inline gnsscorr_sdr_corr accum_block(const gnsscorr_sdr_accum_job& j,
+template <bool kAll>
+__device__ __forceinline__ gnsscorr_sdr_corr accum_block(const gnsscorr_sdr_accum_job& j,
                                                 const uint32_t* __restrict__ d,
                                                 const uint32_t* __restrict__ carrier,
                                                 const uint32_t* __restrict__ codebits,
@@ -229,12 +231,14 @@ __device__ inline gnsscorr_sdr_corr accum_block(const gnsscorr_sdr_accum_job& j,
 #pragma unroll
     for (int k = 0; k < 6; k++) red[threadIdx.x >> 6][k] = (int32_t)acc[k];
   __syncthreads();
-  gnsscorr_sdr_corr r;
-  for (int k = 0; k < 3; k++) {
-    r.i[k] = (int32_t)((uint32_t)red[0][2 * k] + (uint32_t)red[1][2 * k]);
-    r.q[k] = (int32_t)((uint32_t)red[0][2 * k + 1] + (uint32_t)red[1][2 * k + 1]);
+  gnsscorr_sdr_corr r = {};
+  if (kAll || threadIdx.x == 0) {
+    for (int k = 0; k < 3; k++) {
+      r.i[k] = (int32_t)((uint32_t)red[0][2 * k] + (uint32_t)red[1][2 * k]);
+      r.q[k] = (int32_t)((uint32_t)red[0][2 * k + 1] + (uint32_t)red[1][2 * k + 1]);
+    }
   }
-  __syncthreads();   // red is reused by the next job
+  if (kAll) __syncthreads();   // red is reused by the next job
   return r;
 }
 
