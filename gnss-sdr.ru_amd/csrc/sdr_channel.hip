@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <string.h>
+#include <stdlib.h>
 #include "gnsscorr_internal.h"
 #include "sdr_corr_state.h"
 
@@ -501,89 +502,117 @@ __global__ __launch_bounds__(64) void sdr_channel_kernel(
 // over n_packets packets with UpdateState, DumpAccum (:452-525) and the
 // channel's Accum / ProcessFeedback (:530-555) at every dump -- the loop the
 // reference runs per packet on the host, here without leaving the device.
-// One 128-thread workgroup per channel: both waves run the Accum segments
-// (sdrc::accum_block, the kernel sdr_accum_kernel runs per job); thread 0
-// keeps the correlator state in LDS and runs the scalar bookkeeping and
-// Channel::Accum between segments.  The schedule is the host's
-// (gnsscorr_sdr_correlate): per packet at most 3 segments, at most 2 dumps.
-__global__ __launch_bounds__(sdrc::kThreads) void sdr_track_kernel(
-    const uint32_t* __restrict__ packets, int n_packets, int n_rx, const int32_t* __restrict__ rx,
-    gnsscorr_sdr_chan* __restrict__ states, gnsscorr_sdr_corr* __restrict__ corr,
-    Chan* __restrict__ chans, gnsscorr_sdr_feedback* __restrict__ fb_last,
-    gnsscorr_sdr_dump_rec* __restrict__ log, int log_per_ch, int32_t* __restrict__ n_log,
-    int32_t* __restrict__ status, gnsscorr_sdr_subframe* __restrict__ ev, int max_ev,
-    int32_t* __restrict__ n_ev, const uint32_t* __restrict__ carrier,
-    const uint32_t* __restrict__ codebits, int saturate, Twiddles tw) {
+// The schedule is the host's (gnsscorr_sdr_correlate): per packet at most 3
+// segments, at most 2 dumps.
+// One wavefront runs cpw channels.  Lane c (< cpw) owns channel ch0 + c: its
+// correlator state, sums and Channel object sit in LDS and the lane runs the
+// scalar work of its channel (bookkeeping, rotation, Channel::Accum,
+// ProcessFeedback) -- the cpw channels' serial chains side by side in SIMD.
+// Each Accum segment is done by the whole wave (sdrc::accum_wave), one channel
+// after the other.  The scalar chain is latency bound, so lanes working for
+// several channels at once is where the throughput comes from.
+constexpr int kLoopMaxCpw = 16;
+__global__ __launch_bounds__(64, 2) void sdr_track_kernel(
+    const uint32_t* __restrict__ packets, int n_packets, int n_rx, int n_ch, int cpw,
+    const int32_t* __restrict__ rx, gnsscorr_sdr_chan* __restrict__ states,
+    gnsscorr_sdr_corr* __restrict__ corr, Chan* __restrict__ chans,
+    gnsscorr_sdr_feedback* __restrict__ fb_last, gnsscorr_sdr_dump_rec* __restrict__ log,
+    int log_per_ch, int32_t* __restrict__ n_log, int32_t* __restrict__ status,
+    gnsscorr_sdr_subframe* __restrict__ ev, int max_ev, int32_t* __restrict__ n_ev,
+    const uint32_t* __restrict__ carrier, const uint32_t* __restrict__ codebits, int saturate,
+    Twiddles tw) {
   using namespace sdrc;
-  __shared__ gnsscorr_sdr_chan s_st;
-  __shared__ gnsscorr_sdr_corr s_c;
-  __shared__ int32_t red[kThreads / 64][6];
-  const int ch = blockIdx.x;
-  const bool t0 = threadIdx.x == 0;
-  __shared__ Chan cs;   // thread 0's copy of the Channel object (its FFT buffer unused: the
-                        // one in HBM is used); LDS, not scratch: the serial channel
-                        // code is a chain of dependent field accesses
+  __shared__ gnsscorr_sdr_chan s_st[kLoopMaxCpw];
+  __shared__ gnsscorr_sdr_corr s_c[kLoopMaxCpw];
+  __shared__ gnsscorr_sdr_accum_job s_job[kLoopMaxCpw];
+  __shared__ int32_t s_rx[kLoopMaxCpw];
+  // the Channel objects but their FFT buffers (those stay in HBM)
+  __shared__ __attribute__((aligned(16))) unsigned char s_obj[kLoopMaxCpw][offsetof(Chan, fft_buff)];
+  const int lane = threadIdx.x;
+  const int ch0 = blockIdx.x * cpw;
+  const int nc = min(cpw, n_ch - ch0);   // channels of this wave
+  const bool own = lane < nc;
+  const int ch = ch0 + (own ? lane : 0);
+  Chan& cs = *reinterpret_cast<Chan*>(s_obj[own ? lane : 0]);   // fields before fft_buff only
   gnsscorr_sdr_feedback f = {};
   int32_t ndump = 0, stat = 0;
-  const int r = rx ? rx[ch] : 0;
-  if (t0) {
-    s_st = states[ch];
-    s_c = corr[ch];
+  if (own) {
+    s_st[lane] = states[ch];
+    s_c[lane] = corr[ch];
     memcpy(&cs, &chans[ch], offsetof(Chan, fft_buff));
+    const int r = rx ? rx[ch] : 0;
+    s_rx[lane] = r;
+    if (r < 0 || r >= n_rx) stat = -1;
   }
-  if (r < 0 || r >= n_rx) stat = -1;
   __syncthreads();
   Events e = {ev, max_ev, n_ev, ch, 0};
-  for (int p = 0; p < n_packets && stat == 0 && s_st.active; p++) {
-    const uint32_t* pkt = packets + ((size_t)p * n_rx + r) * kN;
+  for (int p = 0; p < n_packets; p++) {
+    bool live = own && stat == 0 && s_st[lane].active;
+    if (!__any(live)) break;   // a stopped or killed channel stays so
     int off = 0, left = kN, dumps = 0;
     for (int phase = 0; phase < 3; phase++) {
-      const bool dump = dumps < 2 && s_st.rollover <= (uint32_t)left;
-      const int samps = dump ? (int)s_st.rollover : left;
-      if (samps > 0) {
-        const gnsscorr_sdr_accum_job j = make_job(s_st, 0, off, samps);
-        if (!job_in_range(j, 1)) {   // uniform: every thread sees the same state
-          stat = 1 + p;
-          break;
-        }
-        // ends with a barrier: every thread has read s_st before thread 0 writes it
-        const gnsscorr_sdr_corr a = accum_block(j, pkt, carrier, codebits, saturate, red);
-        if (t0) {
-          for (int k = 0; k < 3; k++) {
-            s_c.i[k] = (int32_t)((uint32_t)s_c.i[k] + (uint32_t)a.i[k]);
-            s_c.q[k] = (int32_t)((uint32_t)s_c.q[k] + (uint32_t)a.q[k]);
+      bool dump = false;
+      int samps = 0;
+      if (own) {
+        gnsscorr_sdr_accum_job j = {};
+        if (live) {
+          const gnsscorr_sdr_chan& s = s_st[lane];
+          dump = dumps < 2 && s.rollover <= (uint32_t)left;
+          samps = dump ? (int)s.rollover : left;
+          j = make_job(s, 0, off, samps);
+          if (samps > 0 && !job_in_range(j, 1)) {   // the host path returns EINVAL here
+            stat = 1 + p;
+            live = dump = false;
+            samps = 0;
           }
-          update_state(&s_st, samps);
         }
-      } else {
-        __syncthreads();
+        j.samps = samps;
+        s_job[lane] = j;
       }
-      off += samps;
-      left -= samps;
-      if (dump) {
-        if (t0) {
-          rotate(&s_st, &s_c);
+      __syncthreads();
+      for (int c = 0; c < nc; c++) {   // the segments, one channel after the other
+        const gnsscorr_sdr_accum_job j = s_job[c];
+        if (j.samps > 0) {
+          const uint32_t* pkt = packets + ((size_t)p * n_rx + s_rx[c]) * kN;
+          const gnsscorr_sdr_corr a = accum_wave(j, pkt, carrier, codebits, saturate);
+          if (lane == c) {
+            for (int k = 0; k < 3; k++) {
+              s_c[c].i[k] = (int32_t)((uint32_t)s_c[c].i[k] + (uint32_t)a.i[k]);
+              s_c[c].q[k] = (int32_t)((uint32_t)s_c[c].q[k] + (uint32_t)a.q[k]);
+            }
+          }
+        }
+      }
+      if (live) {
+        gnsscorr_sdr_chan* s = &s_st[lane];
+        gnsscorr_sdr_corr* cc = &s_c[lane];
+        if (samps > 0) update_state(s, samps);
+        off += samps;
+        left -= samps;
+        if (dump) {
+          rotate(s, cc);
           e.ms = p;
-          accum(cs, chans[ch].fft_buff, tw, s_c, &f, e);
+          accum(cs, chans[ch].fft_buff, tw, *cc, &f, e);
           if (ndump < log_per_ch) {
             gnsscorr_sdr_dump_rec& d = log[(size_t)ch * log_per_ch + ndump];
             d.packet = p;
             d.phase = phase;
-            d.corr = s_c;
+            d.corr = *cc;
             d.fb = f;
           }
-          after_feedback(&s_st, &s_c, f);
+          after_feedback(s, cc, f);
+          ndump++;
+          dumps++;
         }
-        ndump++;
-        dumps++;
+        if (!dump || !s->active) live = false;
       }
-      __syncthreads();
-      if (!dump || !s_st.active) break;
+      __syncthreads();   // s_job is rewritten by the next phase
+      if (!__any(live)) break;
     }
   }
-  if (t0) {
-    states[ch] = s_st;
-    corr[ch] = s_c;
+  if (own) {
+    states[ch] = s_st[lane];
+    corr[ch] = s_c[lane];
     memcpy(&chans[ch], &cs, offsetof(Chan, fft_buff));
     if (fb_last && ndump > 0) fb_last[ch] = f;
     if (n_log) n_log[ch] = ndump;
@@ -671,10 +700,18 @@ extern "C" int gnsscorr_sdr_track_dev(gnsscorr_sdr_corr_ctx* ctx, const int16_t*
   int saturate;
   gnsscorr_sdr_corr_tables(ctx, &carrier, &codebits, &saturate);
   static const Twiddles tw = make_twiddles();
-  hipLaunchKernelGGL(sdr_track_kernel, dim3(n_ch), dim3(sdrc::kThreads), 0, s,
-                     (const uint32_t*)d_packets, n_packets, n_rx, d_rx, d_states, d_corr, d_ch,
-                     d_fb_last, d_log, log_per_ch, d_n_log, d_status, d_events, max_events,
-                     d_n_events, carrier, codebits, saturate, tw);
+  // channels per wave: about two waves per SIMD for the whole launch (the
+  // scalar chains are latency bound; a wave's lanes run cpw of them at once)
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                              gnsscorr_sdr_corr_device(ctx));
+  int cpw = (n_ch + 8 * cus - 1) / (8 * cus);
+  if (const char* ov = getenv("GNSSCORR_SDR_LOOP_CPW")) cpw = atoi(ov);
+  cpw = cpw < 1 ? 1 : (cpw > kLoopMaxCpw ? kLoopMaxCpw : cpw);
+  hipLaunchKernelGGL(sdr_track_kernel, dim3((n_ch + cpw - 1) / cpw), dim3(64), 0, s,
+                     (const uint32_t*)d_packets, n_packets, n_rx, n_ch, cpw, d_rx, d_states,
+                     d_corr, d_ch, d_fb_last, d_log, log_per_ch, d_n_log, d_status, d_events,
+                     max_events, d_n_events, carrier, codebits, saturate, tw);
   HIP_TRY(hipGetLastError());
   return GNSSCORR_OK;
 }

@@ -57,6 +57,28 @@ __host__ __device__ inline uint32_t carrier_bin(double nco) {
   return (uint32_t)b;
 }
 
+// fmod(x, 1.0) and fmod(x, 1023) without the library's iterative reduction
+// (the device libm's fmod is a long loop): x - trunc(x) is exact for every
+// finite x (the integer bits are removed from x's own significand), and for
+// 0 <= x < 4 * 1023, x - 1023 n with n = trunc(x / 1023) fixed up by one step
+// is exact by Sterbenz's lemma (1023 n <= x < 2 * 1023 n for n >= 1), so both
+// equal fmod bit for bit (a zero result takes the sign of x, as fmod's); other
+// x take fmod itself.
+__host__ __device__ __forceinline__ double fmod_1(double x) {
+#pragma clang fp contract(off)
+  if (!isfinite(x)) return fmod(x, 1.0);
+  const double r = x - trunc(x);
+  return r == 0.0 ? copysign(0.0, x) : r;   // fmod's zero has the sign of x
+}
+__host__ __device__ __forceinline__ double fmod_1023(double x) {
+#pragma clang fp contract(off)
+  if (!(x >= 0.0 && x < 4.0 * 1023.0)) return fmod(x, 1023);
+  double r = x - 1023.0 * trunc(x / 1023.0);
+  if (r < 0.0) r += 1023.0;
+  else if (r >= 1023.0) r -= 1023.0;
+  return r;
+}
+
 __host__ __device__ inline void update_state(gnsscorr_sdr_chan* s, int32_t samps) {   // :369-422
 #pragma clang fp contract(off)
   s->code_phase += samps * s->code_nco * kInvFs;
@@ -75,8 +97,8 @@ __host__ __device__ inline void update_state(gnsscorr_sdr_chan* s, int32_t samps
       }
     }
   }
-  s->carrier_phase_mod = fmod(s->carrier_phase_mod, 1.0);
-  s->code_phase_mod = fmod(s->code_phase_mod, 1023);
+  s->carrier_phase_mod = fmod_1(s->carrier_phase_mod);
+  s->code_phase_mod = fmod_1023(s->code_phase_mod);
   s->rollover -= (uint32_t)samps;
   s->soff += samps;
   for (int k = 0; k < 3; k++) s->coff[k] += samps;
@@ -159,86 +181,79 @@ __host__ __device__ inline bool job_in_range(const gnsscorr_sdr_accum_job& j, in
   return true;
 }
 
-// Correlator::Accum of one job by a 128-thread workgroup (sse_cmulsc >> 14 of the
-// packet by the carrier row, then the E/P/L code bits; int32 wrapping sums).
-// d: the job's packet (2048 CPX); red: 2 x 6 int32 of LDS.  kAll: every thread
-// returns the six sums and red may be reused right after (the device loop);
-// otherwise only thread 0's result is defined (no trailing barrier).  Wave w covers the contiguous samples [1024 w, 1024 w + 1024)
-// of the job, 64 per step; the code bits it needs per arm lie in the 33 words
-// from (cb + 1024 w) >> 5: lane l holds word l of that range (one coalesced load
-// per arm for the whole job) and each sample's bit comes from its word's lane
-// by ds_bpermute.  All 16 steps' packet and carrier words are loaded before
-// the first is used (a plain loop waited on memory latency at every step).
-template <bool kAll>
-__device__ __forceinline__ gnsscorr_sdr_corr accum_block(const gnsscorr_sdr_accum_job& j,
-                                                const uint32_t* __restrict__ d,
-                                                const uint32_t* __restrict__ carrier,
-                                                const uint32_t* __restrict__ codebits,
-                                                int saturate, int32_t (*red)[6]) {
-  static_assert(kThreads == 128 && kN == 2048, "two waves of 1024 samples");
+// Correlator::Accum of one job by ONE wavefront (sse_cmulsc >> 14 of the packet
+// by the carrier row, then the E/P/L code bits; int32 wrapping sums), for the
+// device-resident loop.  d: the job's packet (2048 CPX).  Every lane returns the
+// six sums (xor-shuffle reduction, no LDS, no barrier).  The job is done as two
+// halves of 1024 samples, 64 per step, exactly as a wave of sdr_accum_kernel
+// does its half: per arm the code bits of a half lie in the 33 words from
+// (cb + 1024 h) >> 5; lane l holds word l of that range (one coalesced load per
+// arm) and each sample's bit comes from its word's lane by ds_bpermute.  All 16
+// steps' packet and carrier words of a half are loaded before the first is used.
+__device__ __forceinline__ gnsscorr_sdr_corr accum_wave(const gnsscorr_sdr_accum_job& j,
+                                                       const uint32_t* __restrict__ d,
+                                                       const uint32_t* __restrict__ carrier,
+                                                       const uint32_t* __restrict__ codebits,
+                                                       int saturate) {
+  static_assert(kN == 2048, "two halves of 1024 samples");
   d += j.data_off;
   const uint32_t* sn = carrier + (size_t)j.sbin * kRow + j.soff;
   size_t cb[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) cb[k] = ((size_t)j.sv * kCBins + j.cbin[k]) * kRow + j.coff[k];
   uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-  const int lane = threadIdx.x & 63, wave0 = (threadIdx.x >> 6) * 1024;
-  const int nend = min(j.samps, wave0 + 1024);
-  uint32_t cw[3];
-  uint32_t sh[3];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const size_t bit0 = cb[k] + (size_t)wave0;
-    sh[k] = (uint32_t)bit0 & 31u;
-    // words 0..32 cover bits up to sh + 1023; a lane loads only a word the
-    // wave's samples reach (an idle wave loads nothing)
-    const int last = ((int)sh[k] + (nend - wave0) - 1) >> 5;
-    cw[k] = (wave0 < nend && lane <= last) ? codebits[(bit0 >> 5) + lane] : 0u;
-  }
-  constexpr int kSteps = 1024 / 64;
-  uint32_t av[kSteps], bv[kSteps];
-#pragma unroll
-  for (int st = 0; st < kSteps; st++) {
-    const int n = wave0 + st * 64 + lane;
-    av[st] = n < nend ? d[n] : 0u;
-    bv[st] = n < nend ? sn[n] : 0u;
-  }
-#pragma unroll
-  for (int st = 0; st < kSteps; st++) {
-    const int n = wave0 + st * 64 + lane;
-    const bool live = n < nend;
-    const uint32_t a = av[st], b = bv[st];
-    const int32_t ai = lo16(a), aq = hi16(a), bi = lo16(b), bq = hi16(b);
-    const int32_t ti = (ai * bi - aq * bq + 8192) >> 14, tq = (ai * bq + aq * bi + 8192) >> 14;
-    int32_t wi = saturate ? sat16(ti) : (int32_t)(int16_t)ti;
-    int32_t wq = saturate ? sat16(tq) : (int32_t)(int16_t)tq;
-    if (!live) wi = wq = 0;
-    const uint32_t rel = (uint32_t)(st * 64 + lane);   // n - wave0 < 1024
+  const int lane = threadIdx.x & 63;
+  for (int h = 0; h < 2; h++) {
+    const int wave0 = h * 1024;
+    if (wave0 >= j.samps) break;   // wave-uniform
+    const int nend = min(j.samps, wave0 + 1024);
+    uint32_t cw[3];
+    uint32_t sh[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      const uint32_t r = rel + sh[k];
-      const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r >> 5) << 2), (int)cw[k]);
-      const int32_t m = (int32_t)((word >> (r & 31u)) & 1u) - 1;   // 0: +code, -1: -code
-      acc[2 * k] += (uint32_t)((wi ^ m) - m);       // A.i * code  (+-1)
-      acc[2 * k + 1] += (uint32_t)((wq ^ m) - m);   // A.q * code
+      const size_t bit0 = cb[k] + (size_t)wave0;
+      sh[k] = (uint32_t)bit0 & 31u;
+      const int last = ((int)sh[k] + (nend - wave0) - 1) >> 5;
+      cw[k] = lane <= last ? codebits[(bit0 >> 5) + lane] : 0u;
+    }
+    constexpr int kSteps = 1024 / 64;
+    uint32_t av[kSteps], bv[kSteps];
+#pragma unroll
+    for (int st = 0; st < kSteps; st++) {
+      const int n = wave0 + st * 64 + lane;
+      av[st] = n < nend ? d[n] : 0u;
+      bv[st] = n < nend ? sn[n] : 0u;
+    }
+#pragma unroll
+    for (int st = 0; st < kSteps; st++) {
+      const int n = wave0 + st * 64 + lane;
+      const bool live = n < nend;
+      const uint32_t a = av[st], b = bv[st];
+      const int32_t ai = lo16(a), aq = hi16(a), bi = lo16(b), bq = hi16(b);
+      const int32_t ti = (ai * bi - aq * bq + 8192) >> 14, tq = (ai * bq + aq * bi + 8192) >> 14;
+      int32_t wi = saturate ? sat16(ti) : (int32_t)(int16_t)ti;
+      int32_t wq = saturate ? sat16(tq) : (int32_t)(int16_t)tq;
+      if (!live) wi = wq = 0;
+      const uint32_t rel = (uint32_t)(st * 64 + lane);   // n - wave0 < 1024
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const uint32_t r = rel + sh[k];
+        const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r >> 5) << 2), (int)cw[k]);
+        const int32_t m = (int32_t)((word >> (r & 31u)) & 1u) - 1;   // 0: +code, -1: -code
+        acc[2 * k] += (uint32_t)((wi ^ m) - m);       // A.i * code  (+-1)
+        acc[2 * k + 1] += (uint32_t)((wq ^ m) - m);   // A.q * code
+      }
     }
   }
 #pragma unroll
   for (int k = 0; k < 6; k++)
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc[k] += (uint32_t)__shfl_xor((int)acc[k], o, 64);
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < 6; k++) red[threadIdx.x >> 6][k] = (int32_t)acc[k];
-  __syncthreads();
-  gnsscorr_sdr_corr r = {};
-  if (kAll || threadIdx.x == 0) {
-    for (int k = 0; k < 3; k++) {
-      r.i[k] = (int32_t)((uint32_t)red[0][2 * k] + (uint32_t)red[1][2 * k]);
-      r.q[k] = (int32_t)((uint32_t)red[0][2 * k + 1] + (uint32_t)red[1][2 * k + 1]);
-    }
+  gnsscorr_sdr_corr r;
+  for (int k = 0; k < 3; k++) {
+    r.i[k] = (int32_t)acc[2 * k];
+    r.q[k] = (int32_t)acc[2 * k + 1];
   }
-  if (kAll) __syncthreads();   // red is reused by the next job
   return r;
 }
 
