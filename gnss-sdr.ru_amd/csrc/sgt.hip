@@ -45,9 +45,12 @@ namespace {
 constexpr int kMaxCode = 1023;
 constexpr int kPadLen = kMaxCode + 2;
 constexpr int kMaxWaves = 16;
+#ifndef SGT_WPE
+#define SGT_WPE 3
+#endif
 
 struct SgtParams {
-  int system, file_type, switch_iq, code_length;
+  int system, file_type, switch_iq, code_length, chunked;
   double fs, code_basis, if_freq, l1_if_step, glo_zero, spc;
   double tau1, tau2, k1, k2, k3, pdi_code;
 };
@@ -62,6 +65,15 @@ __device__ __forceinline__ int xcd_channel(int b, int G) {
 // one instruction: a negative index wraps to a huge unsigned and lands on hi
 __device__ __forceinline__ int clampu(int i, int hi) { return (int)min((unsigned)i, (unsigned)hi); }
 
+// a value every lane of the workgroup holds (the channel's state is uniform):
+// held in scalar registers instead of a VGPR pair
+__device__ __forceinline__ double uni(double v) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((int)b);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -72,8 +84,12 @@ __device__ __forceinline__ double wave_sum(double v) {
 // leave the totals in every lane, so an epoch needs no LDS partials and no
 // barrier, and the loop filters run once per wave instead of once per wave of
 // a 4-16-wave workgroup.
-template <int FT, bool CLOSED, bool WAVE>
-__global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
+// MAXT: the launch bound (64 = WAVE; 256 for the default small-receiver shape,
+// which then keeps its registers instead of fitting the 1024-thread budget).
+// Wave mode asks for 3 waves per SIMD (<= 168 VGPRs): measured 3 % faster than
+// the 2 the chunked path otherwise compiles to.
+template <int FT, bool CLOSED, int MAXT>
+__global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kernel(
     SgtParams p, const int8_t* __restrict__ ifbuf, int64_t stride, int64_t n_samples,
     const uint32_t* __restrict__ codes, gnsscorr_sgt_chan* __restrict__ chans, int n_epochs,
     gnsscorr_sgt_epoch* __restrict__ out) {
@@ -82,7 +98,9 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
   // so a 511-chip GLONASS table takes 4.1 KB, not the 1023-chip maximum
   extern __shared__ double s_sgn[];
   __shared__ double s_part[2][kMaxWaves][6];
+  __shared__ double2 s_w[16];   // chunked path: exp(i*A*n/fs), n < kC
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
+  constexpr bool WAVE = MAXT == 64;
   const int T = WAVE ? 64 : blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = T >> 6;
   gnsscorr_sgt_chan c = chans[ch];
@@ -120,11 +138,6 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
     const int blk = (int)blk_d;
     const double aE = c.rem_code - p.spc, aL = c.rem_code + p.spc, aP = c.rem_code;
     const double A = (c.carr_freq * 2.0) * M_PI;        // (carrFreq * 2.0 * %pi)
-    // carrier at the thread's first sample, rotation by T samples
-    const double th0 = A * ((double)tid / p.fs) + c.rem_carr, thw = A * ((double)T / p.fs);
-    double sn, cs, sw, cw;
-    sincos(th0, &sn, &cs);   // one shared argument reduction per angle
-    sincos(thw, &sw, &cw);   // (sgt.o is built with promote-alloca-to-lds off)
     double ie = 0, ip = 0, il = 0, qe = 0, qp = 0, ql = 0;
     const int8_t* src = base + (FT == 2 ? 2 : 1) * c.pos;
     // I/Q byte order as bit-field offsets (switchIQ without a per-sample select)
@@ -146,6 +159,11 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
     const bool in_table = c.rem_code >= p.spc - 1.0 && p.spc >= 0.0 && p.spc < 0.99;
     auto run = [&](auto clamp_tag) {
     constexpr bool kClamp = decltype(clamp_tag)::value;
+    // carrier at the thread's first sample, rotation by T samples
+    const double th0 = A * ((double)tid / p.fs) + c.rem_carr, thw = A * ((double)T / p.fs);
+    double sn, cs, sw, cw;
+    sincos(th0, &sn, &cs);   // one shared argument reduction per angle
+    sincos(thw, &sw, &cw);   // (sgt.o is built with promote-alloca-to-lds off)
     auto index = [&](double x) {
       const int i = (int)ceil(x);
       return kClamp ? clampu(i, L + 1) : i;
@@ -203,7 +221,154 @@ __global__ __launch_bounds__(WAVE ? 64 : 1024) void sgt_track_kernel(
       if (k < blk) sample(k, w[u]);
     }
     };
-    if (in_table)
+    // ---- chunked path (round 3).  A lane takes chunks of kC consecutive
+    // samples (chunk q at k = q*kC - mis, q = lane + j*T, one or two 16-byte
+    // loads on the 16-byte grid of the stream) instead of single samples
+    // strided by T.  Within a chunk each code index takes at most two values
+    // ((kC-1)*step < 1): the index j0 of the chunk's first sample comes from
+    // the exact formula, and the first sample of index j0+1 from the crossing
+    // d = (j0 - a)/step (sample k has index > j0 iff a + k*step > j0, i.e.
+    // k > d).  When d lies within 1e-6 samples of an integer the real-valued
+    // crossing could round either way, so that lane recomputes the chunk's
+    // crossings with the exact fp64 indices, sample by sample.  Samples then
+    // select the code by position (n < beta ? c(j0) : c(j0+1)) instead of
+    // evaluating ceil(rem -/+ spc + k*step) three times each.
+    // Carrier: exp(i theta_k) = exp(i theta_k0) * W_n, n = k - k0; W_n =
+    // exp(i*A*n/fs) (n < kC) is an LDS table read by broadcast, each arm sums
+    // code * W_n * raw over the chunk and rotates the sum by exp(i theta_k0)
+    // once per chunk (tracking.sci:305-326, same sums up to fp64 rounding).
+    constexpr int kC = 16;
+    constexpr int kBps = FT == 2 ? 2 : 1;
+    auto run_chunks = [&]() {
+      const int mis = (int)((uintptr_t)src & 15) / kBps;
+      const uint4* ab = reinterpret_cast<const uint4*>(src - mis * kBps);
+      const int nC = (blk + mis + kC - 1) / kC;
+      const int nIt = (nC + T - 1) / T;
+      const double inv_step = uni(1.0 / step), stp = uni(step);
+      const double aX[3] = {uni(aE), uni(aP), uni(aL)};
+      double sb, cb, sR, cR;
+      sincos(A * ((double)(tid * kC - mis) / p.fs) + c.rem_carr, &sb, &cb);
+      sincos(A * ((double)(T * kC) / p.fs), &sR, &cR);
+      sR = uni(sR);
+      cR = uni(cR);
+      if (tid < kC) {
+        double swl, cwl;
+        sincos(A * ((double)tid / p.fs), &swl, &cwl);
+        s_w[tid] = make_double2(cwl, swl);
+      }
+      __syncthreads();
+      double accI[3] = {0.0, 0.0, 0.0}, accQ[3] = {0.0, 0.0, 0.0};
+      constexpr int kW = kC * kBps / 16;   // 16-byte words per chunk
+      uint4 nx[kW];
+      auto fetch = [&](int it, uint4 (&x)[kW]) {
+        const int q = it * T + tid;
+#pragma unroll
+        for (int u = 0; u < kW; u++) {
+          // only words holding a sample of the epoch: none past the stream's end
+          const int ks = q * kC - mis + u * (16 / kBps);
+          x[u] = ks < blk ? ab[q * kW + u] : make_uint4(0, 0, 0, 0);
+        }
+      };
+      fetch(0, nx);
+      for (int it = 0; it < nIt; it++) {
+        uint32_t wd[4 * kW];
+#pragma unroll
+        for (int u = 0; u < kW; u++) {
+          wd[4 * u] = nx[u].x; wd[4 * u + 1] = nx[u].y;
+          wd[4 * u + 2] = nx[u].z; wd[4 * u + 3] = nx[u].w;
+        }
+        if (it + 1 < nIt) fetch(it + 1, nx);
+        const int q = it * T + tid;
+        const int k0 = q * kC - mis;
+        // the epoch's first and last chunks: samples outside [0, blk) count as 0
+        if (k0 < 0 || k0 + kC > blk) {
+#pragma unroll
+          for (int n = 0; n < kC; n++) {
+            const bool v = (unsigned)(k0 + n) < (unsigned)blk;
+            constexpr int kSpw = 4 / kBps;   // samples per dword
+            const uint32_t m = (kBps == 2 ? 0xffffu : 0xffu) << (8 * kBps * (n % kSpw));
+            wd[n / kSpw] &= v ? 0xffffffffu : ~m;
+          }
+        }
+        const double t0 = (double)k0 * stp;
+        int beta[3], j0[3];
+        double g0[3], g1[3];
+        bool risky = false;
+#pragma unroll
+        for (int x = 0; x < 3; x++) {
+          const double jf = ceil(aX[x] + t0);
+          j0[x] = (int)jf;
+          const double d = (jf - aX[x]) * inv_step;
+          const double fd = floor(d);
+          const double fr = d - fd;
+          risky |= !(fr > 1e-6 && fr < 1.0 - 1e-6);
+          beta[x] = min(max((int)fd + 1 - k0, 1), kC);
+          // the code as +-1.0: only the high word differs (the low one is 0)
+          const uint32_t* sg = reinterpret_cast<const uint32_t*>(s_sgn) + 1;
+          g0[x] = __longlong_as_double((long long)sg[2 * clampu(j0[x], L + 1)] << 32);
+          g1[x] = __longlong_as_double((long long)sg[2 * clampu(j0[x] + 1, L + 1)] << 32);
+        }
+        if (risky && q < nC) {
+          // exact crossings: the first sample whose index exceeds j0
+#pragma unroll 1
+          for (int x = 0; x < 3; x++) {
+            int b = kC;
+#pragma unroll 1
+            for (int n = kC - 1; n >= 1; n--)
+              if ((int)ceil(aX[x] + (double)(k0 + n) * stp) > j0[x]) b = n;
+            beta[x] = b;
+          }
+        }
+        double Ur[3] = {0.0, 0.0, 0.0}, Ui[3] = {0.0, 0.0, 0.0};
+        // the W_n reads are loop invariant: an opaque offset per chunk keeps
+        // them from being hoisted out of the chunk loop (16 complex in VGPRs)
+        int wo = 0;
+        asm volatile("" : "+v"(wo));
+#pragma unroll
+        for (int n = 0; n < kC; n++) {
+          double ur, ui;
+          if constexpr (FT == 2) {
+            const uint32_t w = wd[n >> 1];
+            const int sh = (n & 1) * 16;
+            const double re = (double)(int)__builtin_amdgcn_sbfe(w, sh + sh_re, 8);
+            const double im = (double)(int)__builtin_amdgcn_sbfe(w, sh + sh_im, 8);
+            const double2 W = s_w[n + wo];   // broadcast read
+            ur = fma(W.x, re, -(W.y * im));   // W_n * raw
+            ui = fma(W.x, im, W.y * re);
+          } else {
+            const double re = (double)(int)__builtin_amdgcn_sbfe(wd[n >> 2], (n & 3) * 8, 8);
+            const double2 W = s_w[n + wo];
+            ur = W.x * re;
+            ui = W.y * re;
+          }
+#pragma unroll
+          for (int x = 0; x < 3; x++) {
+            const double g = n < beta[x] ? g0[x] : g1[x];
+            Ur[x] = fma(ur, g, Ur[x]);
+            Ui[x] = fma(ui, g, Ui[x]);
+          }
+#ifdef SGT_SCHED
+          if (n % SGT_SCHED == SGT_SCHED - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+        // exp(i theta_k0) * U: real part -> Q (qBasebandSignal), imaginary -> I
+#pragma unroll
+        for (int x = 0; x < 3; x++) {
+          accQ[x] = fma(cb, Ur[x], fma(-sb, Ui[x], accQ[x]));
+          accI[x] = fma(sb, Ur[x], fma(cb, Ui[x], accI[x]));
+        }
+        const double cn = fma(cb, cR, -(sb * sR));
+        sb = fma(sb, cR, cb * sR);
+        cb = cn;
+      }
+      ie = accI[0]; ip = accI[1]; il = accI[2];
+      qe = accQ[0]; qp = accQ[1]; ql = accQ[2];
+    };
+    const bool chunked = p.chunked && in_table && (double)(kC - 1) * step < 0.999 &&
+                         ((uintptr_t)src & (kBps - 1)) == 0;
+    if (chunked)
+      run_chunks();
+    else if (in_table)
       run(std::false_type{});
     else
       run(std::true_type{});
@@ -377,6 +542,9 @@ extern "C" int gnsscorr_sgt_create(gnsscorr_sgt_ctx** out, const gnsscorr_sgt_cf
   p.file_type = cfg->file_type;
   p.switch_iq = cfg->system == 1 ? cfg->switch_iq : 0;
   p.code_length = cfg->code_length;
+  // GNSSCORR_SGT_CHUNK=0: the per-sample index path only (A/B and tests)
+  const char* chk = getenv("GNSSCORR_SGT_CHUNK");
+  p.chunked = !(chk && chk[0] == '0');
   p.fs = cfg->samp_rate;
   p.code_basis = cfg->code_freq_basis;
   p.if_freq = cfg->if_freq;
@@ -442,10 +610,13 @@ extern "C" int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx* c, const int8_t* d_if, i
 #define SGT_LAUNCH(FT, CL)                                                                     \
   do {                                                                                         \
     if (T == 64)                                                                               \
-      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, true>), grid, block, tab, c->stream, c->p, \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 64>), grid, block, tab, c->stream, c->p,   \
+                         d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
+    else if (T <= 256)                                                                         \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 256>), grid, block, tab, c->stream, c->p,  \
                          d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
     else                                                                                       \
-      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, false>), grid, block, tab, c->stream, c->p, \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 1024>), grid, block, tab, c->stream, c->p, \
                          d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
   } while (0)
   if (c->cfg.file_type == 2) {
