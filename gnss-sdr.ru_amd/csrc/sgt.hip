@@ -45,6 +45,9 @@ namespace {
 constexpr int kMaxCode = 1023;
 constexpr int kPadLen = kMaxCode + 2;
 constexpr int kMaxWaves = 16;
+#ifndef SGT_KC32
+#define SGT_KC32 1
+#endif
 #ifndef SGT_WPE
 #define SGT_WPE 3
 #endif
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
   // so a 511-chip GLONASS table takes 4.1 KB, not the 1023-chip maximum
   extern __shared__ double s_sgn[];
   __shared__ double s_part[2][kMaxWaves][6];
-  __shared__ double2 s_w[16];   // chunked path: exp(i*A*n/fs), n < kC
+  __shared__ double2 s_w[32];   // chunked path: exp(i*A*n/fs), n < kC
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
   constexpr bool WAVE = MAXT == 64;
   const int T = WAVE ? 64 : blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -237,9 +240,9 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
     // exp(i*A*n/fs) (n < kC) is an LDS table read by broadcast, each arm sums
     // code * W_n * raw over the chunk and rotates the sum by exp(i theta_k0)
     // once per chunk (tracking.sci:305-326, same sums up to fp64 rounding).
-    constexpr int kC = 16;
     constexpr int kBps = FT == 2 ? 2 : 1;
-    auto run_chunks = [&]() {
+    auto run_chunks = [&](auto kc_tag) {
+      constexpr int kC = decltype(kc_tag)::value;
       const int mis = (int)((uintptr_t)src & 15) / kBps;
       const uint4* ab = reinterpret_cast<const uint4*>(src - mis * kBps);
       const int nC = (blk + mis + kC - 1) / kC;
@@ -364,10 +367,12 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
       ie = accI[0]; ip = accI[1]; il = accI[2];
       qe = accQ[0]; qp = accQ[1]; ql = accQ[2];
     };
-    const bool chunked = p.chunked && in_table && (double)(kC - 1) * step < 0.999 &&
+    const bool chunked = p.chunked && in_table && 15.0 * step < 0.999 &&
                          ((uintptr_t)src & (kBps - 1)) == 0;
-    if (chunked)
-      run_chunks();
+    if (chunked && SGT_KC32 && 31.0 * step < 0.999)
+      run_chunks(std::integral_constant<int, 32>{});
+    else if (chunked)
+      run_chunks(std::integral_constant<int, 16>{});
     else if (in_table)
       run(std::false_type{});
     else

@@ -81,6 +81,46 @@ def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch, threads,
     assert (ch["code_freq"] == ch0["code_freq"]).all()
 
 
+@pytest.mark.parametrize("chunk", ["1", "0"])
+@pytest.mark.parametrize("system,file_type", [(1, 2), (0, 2), (1, 1)])
+def test_open_loop_crossings_on_exact_chips(gpu, system, file_type, chunk, monkeypatch):
+    """codeFreq = fs/32 (GPS: fs/16) and remCode on the 1/32 grid: every code index
+    crossing ceil(remCode -/+ spc + k*step) lands exactly on an integer chip.  There
+    the chunked path's real-valued crossing estimate has no margin, so the exact
+    per-sample scan decides (sgt.hip run_chunks); GNSSCORR_SGT_CHUNK=0 runs the
+    per-sample index path on the same inputs.  Indices and state bit-exact."""
+    gc = gpu
+    monkeypatch.setenv("GNSSCORR_SGT_CHUNK", chunk)
+    rng = np.random.default_rng(5 + system + 2 * file_type)
+    n = 120000
+    IF = gc.ifgen(n, [], fs=FS, iq=file_type == 2, seed=33)
+    d_if = gc.DevBuf.from_array(IF)
+    ctx = gc.SgtCtx(system, fileType=file_type, samplingFreq=FS)
+    s = S.settings(system, fileType=file_type, samplingFreq=FS)
+    C = 32
+    ids = rng.integers(-7, 7, C) if system == 1 else rng.integers(1, 33, C)
+    ch = np.zeros(C, gc.SGT_CHAN)
+    ch["code_id"] = ids
+    ch["pos"] = rng.integers(0, n - 20000, C)
+    ch["code_freq"] = FS / (32 if system == 1 else 16)
+    ch["rem_code"] = rng.integers(0, 2, C) / 32.0
+    ch["rem_carr"] = rng.uniform(-6.2, 6.2, C)
+    ch["carr_freq"] = rng.uniform(-3e6, 3e6, C)
+    ch0 = ch.copy()
+    ep = ctx.track(d_if.ptr, 0, n, ch, 1, closed_loop=False)[:, 0]
+    for i in range(C):
+        pad = S.padded_code(system, int(ids[i]))
+        sums, blk, pos, rc, rcar = S.correlate(IF, s, pad, int(ch0["pos"][i]),
+                                               float(ch0["rem_code"][i]),
+                                               float(ch0["rem_carr"][i]),
+                                               float(ch0["code_freq"][i]),
+                                               float(ch0["carr_freq"][i]))
+        assert ep["status"][i] == 0 and ep["blksize"][i] == blk
+        assert ch["pos"][i] == pos and ch["rem_code"][i] == rc and ch["rem_carr"][i] == rcar
+        got = np.array([ep[f][i] for f in SUMS])
+        assert _close(got, sums).all(), (i, got, sums)
+
+
 def _glonass_scene(gc, n_ms, fs=FS):
     rng = np.random.default_rng(5)
     fchs = np.arange(-7, 7)
