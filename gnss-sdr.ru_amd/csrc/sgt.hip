@@ -15,6 +15,10 @@
 //                thread, then an fp64 rotation per T samples (:305-313)
 //    sums        I = code*imag(carr*raw), Q = code*real(carr*raw) (:316-326),
 //                code +-1 applied as an fp64 sign flip (table of sign masks)
+//  chunked path (default when 15*step < 1): kC consecutive samples per lane
+//    and chunk, exact index of the chunk's first sample plus the exact
+//    crossing to the next chip, code by position, carrier as an LDS table
+//    W_n times one rotation per chunk (run_chunks below)
 //  reduction: wavefront xor-shuffles, per-wave partials in LDS (double
 //    buffered by epoch parity -> one barrier per epoch), every thread adds the
 //    wave partials in the same order and runs the loop filters itself, so the
