@@ -740,7 +740,6 @@ __global__ __launch_bounds__(256) void acq64_wipe_kernel(
     }
     __syncthreads();
     n_cls = s_nc;
-    cfreq = s_cf;
   } else {
     n_cls = *n_cls_dev;
   }
@@ -749,7 +748,8 @@ __global__ __launch_bounds__(256) void acq64_wipe_kernel(
        i += (long)gridDim.x * blockDim.x) {
     const int row = (int)(i / N), n = (int)(i % N);
     const int cls = row / n_blocks, blk = row % n_blocks;
-    const double f = cfreq[cls];
+    // (an LDS / global pointer select would make this a flat load)
+    const double f = fuse_n > 0 ? s_cf[cls] : cfreq[cls];
     const bool cplx = iq & GNSSCORR_IF_IQ, pk = iq & GNSSCORR_IF_PACKED2;
     const int ne = cplx ? 2 : 1;
     const long e0 = (long)blk * coh * N * ne;   // first element of the block
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   const int2 fm = fmap[group_freq[g * n_bins + bin]];
   const int m = fm.y;
   const double inv_n2 = 1.0 / ((double)N * (double)N);
-  const v2d* Fc0 = F + (long)code * rs;
+  const long fofs0 = (long)code * rs;
 
   double pw[K3][R3], pwl[2] = {-1.0, -1.0};   // pwl: leftover outputs (P::lvalid)
 
@@ -953,8 +953,12 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     // the code row is the same for every block: keep the compiler from
     // hoisting its loads out of the block loop (they would stay live in
     // registers across the whole transform)
-    const v2d* Fc = Fc0;
-    asm volatile("" : "+s"(Fc));
+    // (the offset, not the pointer, goes through the asm: an opaque pointer
+    // loses its global address space, and the code loads became flat loads,
+    // whose completion the waitcnt logic can only wait for all at once)
+    long fofs = fofs0;
+    asm volatile("" : "+s"(fofs));
+    const v2d* Fc = F + fofs;
     // likewise every thread-dependent address: t is opaque per block, so the
     // index arithmetic is redone per block instead of held across it
     int t = threadIdx.x;

@@ -940,9 +940,9 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
           // for two 1024-thread workgroups per CU.  The tail run (staged in
           // LDS) goes through the same loop with its missing pairs masked, so
           // it does not serialise behind the full runs of its wave.
-          const uint4* run = stage ? &s_ifq[tid * kPitch] : reinterpret_cast<const uint4*>(src);
 #ifdef TRACK_LOAD4   // round 2's "four loads at a time" variant (tools/gpu_mad.sh)
           if (!stage) {
+            const uint4* run = reinterpret_cast<const uint4*>(src);
 #pragma unroll 1
             for (int j = 0; j < kVec; j += 4) {
               const uint4 u0 = run[j], u1 = run[j + 1], u2 = run[j + 2], u3 = run[j + 3];
@@ -954,13 +954,26 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
           } else
 #endif
           {
-          uint4 nx = run[0];
+          // one loop per source, typed by address space: a pointer selected
+          // between the LDS stage and global memory is a generic pointer, and
+          // its loads became flat loads, which count in both vmcnt and lgkmcnt -- every wait for a
+          // LO-word or E/P/L-row read then also waited for the prefetch
+          typedef unsigned int V4U __attribute__((ext_vector_type(4)));
+          auto run_loop = [&](auto run) {
+            V4U nx = run[0];
 #pragma unroll 1
-          for (int j = 0; j < kVec; j++) {
-            const uint4 u = nx;
-            if (j + 1 < kVec) nx = run[j + 1];
-            chunk(u, j);
-          }
+            for (int j = 0; j < kVec; j++) {
+              const uint4 u = make_uint4(nx.x, nx.y, nx.z, nx.w);
+              if (j + 1 < kVec) nx = run[j + 1];
+              chunk(u, j);
+            }
+          };
+          typedef const __attribute__((address_space(3))) V4U* LdsU4;
+          typedef const __attribute__((address_space(1))) V4U* GlbU4;
+          if (stage)
+            run_loop((LdsU4)(&s_ifq[tid * kPitch]));
+          else
+            run_loop((GlbU4)(src));
           }
         } else if (PK && L == kRun) {
           // packed, unstaged (channels of a workgroup on different streams):
