@@ -21,7 +21,7 @@ def pick(d):
         if isinstance(v, dict):
             sub = {kk: vv for kk, vv in v.items() if kk in ('kern_ms', 'mean_us')}
             if sub: out[k] = sub
-        elif k in ('corr_ms', 'kern_ms', 'cl_ms', 'dt'):
+        elif k in ('corr_ms', 'kern_ms', 'cl_ms', 'lat_ms', 'dt'):
             out[k] = v
     return out
 print('$P $V$i', pick(d))
