@@ -81,10 +81,26 @@ __device__ __forceinline__ double uni(double v) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// wave total, uniform: DPP row_shr 1/2/4/8 (a Hillis-Steele scan in each
+// 16-lane row, 0.0 shifted in) leaves each row's sum in its lane 15 and the
+// four rows add in scalar registers -- VALU only, where a 64-bit __shfl_xor
+// butterfly is two ds_bpermute round trips per step.  Every lane must be active.
+template <int CTRL>
+__device__ __forceinline__ double dpp_shr(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_shr<0x111>(v);
+  v += dpp_shr<0x112>(v);
+  v += dpp_shr<0x114>(v);
+  v += dpp_shr<0x118>(v);
+  return (lane_f64(v, 15) + lane_f64(v, 31)) + (lane_f64(v, 47) + lane_f64(v, 63));
 }
 
 // WAVE: one wavefront per channel (many-channel launches): the butterfly sums
@@ -255,13 +271,23 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
       const double aX[3] = {uni(aE), uni(aP), uni(aL)};
       double sb, cb, sR, cR;
       sincos(A * ((double)(tid * kC - mis) / p.fs) + c.rem_carr, &sb, &cb);
-      sincos(A * ((double)(T * kC) / p.fs), &sR, &cR);
-      sR = uni(sR);
-      cR = uni(cR);
-      if (tid < kC) {
-        double swl, cwl;
-        sincos(A * ((double)tid / p.fs), &swl, &cwl);
-        s_w[tid] = make_double2(cwl, swl);
+      double swl = 0.0, cwl = 1.0;
+      if (WAVE || tid < kC) sincos(A * ((double)tid / p.fs), &swl, &cwl);   // W_tid
+      if (tid < kC) s_w[tid] = make_double2(cwl, swl);
+      if constexpr (WAVE) {
+        // the rotation by T*kC samples without a third sincos: lanes 63 and 0
+        // hold the carrier at k = 63 kC - mis and -mis, lane kC holds W_kC, so
+        // exp(i A 64 kC / fs) = e(63) * conj(e(0)) * W_kC (fp64 rounding only)
+        const double c63 = lane_f64(cb, 63), s63 = lane_f64(sb, 63);
+        const double c0 = lane_f64(cb, 0), s0 = lane_f64(sb, 0);
+        const double cK = lane_f64(cwl, kC), sK = lane_f64(swl, kC);
+        const double dc = fma(c63, c0, s63 * s0), ds = fma(s63, c0, -(c63 * s0));
+        cR = fma(dc, cK, -(ds * sK));
+        sR = fma(dc, sK, ds * cK);
+      } else {
+        sincos(A * ((double)(T * kC) / p.fs), &sR, &cR);
+        sR = uni(sR);
+        cR = uni(cR);
       }
       __syncthreads();
       double accI[3] = {0.0, 0.0, 0.0}, accQ[3] = {0.0, 0.0, 0.0};

@@ -220,7 +220,10 @@ def test_many_channels_launch_shape(gpu, reps):
     small = ch14.copy()
     e_big = ctx.track(d_if.ptr, 0, len(IF) // 2, big, 3, closed_loop=True)
     e_small = ctx.track(d_if.ptr, 0, len(IF) // 2, small, 3, closed_loop=True)
+    # The shapes rotate the carrier by T*kC samples per chunk pass (T = 64 / 256
+    # threads), from differently rounded fp64 angles of ~2.4e3 rad (ulp 4.5e-13):
+    # the phases drift apart by ~1e-12 rad per pass, ~1e-11 relative per epoch.
     for f in S.FIELDS:
         a = e_big[f].reshape(reps, 14, 3)
-        assert _close(a, np.broadcast_to(e_small[f], a.shape), rtol=1e-12, atol=1e-9).all(), f
+        assert _close(a, np.broadcast_to(e_small[f], a.shape), rtol=1e-10, atol=1e-8).all(), f
     assert (e_big["blksize"].reshape(reps, 14, 3) == e_small["blksize"]).all()
