@@ -58,9 +58,81 @@ constexpr int kMaxWaves = 16;
 
 struct SgtParams {
   int system, file_type, switch_iq, code_length, chunked;
+  int code_nco_variant, abs_sample_variant;   // tracking.sci:366/367, :379/:384
   double fs, code_basis, if_freq, l1_if_step, glo_zero, spc;
   double tau1, tau2, k1, k2, k3, pdi_code;
 };
+
+// End of one epoch of blk samples whose six sums are S (I_E, I_P, I_L, Q_E,
+// Q_P, Q_L): the carry-over (tracking.sci:301-313), and closed loop the
+// FLL-assisted PLL (:329-351) and the DLL (:353-375), then the record
+// (:377-398).  One definition for the tracking kernel and the sums-replay
+// kernel, so the replay against the reference's recorded run
+// (tests/test_sgt_trackres_gpu.py) checks the code the tracker runs.
+template <bool CLOSED>
+__device__ __forceinline__ gnsscorr_sgt_epoch sgt_epoch_end(const SgtParams& p,
+                                                            gnsscorr_sgt_chan& c, int blk,
+                                                            double step, const double (&S)[6]) {
+#pragma clang fp contract(off)
+  const double I_E = S[0], I_P = S[1], I_L = S[2], Q_E = S[3], Q_P = S[4], Q_L = S[5];
+  const double dL = (double)p.code_length, twopi = 2.0 * M_PI;
+  const double A = (c.carr_freq * 2.0) * M_PI;        // (carrFreq * 2.0 * %pi)
+  // carry-over (tracking.sci:301-313)
+  const double tlast = c.rem_code + (double)(blk - 1) * step;   // tcode(blksize), prompt range
+  c.rem_code = (tlast + step) - dL;
+  const double last = A * ((double)blk / p.fs) + c.rem_carr;
+  c.rem_carr = last - trunc(last / twopi) * twopi;
+  c.pos += blk;
+  double code_err = 0, carr_err = 0;
+  if (CLOSED) {
+    // FLL-assisted PLL (tracking.sci:329-353)
+    const double I2 = c.i1, Q2 = c.q1;
+    c.i1 = I_P; c.q1 = Q_P;
+    const double cross = c.i1 * Q2 - I2 * c.q1;
+    const double dot = fabs(c.i1 * I2 + c.q1 * Q2);
+    const double freq_err = atan2(cross, dot) / M_PI;
+    carr_err = atan(Q_P / I_P) / (2.0 * M_PI);
+    const double carr_nco = c.old_carr_nco + p.k1 * carr_err - p.k2 * c.old_carr_error -
+                            p.k3 * freq_err;
+    c.old_carr_nco = carr_nco;
+    c.old_carr_error = carr_err;
+    c.carr_freq = c.carr_freq_basis + carr_nco;
+    // DLL (tracking.sci:355-374)
+    const double aEm = sqrt(I_E * I_E + Q_E * Q_E), aLm = sqrt(I_L * I_L + Q_L * Q_L);
+    code_err = (aEm - aLm) / (aEm + aLm);
+    const double code_nco = c.old_code_nco + (p.tau2 / p.tau1) * (code_err - c.old_code_error) +
+                            code_err * (p.pdi_code / p.tau1);
+    c.old_code_nco = code_nco;
+    c.old_code_error = code_err;
+    if (p.code_nco_variant == 1) {
+      c.code_freq = p.code_basis - code_nco;               // :366, no carrier aiding
+    } else if (p.system == 1) {
+      const double fch = (double)c.code_id;                // :367-370
+      c.code_freq = p.code_basis - code_nco +
+                    (c.carr_freq - (p.if_freq + p.l1_if_step * fch)) /
+                        ((p.glo_zero + fch * p.l1_if_step) / p.code_basis);
+    } else {
+      c.code_freq = p.code_basis - code_nco + ((c.carr_freq - p.if_freq) / 1540);
+    }
+  }
+  c.n_epochs++;
+  gnsscorr_sgt_epoch r;
+  r.i_e = I_E; r.i_p = I_P; r.i_l = I_L; r.q_e = Q_E; r.q_p = Q_P; r.q_l = Q_L;
+  r.carr_freq = c.carr_freq;
+  r.code_freq = c.code_freq;
+  // :379 mtell(fid)/dataAdaptCoeff (the whole-sample position after the read)
+  // or :384 currentSample/dataAdaptCoeff - remCodePhase*(fs/1000)/codeLength
+  r.absolute_sample = p.abs_sample_variant == 1
+                          ? (double)c.pos
+                          : (double)c.pos - c.rem_code * (p.fs / 1000) / dL;
+  r.dll_discr = code_err;
+  r.dll_discr_filt = c.old_code_nco;
+  r.pll_discr = carr_err;
+  r.pll_discr_filt = c.old_carr_nco;
+  r.blksize = (int32_t)blk;
+  r.status = 0;
+  return r;
+}
 
 __device__ __forceinline__ int xcd_channel(int b, int G) {
   const int q = G >> 3, r = G & 7, x = b & 7, slot = b >> 3;
@@ -135,7 +207,6 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
   __syncthreads();
 
   const int8_t* base = ifbuf + (int64_t)c.stream * stride;
-  const double twopi = 2.0 * M_PI;
   const double dL = (double)L;
   int e = 0;
   for (; e < n_epochs; e++) {
@@ -423,61 +494,46 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
 #pragma unroll
         for (int j = 0; j < 6; j++) S[j] += s_part[par][w][j];
     }
-    const double I_E = S[0], I_P = S[1], I_L = S[2], Q_E = S[3], Q_P = S[4], Q_L = S[5];
-
-    // carry-over (tracking.sci:301-313)
-    const double tlast = aP + (double)(blk - 1) * step;   // tcode(blksize) of the prompt range
-    c.rem_code = (tlast + step) - dL;
-    const double last = A * ((double)blk / p.fs) + c.rem_carr;
-    c.rem_carr = last - trunc(last / twopi) * twopi;
-    c.pos += blk;
-    double code_err = 0, carr_err = 0;
-    if (CLOSED) {
-      // FLL-assisted PLL (tracking.sci:329-353)
-      const double I2 = c.i1, Q2 = c.q1;
-      c.i1 = I_P; c.q1 = Q_P;
-      const double cross = c.i1 * Q2 - I2 * c.q1;
-      const double dot = fabs(c.i1 * I2 + c.q1 * Q2);
-      const double freq_err = atan2(cross, dot) / M_PI;
-      carr_err = atan(Q_P / I_P) / (2.0 * M_PI);
-      const double carr_nco = c.old_carr_nco + p.k1 * carr_err - p.k2 * c.old_carr_error -
-                              p.k3 * freq_err;
-      c.old_carr_nco = carr_nco;
-      c.old_carr_error = carr_err;
-      c.carr_freq = c.carr_freq_basis + carr_nco;
-      // DLL (tracking.sci:355-374)
-      const double aEm = sqrt(I_E * I_E + Q_E * Q_E), aLm = sqrt(I_L * I_L + Q_L * Q_L);
-      code_err = (aEm - aLm) / (aEm + aLm);
-      const double code_nco = c.old_code_nco + (p.tau2 / p.tau1) * (code_err - c.old_code_error) +
-                              code_err * (p.pdi_code / p.tau1);
-      c.old_code_nco = code_nco;
-      c.old_code_error = code_err;
-      if (p.system == 1) {
-        const double fch = (double)c.code_id;
-        c.code_freq = p.code_basis - code_nco +
-                      (c.carr_freq - (p.if_freq + p.l1_if_step * fch)) /
-                          ((p.glo_zero + fch * p.l1_if_step) / p.code_basis);
-      } else {
-        c.code_freq = p.code_basis - code_nco + ((c.carr_freq - p.if_freq) / 1540);
-      }
-    }
-    c.n_epochs++;
-    if (tid == 0) {
-      gnsscorr_sgt_epoch r;
-      r.i_e = I_E; r.i_p = I_P; r.i_l = I_L; r.q_e = Q_E; r.q_p = Q_P; r.q_l = Q_L;
-      r.carr_freq = c.carr_freq;
-      r.code_freq = c.code_freq;
-      r.absolute_sample = (double)c.pos - c.rem_code * (p.fs / 1000) / dL;
-      r.dll_discr = code_err;
-      r.dll_discr_filt = c.old_code_nco;
-      r.pll_discr = carr_err;
-      r.pll_discr_filt = c.old_carr_nco;
-      r.blksize = (int32_t)blk;
-      r.status = 0;
-      *rec = r;
-    }
+    const gnsscorr_sgt_epoch r = sgt_epoch_end<CLOSED>(p, c, blk, step, S);
+    if (tid == 0) *rec = r;
   }
   if (tid == 0) chans[ch] = c;
+}
+
+// The loop half alone: each thread runs one channel's epochs on given sums
+// (sums[(ch*n_epochs + e)*6 + j]) instead of correlations of a record.  No
+// record bounds (there is no record); a NaN / negative / >= 2^31 blksize stops
+// the channel as in the tracking kernel.
+__global__ void sgt_replay_kernel(SgtParams p, gnsscorr_sgt_chan* __restrict__ chans, int n_ch,
+                                  int n_epochs, const double* __restrict__ sums,
+                                  gnsscorr_sgt_epoch* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= n_ch) return;
+  gnsscorr_sgt_chan c = chans[ch];
+  for (int e = 0; e < n_epochs; e++) {
+    gnsscorr_sgt_epoch* rec = out + (int64_t)ch * n_epochs + e;
+    if (c.status != 0) {
+      gnsscorr_sgt_epoch z = {};
+      z.status = 1;
+      *rec = z;
+      continue;
+    }
+    const double step = c.code_freq / p.fs;
+    const double blk_d = ceil(((double)p.code_length - c.rem_code) / step);
+    if (!(blk_d >= 0.0 && blk_d < 2147483648.0)) {
+      c.status = 1;
+      gnsscorr_sgt_epoch z = {};
+      z.status = 1;
+      z.blksize = -1;
+      *rec = z;
+      continue;
+    }
+    const double* sp = sums + ((int64_t)ch * n_epochs + e) * 6;
+    const double S[6] = {sp[0], sp[1], sp[2], sp[3], sp[4], sp[5]};
+    *rec = sgt_epoch_end<true>(p, c, (int)blk_d, step, S);
+  }
+  chans[ch] = c;
 }
 
 }  // namespace
@@ -513,9 +569,11 @@ static int check_cfg(const gnsscorr_sgt_cfg* cfg) {
   if (!cfg || (cfg->system != 0 && cfg->system != 1) ||
       (cfg->file_type != 1 && cfg->file_type != 2) || cfg->samp_rate <= 0 ||
       cfg->code_freq_basis <= 0 || cfg->dll_spacing < 0 || cfg->dll_spacing >= 1 ||
-      cfg->code_length != (cfg->system == 1 ? 511 : 1023)) {
+      cfg->code_length != (cfg->system == 1 ? 511 : 1023) ||
+      (cfg->code_nco_variant != 0 && cfg->code_nco_variant != 1) ||
+      (cfg->abs_sample_variant != 0 && cfg->abs_sample_variant != 1)) {
     gnsscorr_set_error("sgt: bad config (system 0/1, file_type 1/2, code_length 1023/511, "
-                       "0<=dll_spacing<1)");
+                       "0<=dll_spacing<1, variants 0/1)");
     return GNSSCORR_EINVAL;
   }
   return GNSSCORR_OK;
@@ -577,6 +635,8 @@ extern "C" int gnsscorr_sgt_create(gnsscorr_sgt_ctx** out, const gnsscorr_sgt_cf
   p.file_type = cfg->file_type;
   p.switch_iq = cfg->system == 1 ? cfg->switch_iq : 0;
   p.code_length = cfg->code_length;
+  p.code_nco_variant = cfg->code_nco_variant;
+  p.abs_sample_variant = cfg->abs_sample_variant;
   // GNSSCORR_SGT_CHUNK=0: the per-sample index path only (A/B and tests)
   const char* chk = getenv("GNSSCORR_SGT_CHUNK");
   p.chunked = !(chk && chk[0] == '0');
@@ -715,3 +775,56 @@ extern "C" int gnsscorr_sgt_sync(gnsscorr_sgt_ctx* c) {
 }
 
 extern "C" void* gnsscorr_sgt_stream(gnsscorr_sgt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int gnsscorr_sgt_replay_dev(gnsscorr_sgt_ctx* c, int n_ch, gnsscorr_sgt_chan* d_chan,
+                                       int n_epochs, const double* d_sums,
+                                       gnsscorr_sgt_epoch* d_ep) {
+  if (!c || !d_chan || !d_sums || !d_ep || n_ch < 1 || n_epochs < 1) {
+    gnsscorr_set_error("gnsscorr_sgt_replay_dev: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  hipLaunchKernelGGL(sgt_replay_kernel, dim3((n_ch + 63) / 64), dim3(64), 0, c->stream, c->p,
+                     d_chan, n_ch, n_epochs, d_sums, d_ep);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_sgt_replay(gnsscorr_sgt_ctx* c, int n_ch, gnsscorr_sgt_chan* h_chan,
+                                   int n_epochs, const double* h_sums, gnsscorr_sgt_epoch* h_ep) {
+  if (!c || !h_chan || !h_sums || !h_ep || n_ch < 1 || n_epochs < 1) {
+    gnsscorr_set_error("gnsscorr_sgt_replay: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  const size_t nc = (size_t)n_ch, ne = nc * (size_t)n_epochs;
+  gnsscorr_sgt_chan* d_chan = nullptr;
+  double* d_sums = nullptr;
+  gnsscorr_sgt_epoch* d_ep = nullptr;
+  hipError_t e = hipMalloc(&d_chan, nc * sizeof(gnsscorr_sgt_chan));
+  if (e == hipSuccess) e = hipMalloc(&d_sums, ne * 6 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&d_ep, ne * sizeof(gnsscorr_sgt_epoch));
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(d_chan, h_chan, nc * sizeof(gnsscorr_sgt_chan), hipMemcpyHostToDevice,
+                       c->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(d_sums, h_sums, ne * 6 * sizeof(double), hipMemcpyHostToDevice,
+                       c->stream);
+  int rc = GNSSCORR_OK;
+  if (e == hipSuccess) rc = gnsscorr_sgt_replay_dev(c, n_ch, d_chan, n_epochs, d_sums, d_ep);
+  if (e == hipSuccess && rc == GNSSCORR_OK)
+    e = hipMemcpyAsync(h_chan, d_chan, nc * sizeof(gnsscorr_sgt_chan), hipMemcpyDeviceToHost,
+                       c->stream);
+  if (e == hipSuccess && rc == GNSSCORR_OK)
+    e = hipMemcpyAsync(h_ep, d_ep, ne * sizeof(gnsscorr_sgt_epoch), hipMemcpyDeviceToHost,
+                       c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_chan);
+  (void)hipFree(d_sums);
+  (void)hipFree(d_ep);
+  if (e != hipSuccess) {
+    gnsscorr_set_error("gnsscorr_sgt_replay: %s", hipGetErrorString(e));
+    return GNSSCORR_EDEVICE;
+  }
+  return rc;
+}

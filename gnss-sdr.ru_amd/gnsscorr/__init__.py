@@ -142,7 +142,8 @@ class SgtCfg(C.Structure):
                 ("if_freq", C.c_double), ("l1_if_step", C.c_double),
                 ("glonass_zero_channel", C.c_double), ("dll_spacing", C.c_double),
                 ("dll_noise_bw", C.c_double), ("dll_damping", C.c_double),
-                ("pll_noise_bw", C.c_double), ("fll_noise_bw", C.c_double)]
+                ("pll_noise_bw", C.c_double), ("fll_noise_bw", C.c_double),
+                ("code_nco_variant", C.c_int32), ("abs_sample_variant", C.c_int32)]
 
 
 class SdrCorrCfg(C.Structure):
@@ -170,7 +171,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_acq_set_records",
     "gnsscorr_sgt_loop_coefs", "gnsscorr_sgt_init_chan", "gnsscorr_sgt_create",
     "gnsscorr_sgt_destroy", "gnsscorr_sgt_track_dev", "gnsscorr_sgt_track", "gnsscorr_sgt_sync",
-    "gnsscorr_sgt_stream",
+    "gnsscorr_sgt_stream", "gnsscorr_sgt_replay", "gnsscorr_sgt_replay_dev",
     "gnsscorr_sdr_prn_codes", "gnsscorr_sdr_sine_gen", "gnsscorr_sdr_acq_create",
     "gnsscorr_sdr_acq_destroy", "gnsscorr_sdr_acq_strong", "gnsscorr_sdr_acq_strong_dev",
     "gnsscorr_sdr_channel_start", "gnsscorr_sdr_channel_accum_dev", "gnsscorr_sdr_track_dev",
@@ -250,6 +251,8 @@ def lib() -> C.CDLL:
         "gnsscorr_sgt_destroy": (I, [P]),
         "gnsscorr_sgt_track_dev": (I, [P, P, I64, I64, I, P, I, I, P]),
         "gnsscorr_sgt_track": (I, [P, P, I64, I64, I, P, I, I, P]),
+        "gnsscorr_sgt_replay": (I, [P, I, P, I, P, P]),
+        "gnsscorr_sgt_replay_dev": (I, [P, I, P, I, P, P]),
         "gnsscorr_sgt_sync": (I, [P]),
         "gnsscorr_sgt_stream": (P, [P]),
         "gnsscorr_sdr_prn_codes": (I, [P]),
@@ -670,7 +673,7 @@ def sgt_cfg(system: int, device: int = 0, **kw) -> SgtCfg:
              L1_IF_step=0.5625e6 if glo else 0.0, GLONASS_zero_channel=1602e6 if glo else 0.0,
              dllCorrelatorSpacing=0.05 if glo else 0.2, dllNoiseBandwidth=0.5 if glo else 0.1,
              dllDampingRatio=0.7, pllNoiseBandwidth=25.0, fllNoiseBandwidth=250.0, fileType=2,
-             switchIQ=0)
+             switchIQ=0, codeNcoVariant=0, absSampleVariant=0)
     unknown = set(kw) - set(d) - {"system"}
     if unknown:
         raise ValueError(f"unknown settings {sorted(unknown)}")
@@ -678,7 +681,8 @@ def sgt_cfg(system: int, device: int = 0, **kw) -> SgtCfg:
     return SgtCfg(system, d["fileType"], d["switchIQ"], d["codeLength"], device, 0,
                   d["samplingFreq"], d["codeFreqBasis"], d["IF"], d["L1_IF_step"],
                   d["GLONASS_zero_channel"], d["dllCorrelatorSpacing"], d["dllNoiseBandwidth"],
-                  d["dllDampingRatio"], d["pllNoiseBandwidth"], d["fllNoiseBandwidth"])
+                  d["dllDampingRatio"], d["pllNoiseBandwidth"], d["fllNoiseBandwidth"],
+                  d["codeNcoVariant"], d["absSampleVariant"])
 
 
 class SgtCtx:
@@ -728,6 +732,18 @@ class SgtCtx:
         _check(lib().gnsscorr_sgt_track_dev(self.h, d_if, stride, n_samples, n_ch, d_chan,
                                             n_epochs, int(closed_loop), d_epochs),
                "gnsscorr_sgt_track_dev")
+
+    def replay(self, chans, sums):
+        """The loop half on given sums [n_ch, n_epochs, 6] (I_E, I_P, I_L, Q_E, Q_P,
+        Q_L); host channel array in/out; returns epochs [n_ch, n_epochs]."""
+        assert chans.dtype == SGT_CHAN and chans.flags.c_contiguous
+        sums = np.ascontiguousarray(sums, dtype=np.float64)
+        n_ch, n_ep = sums.shape[0], sums.shape[1]
+        assert sums.shape == (len(chans), n_ep, 6)
+        ep = np.zeros((n_ch, n_ep), SGT_EPOCH)
+        _check(lib().gnsscorr_sgt_replay(self.h, n_ch, _ptr(chans), n_ep, _ptr(sums), _ptr(ep)),
+               "gnsscorr_sgt_replay")
+        return ep
 
     def sync(self):
         _check(lib().gnsscorr_sgt_sync(self.h), "gnsscorr_sgt_sync")

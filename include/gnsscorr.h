@@ -391,6 +391,12 @@ typedef struct {          /* initSettings.sci fields used by tracking.sci     */
   double  dll_spacing;    /* settings.dllCorrelatorSpacing [chips]             */
   double  dll_noise_bw, dll_damping;   /* calcLoopCoef(dllNoiseBandwidth, dllDampingRatio, 1) */
   double  pll_noise_bw, fll_noise_bw;  /* calcFLLPLLLoopCoef(pll, fll, PDIcarr=0.001) */
+  /* tracking.sci variants; 0 = the current file for both.  The reference's
+   * recorded runs (GLONASS/L1,L2/trackingResults.dat) used 1 and 1. */
+  int32_t code_nco_variant;   /* 0: codeFreq with carrier aiding (:367-370, GPS :1540 form);
+                                 1: codeFreq = codeFreqBasis - codeNco (:366)          */
+  int32_t abs_sample_variant; /* 0: currentSample - remCodePhase*(fs/1000)/L (:384);
+                                 1: mtell(fid)/dataAdaptCoeff, whole samples (:379)    */
 } gnsscorr_sgt_cfg;
 
 typedef struct {          /* one tracking channel (tracking.sci:159-201 + loop state) */
@@ -438,6 +444,18 @@ int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx *ctx, const int8_t *d_if, int64_t st
 int gnsscorr_sgt_track(gnsscorr_sgt_ctx *ctx, const int8_t *d_if, int64_t stream_stride,
                        int64_t n_samples, int n_ch, gnsscorr_sgt_chan *h_chan, int n_epochs,
                        int closed_loop, gnsscorr_sgt_epoch *h_epochs);
+/* The loop half alone (tracking.sci:248-252, 301-313, 329-398): n_epochs
+ * epochs of n_ch channels driven by given correlator sums instead of a record,
+ * sums[(ch*n_epochs + e)*6 + j], j = I_E, I_P, I_L, Q_E, Q_P, Q_L.  Runs the
+ * same device code as the closed-loop tracker (blksize / remCodePhase chain,
+ * discriminators, filters, NCO frequencies, absoluteSample).  For a host that
+ * correlates elsewhere, and to replay a recorded trackResults.  _dev:
+ * device buffers, asynchronous on the context's stream; without: host
+ * buffers, synchronous. */
+int gnsscorr_sgt_replay_dev(gnsscorr_sgt_ctx *ctx, int n_ch, gnsscorr_sgt_chan *d_chan,
+                            int n_epochs, const double *d_sums, gnsscorr_sgt_epoch *d_epochs);
+int gnsscorr_sgt_replay(gnsscorr_sgt_ctx *ctx, int n_ch, gnsscorr_sgt_chan *h_chan,
+                        int n_epochs, const double *h_sums, gnsscorr_sgt_epoch *h_epochs);
 int gnsscorr_sgt_sync(gnsscorr_sgt_ctx *ctx);
 void *gnsscorr_sgt_stream(gnsscorr_sgt_ctx *ctx);
 

@@ -13,10 +13,21 @@ code[ceil(remCode -/+ spc + k*step) + 1] from the padded code [c(end) c c(1)];
 carrier exp(i*((2*pi*f)*t + remCarr)); I = sum(code*imag(carr*raw)),
 Q = sum(code*real(carr*raw)); then the FLL-assisted PLL and the DLL.
 
-Assumptions (unverifiable here): Scilab's `a:step:b` yields a + k*step
-(ImplicitList element formula), and complex products/sums are plain IEEE fp64.
-Parity status: no Scilab in the image -> "parity unpinned" against
-a Scilab run; pinned by planted-signal tracking KATs (tests/test_sgt_oracle.py).
+Assumptions: Scilab's `a:step:b` yields a + k*step (ImplicitList element
+formula), and complex products/sums are plain IEEE fp64.
+
+Parity status: the LOOP half (blksize / remCodePhase chain, FLL/PLL and DLL
+discriminators and filters, carrFreq, codeFreq, absoluteSample) is PINNED to
+the reference's own recorded runs: SCI/GLONASS/L1/trackingResults.dat and
+L2/trackingResults.dat (1500 epochs each, written by postProcessing.sce:143),
+replayed from their recorded sums by `replay` (tests/test_sgt_trackres.py):
+codeFreq, dllDiscr, dllDiscrFilt and absoluteSample equal the record
+bit-for-bit, carrFreq/pllDiscr/pllDiscrFilt to within the last-ulp atan
+difference of the Scilab build.  Those runs used the tracking.sci variants now
+commented out: codeFreq without carrier aiding (:366, `codeNcoVariant=1`)
+and absoluteSample = mtell/dataAdaptCoeff (:379, `absSampleVariant=1`).  The
+CORRELATOR half (the six sums) has no recorded input IF in the reference, so
+it stays pinned by planted-signal KATs only (tests/test_sgt_oracle.py).
 Only tests/, smoke() and bench.py's cpu_baseline use this module.
 """
 from __future__ import annotations
@@ -58,6 +69,10 @@ def settings(system: int, **kw) -> dict:
                  L1_IF_step=0.0, GLONASS_zero_channel=0.0, dllCorrelatorSpacing=0.2,
                  dllNoiseBandwidth=0.1, dllDampingRatio=0.7, pllNoiseBandwidth=25.0,
                  fllNoiseBandwidth=250.0, fileType=2, switchIQ=0)
+    # tracking.sci variants (both 0 = the current file): codeNcoVariant 1 =
+    # codeFreq = basis - codeNco (:366, no carrier aiding); absSampleVariant 1 =
+    # absoluteSample = mtell(fid)/dataAdaptCoeff, the whole-sample position (:379)
+    s.update(codeNcoVariant=0, absSampleVariant=0)
     s.update(kw)
     return s
 
@@ -108,53 +123,107 @@ def correlate(IF, s, code_pad, pos, rem_code, rem_carr, code_freq, carr_freq):
     return sums, blksize, pos + blksize, rem_code_n, rem_carr_n
 
 
-def track(IF, s, code_id, code_phase_1b, acquired_freq, n_ms, skip=0):
-    """tracking.sci per-channel loop for n_ms epochs.  code_id: GPS PRN or GLONASS FCH.
-    Returns a dict of FIELDS arrays (length = epochs actually processed) + 'blksize'."""
-    fs, L = s["samplingFreq"], s["codeLength"]
-    tau1, tau2 = calc_loop_coef(s["dllNoiseBandwidth"], s["dllDampingRatio"], 1.0)
-    k1, k2, k3 = calc_fll_pll_loop_coef(s["pllNoiseBandwidth"], s["fllNoiseBandwidth"], 0.001)
-    PDIcode = 0.001
-    code_pad = padded_code(s["system"], code_id)
-    pos = skip + code_phase_1b - 1                         # mseek, :163-168
-    code_freq = s["codeFreqBasis"]
-    rem_code = 0.0
-    carr_freq = carr_basis = acquired_freq
-    rem_carr = 0.0
-    old_code_nco = old_code_err = old_carr_nco = old_carr_err = 0.0
-    I1 = Q1 = 0.001
-    out = {f: [] for f in FIELDS}
-    out["blksize"] = []
-    for _ in range(n_ms):
-        r = correlate(IF, s, code_pad, pos, rem_code, rem_carr, code_freq, carr_freq)
-        if r is None:
-            break
-        (I_E, I_P, I_L, Q_E, Q_P, Q_L), blk, pos, rem_code, rem_carr = r
-        I2, Q2 = I1, Q1
-        I1, Q1 = I_P, Q_P
-        cross = I1 * Q2 - I2 * Q1
-        dot = abs(I1 * I2 + Q1 * Q2)
+class Loop:
+    """Per-channel loop state and the update after one epoch's sums
+    (tracking.sci:179-201 initial values, :329-398 per epoch)."""
+
+    def __init__(self, s, code_id, pos, acquired_freq):
+        self.s = s
+        self.tau1, self.tau2 = calc_loop_coef(s["dllNoiseBandwidth"], s["dllDampingRatio"], 1.0)
+        self.k1, self.k2, self.k3 = calc_fll_pll_loop_coef(s["pllNoiseBandwidth"],
+                                                           s["fllNoiseBandwidth"], 0.001)
+        self.code_id = code_id
+        self.pos = pos
+        self.code_freq = s["codeFreqBasis"]
+        self.rem_code = 0.0
+        self.carr_freq = self.carr_basis = acquired_freq
+        self.rem_carr = 0.0
+        self.old_code_nco = self.old_code_err = self.old_carr_nco = self.old_carr_err = 0.0
+        self.I1 = self.Q1 = 0.001
+
+    def blksize(self):
+        """tracking.sci:250-252."""
+        step = self.code_freq / self.s["samplingFreq"]
+        return int(math.ceil((self.s["codeLength"] - self.rem_code) / step)), step
+
+    def advance(self, blk, step, rem_carr_n=None):
+        """Carry-over of an epoch of blk samples (:258, :295-302, :309-310)."""
+        tP_last = self.rem_code + float(blk - 1) * step
+        self.rem_code = (tP_last + step) - self.s["codeLength"]
+        self.pos += blk
+        if rem_carr_n is not None:
+            self.rem_carr = rem_carr_n
+
+    def update(self, sums):
+        """FLL-assisted PLL + DLL on one epoch's sums (:329-398); returns the record
+        values in FIELDS order."""
+        s = self.s
+        I_E, I_P, I_L, Q_E, Q_P, Q_L = (float(x) for x in sums)
+        I2, Q2 = self.I1, self.Q1
+        self.I1, self.Q1 = I_P, Q_P
+        cross = self.I1 * Q2 - I2 * self.Q1
+        dot = abs(self.I1 * I2 + self.Q1 * Q2)
         freq_err = math.atan2(cross, dot) / math.pi
         carr_err = math.atan(Q_P / I_P) / (2.0 * math.pi)
-        carr_nco = old_carr_nco + k1 * carr_err - k2 * old_carr_err - k3 * freq_err
-        old_carr_nco, old_carr_err = carr_nco, carr_err
-        carr_freq = carr_basis + carr_nco
+        carr_nco = self.old_carr_nco + self.k1 * carr_err - self.k2 * self.old_carr_err - \
+            self.k3 * freq_err
+        self.old_carr_nco, self.old_carr_err = carr_nco, carr_err
+        self.carr_freq = self.carr_basis + carr_nco
         aE = math.sqrt(I_E * I_E + Q_E * Q_E)
         aL = math.sqrt(I_L * I_L + Q_L * Q_L)
         code_err = (aE - aL) / (aE + aL)
-        code_nco = old_code_nco + (tau2 / tau1) * (code_err - old_code_err) + \
-            code_err * (PDIcode / tau1)
-        old_code_nco, old_code_err = code_nco, code_err
-        if s["system"] == 1:
-            fch = code_id
-            code_freq = s["codeFreqBasis"] - code_nco + \
-                (carr_freq - (s["IF"] + s["L1_IF_step"] * fch)) / \
+        code_nco = self.old_code_nco + (self.tau2 / self.tau1) * (code_err - self.old_code_err) + \
+            code_err * (0.001 / self.tau1)
+        self.old_code_nco, self.old_code_err = code_nco, code_err
+        if s["codeNcoVariant"] == 1:
+            self.code_freq = s["codeFreqBasis"] - code_nco                      # :366
+        elif s["system"] == 1:
+            fch = self.code_id
+            self.code_freq = s["codeFreqBasis"] - code_nco + \
+                (self.carr_freq - (s["IF"] + s["L1_IF_step"] * fch)) / \
                 ((s["GLONASS_zero_channel"] + fch * s["L1_IF_step"]) / s["codeFreqBasis"])
         else:
-            code_freq = s["codeFreqBasis"] - code_nco + ((carr_freq - s["IF"]) / 1540)
-        abs_sample = pos - rem_code * (fs / 1000) / L
-        for f, v in zip(FIELDS, (I_E, I_P, I_L, Q_E, Q_P, Q_L, carr_freq, code_freq, abs_sample,
-                                 code_err, code_nco, carr_err, carr_nco)):
+            self.code_freq = s["codeFreqBasis"] - code_nco + ((self.carr_freq - s["IF"]) / 1540)
+        if s["absSampleVariant"] == 1:
+            abs_sample = float(self.pos)                                         # :379
+        else:
+            abs_sample = self.pos - self.rem_code * (s["samplingFreq"] / 1000) / s["codeLength"]
+        return (I_E, I_P, I_L, Q_E, Q_P, Q_L, self.carr_freq, self.code_freq, abs_sample,
+                code_err, code_nco, carr_err, carr_nco)
+
+
+def replay(sums, s, code_id, code_phase_1b, acquired_freq, skip=0):
+    """The loop half of tracking.sci driven by given per-epoch sums [n, 6]
+    (I_E, I_P, I_L, Q_E, Q_P, Q_L) instead of correlations of a record: blksize
+    and remCodePhase chain, discriminators, filters, NCO frequencies and
+    absoluteSample.  Pins the loop against a recorded trackResults."""
+    lp = Loop(s, code_id, skip + code_phase_1b - 1, acquired_freq)
+    out = {f: [] for f in FIELDS}
+    out["blksize"] = []
+    for row in np.asarray(sums, dtype=np.float64):
+        blk, step = lp.blksize()
+        lp.advance(blk, step)
+        for f, v in zip(FIELDS, lp.update(row)):
+            out[f].append(v)
+        out["blksize"].append(blk)
+    return {f: np.asarray(v) for f, v in out.items()}
+
+
+def track(IF, s, code_id, code_phase_1b, acquired_freq, n_ms, skip=0):
+    """tracking.sci per-channel loop for n_ms epochs.  code_id: GPS PRN or GLONASS FCH.
+    Returns a dict of FIELDS arrays (length = epochs actually processed) + 'blksize'."""
+    code_pad = padded_code(s["system"], code_id)
+    lp = Loop(s, code_id, skip + code_phase_1b - 1, acquired_freq)   # mseek, :163-168
+    out = {f: [] for f in FIELDS}
+    out["blksize"] = []
+    for _ in range(n_ms):
+        r = correlate(IF, s, code_pad, lp.pos, lp.rem_code, lp.rem_carr, lp.code_freq,
+                      lp.carr_freq)
+        if r is None:
+            break
+        sums, blk, pos, rem_code, rem_carr = r
+        lp.pos, lp.rem_code, lp.rem_carr = pos, rem_code, rem_carr
+        for f, v in zip(FIELDS, lp.update(sums)):
             out[f].append(v)
         out["blksize"].append(blk)
     return {f: np.asarray(v) for f, v in out.items()}
