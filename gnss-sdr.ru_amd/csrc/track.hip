@@ -727,6 +727,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
     int stage_ok) {
   __shared__ uint2 s_lo[64];
   __shared__ int s_stream[kMaxCpw];
+  __shared__ int s_short[kMaxCpw];
   // dynamic LDS: [cpw][ep_cap][6] epoch sums | [cpw][kPk8Stage] E/P/L row bytes |
   // staged IF runs (lane runs of 128 B at a 144 B pitch)
   extern __shared__ uint4 s_dyn[];
@@ -776,6 +777,13 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
     else c.j1 = kNever;  // uint16 half-chip can never reach D
   }
   c.base = (active ? cmd.prn : 0) * GNSSCORR_OSG_ROW;
+  // A lane of the piece path covers kPieceSpan + kPieceLen samples (two pieces)
+  // and holds at most one dump.  Two consecutive dumps are D code carries
+  // apart, at least D * 2^32 / kinc2 - 1 samples: a channel whose epoch can be
+  // that short (about 2.05-2.08 Msps, one half-chip per sample) sends its
+  // workgroup to the per-thread 64-sample runs, which hold one dump at most.
+  if (tid == 0)
+    s_short[q] = active && ((uint64_t)c.D << 32) <= (uint64_t)(kPieceSpan + kPieceLen + 1) * c.kinc2;
   TRACK_PSTAMP(1);
   const uint64_t Rtot = ((uint64_t)c.K0 + (uint64_t)nsamp * c.kinc2) >> 32;
   const uint32_t ndump = n_dumps_after(c, Rtot);
@@ -809,9 +817,10 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   s_pk8 += c.base & 3;
   __syncthreads();
   int sst = -1;
-  bool uni = true;
+  bool uni = true, any_short = false;
   for (int k = 0; k < cpw; k++) {
     const int v = s_stream[k];
+    any_short |= s_short[k] != 0;
     if (v >= 0) {
       if (sst < 0) sst = v;
       else if (v != sst) uni = false;
@@ -825,7 +834,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   // (stage_ok 3: A/B, round-2 lane reads for mixed streams; 4: A/B, the piece
   // path for every workgroup)
   const bool shared_stage = IQ && stage_ok && stage_ok != 4 && uni && sst >= 0;
-  const bool pieces = IQ && (stage_ok == 1 || stage_ok == 4) && !shared_stage;
+  const bool pieces = IQ && (stage_ok == 1 || stage_ok == 4) && !shared_stage && !any_short;
   const bool stage = shared_stage;
   uint4* s_ifq = s_if;
   if (stage) {

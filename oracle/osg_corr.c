@@ -102,6 +102,13 @@ void osgo_ch_code(osgo_t *o, int ch, long freq)
 }
 int osgo_reg_read(const osgo_t *o, int addr) { return (short)o->reg_read[addr & 0xFF]; }
 
+/* Optional log of every dump (test-only: the reference latches only the last
+ * dump of a call in REG_read); entries {ch, IL, QL, IP, QP, IE, QE}. */
+static int32_t *g_dlog;
+static int g_dcap, g_dn;
+void osgo_dump_log(int32_t *buf, int cap) { g_dlog = buf; g_dcap = cap; g_dn = 0; }
+int  osgo_dump_count(void) { return g_dn; }
+
 /* ---- Sim_GP2021_int restated (correlator.c:148-316) --------------------- */
 void osgo_sim(osgo_t *o, const int8_t *IF, long nsamp)
 {
@@ -162,6 +169,11 @@ void osgo_sim(osgo_t *o, const int8_t *IF, long nsamp)
         if (h >= slew_dump) {
           int r = (ch << 3) + 0x84;
           for (int k = 0; k < 6; k++) o->reg_read[r + k] = a[k];
+          if (g_dlog && g_dn < g_dcap) {
+            g_dlog[7 * g_dn] = ch;
+            for (int k = 0; k < 6; k++) g_dlog[7 * g_dn + 1 + k] = a[k];
+            g_dn++;
+          }
           o->reg_write[r] = 0;
           for (int k = 0; k < 6; k++) a[k] = 0;
           o->half_chip[ch] = 0;

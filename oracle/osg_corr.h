@@ -37,6 +37,10 @@ void osgo_table_image(int8_t *out);
 
 void osgo_init(osgo_t *o, int n_channels, int use_iq, double samp_rate, double tic_period);
 void osgo_sim(osgo_t *o, const int8_t *IF, long nsamp);
+/* Test-only: log every dump of later osgo_sim calls into buf (cap entries of 7
+ * int32 {ch, IL, QL, IP, QP, IE, QE}); NULL stops logging.  Not thread-safe. */
+void osgo_dump_log(int32_t *buf, int cap);
+int  osgo_dump_count(void);
 
 /* Register accessors mirroring gp2021/gp2021.c:11-130 (host side). */
 void osgo_ch_cntl(osgo_t *o, int ch, int prn);

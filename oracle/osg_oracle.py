@@ -96,6 +96,20 @@ class OracleOSG:
         IF = np.ascontiguousarray(IF, np.int8)
         self.L.osgo_sim(self.p, IF.ctypes.data, nsamp)
 
+    def sim_dumps(self, IF: np.ndarray, nsamp: int, cap: int = 4096) -> np.ndarray:
+        """sim() that also returns EVERY dump of the call, [n, 7] int32
+        {ch, IL, QL, IP, QP, IE, QE} in sample order (REG_read keeps the last)."""
+        log = np.zeros((cap, 7), np.int32)
+        self.L.osgo_dump_log.argtypes = [C.c_void_p, C.c_int]
+        self.L.osgo_dump_count.restype = C.c_int
+        self.L.osgo_dump_log(log.ctypes.data, cap)
+        try:
+            self.sim(IF, nsamp)
+            n = self.L.osgo_dump_count()
+        finally:
+            self.L.osgo_dump_log(None, 0)
+        return log[:n].copy()
+
     def chan_state(self):
         s = self._st
         n = self.n_channels

@@ -134,6 +134,101 @@ def test_one_stream_per_channel_vs_oracle(gpu, oracle, per_channel_layout):
             np.testing.assert_array_equal(st[key][c], ref_state[c][key][0], err_msg=f"{key} ch{c}")
 
 
+# code NCO words for low sample rates: at fs = 4.092 Msps a half-chip is 2
+# samples (kinc2 = 2^31), at 2.048 Msps about one (kinc2 ~ 0.999 * 2^32).  There
+# an epoch of D >= 2046 half-chips can be as short as a piece-path lane's span
+# of 2080 samples (two 32-sample pieces 2048 apart), so those channels must
+# not take the per-wave piece path (track.hip: s_short).
+LOW_RATES = {"4.092": 1 << 30, "2.048": int(round((1 << 31) * 2.046 / 2.048))}
+
+
+def _low_rate_cmds(rng, n_calls, C, code_incr, slews):
+    cmds = _random_cmds(rng, n_calls, C, C)
+    for k in range(n_calls):
+        cmds[k]["stream"] = np.arange(C)
+        cmds[k]["code_incr"] = code_incr + rng.integers(-20000, 20000, size=C)
+        cmds[k]["slew"] = slews
+    return cmds
+
+
+def _layout_streams(streams, nsamp, n_calls):
+    stride = ((nsamp * n_calls * 2 + 63) // 64) * 64 // 2
+    buf = np.ones(stride * 2 * len(streams), np.int8)
+    for i, st in enumerate(streams):
+        buf[i * stride * 2: i * stride * 2 + len(st)] = st
+    return buf, stride
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("rate", sorted(LOW_RATES))
+@pytest.mark.parametrize("nsamp", [5000, 16368])
+def test_low_rate_one_stream_per_channel_all_dumps_vs_oracle(gpu, oracle, rate, nsamp, packed):
+    """C_s = 1 at 4.092 / 2.048 Msps code rates, no slew: EVERY dump of every
+    call equals the oracle's (its dump log: REG_read latches only the last)."""
+    rng = np.random.default_rng(11 + nsamp + 3 * packed)
+    C, n_calls = 40, 2
+    streams = [S.synth_if(nsamp * n_calls, 500 + i, [(i % 32 + 1, 37 * i, 0, 3)]) for i in range(C)]
+    cmds = _low_rate_cmds(rng, n_calls, C, LOW_RATES[rate], 0)
+    buf, stride = _layout_streams(streams, nsamp, n_calls)
+    ctx = gpu.TrackCtx(C, iq=True, max_nsamp=nsamp, packed=packed)
+    got = []
+    for k in range(n_calls):
+        chunk = buf[k * nsamp * 2:]
+        res, _, d = ctx.track(gpu.pack2(chunk) if packed else chunk, nsamp, cmds[k], n_streams=C,
+                              stream_stride=stride, all_dumps=True)
+        got.append((res["n_dumps"].copy(), d.copy()))
+    st = ctx.get_state()
+    multi = 0
+    for c in range(C):
+        o = oracle.OracleOSG(1, True, 16.368e6, 0.0)
+        rw = o.REG_write
+        rw[7] = -1
+        for k in range(n_calls):
+            cm = cmds[k, c]
+            rw[0] = cm["prn"]
+            rw[3], rw[4] = int(cm["carrier_incr"]) >> 16, int(cm["carrier_incr"]) & 0xFFFF
+            rw[5], rw[6] = int(cm["code_incr"]) >> 16, int(cm["code_incr"]) & 0xFFFF
+            rw[0x84] = 0
+            want = o.sim_dumps(streams[c][k * nsamp * 2:(k + 1) * nsamp * 2], nsamp)[:, 1:]
+            nd, d = got[k]
+            assert nd[c] == len(want), (c, k, nd[c], len(want))
+            np.testing.assert_array_equal(d[c, :nd[c]], want, err_msg=f"ch{c} call{k}")
+            multi += len(want) >= 2
+        ref = o.chan_state()
+        for key in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+            np.testing.assert_array_equal(st[key][c], ref[key][0], err_msg=f"{key} ch{c}")
+    if not (rate == "4.092" and nsamp < 8184):   # (a 4092-sample epoch: 1-2 per call)
+        assert multi >= C // 2      # most calls of active channels hold several dumps
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("rate", sorted(LOW_RATES))
+def test_low_rate_one_stream_per_channel_slews_vs_oracle(gpu, oracle, rate, packed):
+    """Same rates with slews around the piece path's limit (D = 2046 + slew
+    against a 2080-sample lane span) and beyond the staged E/P/L row: last dump,
+    dump flags and channel state bit-exact over 3 calls of 16368 samples."""
+    rng = np.random.default_rng(23 + 5 * packed)
+    C, nsamp, n_calls = 42, 16368, 3
+    streams = [S.synth_if(nsamp * n_calls, 700 + i, [(i % 32 + 1, 41 * i, 0, 3)]) for i in range(C)]
+    slews = np.resize(np.array([0, 30, 34, 35, 36, 40, 200, 1100, 3000], np.uint32), C)
+    cmds = _low_rate_cmds(rng, n_calls, C, LOW_RATES[rate], slews)
+    ref, ref_nd, ref_state = _oracle_channels(oracle, streams, nsamp, cmds)
+    buf, stride = _layout_streams(streams, nsamp, n_calls)
+    ctx = gpu.TrackCtx(C, iq=True, max_nsamp=nsamp, packed=packed)
+    for k in range(n_calls):
+        chunk = buf[k * nsamp * 2:]
+        res, _ = ctx.track(gpu.pack2(chunk) if packed else chunk, nsamp, cmds[k], n_streams=C,
+                           stream_stride=stride)
+        got_nd = (res["n_dumps"] > 0).astype(np.int32)
+        np.testing.assert_array_equal(got_nd, ref_nd[k])
+        m = got_nd == 1
+        np.testing.assert_array_equal(res["dump"][m], ref[k][m])
+    st = ctx.get_state()
+    for c in range(C):
+        for key in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+            np.testing.assert_array_equal(st[key][c], ref_state[c][key][0], err_msg=f"{key} ch{c}")
+
+
 def test_chunking_invariance_full_size(gpu):
     """One 16368-sample call == two 8184-sample calls (4096 channels)."""
     rng = np.random.default_rng(3)
