@@ -70,6 +70,14 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 // ---- compile-time arithmetic -------------------------------------------------
 constexpr double kPi = 3.14159265358979323846264338327950288;
 
+// LDS one workgroup may allocate on the build's offload arch: the library is
+// built for gfx950 only (Makefile ARCH), where a workgroup may take the CU's
+// whole 160 KiB.  acq64_corr_kernel sizes its parked non-coherent sums from it.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "acq64.hip sizes its LDS for gfx950 (160 KiB per workgroup)"
+#endif
+constexpr int kLdsBudget = 160 * 1024;
+
 constexpr double poly_sin(double x) {   // |x| <= pi/4, 1 ulp
   double x2 = x * x, term = x, sum = x;
   for (int i = 1; i < 12; i++) {
@@ -919,13 +927,16 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   // beside the exchange plane for the whole row (the others are parked in the
   // plane between blocks, see start_sums)
   constexpr int kLdsOther = N * 8 + P::LS * 16 + R3 * 16 + P::NW * 20 + 256;
-  constexpr int kE0 = kNC ? (163840 - kLdsOther) / (8 * T) : 0;
+  constexpr int kE0 = kNC ? (kLdsBudget - kLdsOther) / (8 * T) : 0;
   constexpr int kE = kE0 < K3 * R3 ? kE0 : K3 * R3;
   __shared__ double lds[N + kE * T];   // the exchange plane, then s_extra
   __shared__ v2d side[P::LS];
   __shared__ v2d tw3[R3];
   __shared__ double s_v[P::NW], s_m[P::NW];
   __shared__ int s_k[P::NW];
+  static_assert(sizeof(double) * (N + kE * T) + sizeof(v2d) * (P::LS + R3) +
+                        (2 * sizeof(double) + sizeof(int)) * P::NW <= (size_t)kLdsBudget,
+                "acq64_corr_kernel: static LDS over the gfx950 budget");
   double* const s_extra = lds + N;
   const int t = threadIdx.x;
   const bool act = t < T;

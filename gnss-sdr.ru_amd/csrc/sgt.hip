@@ -204,6 +204,9 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
   for (int i = tid; i < L + 2; i += T) {
     s_sgn[i] = codes[row * kPadLen + i] ? -1.0 : 1.0;   // sign-bit masks of the table
   }
+  // one guard entry past the padded table (a copy of entry L+1): the unclamped
+  // in_table path relies on a rounding argument to stay within [0, L+1]
+  if (tid == 0) s_sgn[L + 2] = codes[row * kPadLen + L + 1] ? -1.0 : 1.0;
   __syncthreads();
 
   const int8_t* base = ifbuf + (int64_t)c.stream * stride;
@@ -701,7 +704,7 @@ extern "C" int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx* c, const int8_t* d_if, i
     if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) T = v;
   }
   dim3 grid(n_ch), block(T);
-  const size_t tab = (size_t)(c->p.code_length + 2) * sizeof(double);   // s_sgn
+  const size_t tab = (size_t)(c->p.code_length + 3) * sizeof(double);   // s_sgn + guard
 #define SGT_LAUNCH(FT, CL)                                                                     \
   do {                                                                                         \
     if (T == 64)                                                                               \

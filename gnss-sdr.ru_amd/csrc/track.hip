@@ -1224,10 +1224,23 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   // IF copy).  The 1.5-round tail at 3072 channels (768 workgroups, 512
   // resident) is cheaper than smaller workgroups (MI355X, 3072 x 1 ms:
   // cpw 4 33.4 us, 3 35.2, 2 34.1, 1 46.4); GNSSCORR_TRACK_CPW overrides.
-  int cpw = min(kMaxCpw, kMaxThreads / threads);
-  if (c->cpw_override > 0) cpw = min(cpw, c->cpw_override);
-  // the LDS must fit beside the static LDS (s_lo, s_stream: < 1 KiB)
-  while (cpw > 1 && lds_bytes(cpw) + 1024 > c->lds_max) cpw--;
+  int cpw = 1;
+  auto pick_cpw = [&]() {
+    cpw = min(kMaxCpw, kMaxThreads / threads);
+    if (c->cpw_override > 0) cpw = min(cpw, c->cpw_override);
+    // the LDS must fit beside the static LDS (s_lo, s_stream, s_short: < 1 KiB)
+    while (cpw > 1 && lds_bytes(cpw) + 1024 > c->lds_max) cpw--;
+  };
+  pick_cpw();
+  if (stage && lds_bytes(cpw) + 1024 > c->lds_max) {   // no room for the IF stage or
+    stage = 0;                                          // the piece slots: lane reads
+    pick_cpw();
+  }
+  if (lds_bytes(cpw) + 1024 > c->lds_max) {
+    gnsscorr_set_error("gnsscorr_track: nsamp %lld needs %zu B of LDS per workgroup, the device "
+                       "allows %zu", (long long)nsamp, lds_bytes(cpw) + 1024, c->lds_max);
+    return GNSSCORR_EINVAL;
+  }
   dim3 grid((C + cpw - 1) / cpw), block(threads * cpw);
   const size_t dyn = lds_bytes(cpw);
 #define TRACK_LAUNCH(IQ, PK, ST)                                                               \
@@ -1376,10 +1389,16 @@ extern "C" int gnsscorr_device_lds_bytes(int device) {
   int blk = 0, cu = 0;
   if (hipDeviceGetAttribute(&blk, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess)
     blk = 0;
-  if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) !=
-      hipSuccess)
-    cu = 0;
-  return blk > cu ? blk : cu;
+  // gfx950 lets one workgroup allocate the CU's whole 160 KiB LDS, while the
+  // runtime's per-block attribute may report the older 64 KiB; elsewhere the
+  // per-block attribute is the limit
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess &&
+      strncmp(prop.gcnArchName, "gfx950", 6) == 0 &&
+      hipDeviceGetAttribute(&cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) ==
+          hipSuccess && cu > blk)
+    return cu;
+  return blk;
 }
 
 extern "C" int gnsscorr_device_count(void) {

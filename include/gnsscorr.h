@@ -39,8 +39,9 @@ const char *gnsscorr_version(void);
 /* Number of visible HIP devices (0 on a CPU-only host; never initialises
  * more than hipGetDeviceCount does). */
 int gnsscorr_device_count(void);
-/* LDS bytes one workgroup may allocate on a device (the larger of HIP's
- * per-block and per-CU attributes: 160 KiB on gfx950); 0 if it cannot be read.
+/* LDS bytes one workgroup may allocate on a device: 160 KiB on gfx950 (the
+ * per-CU attribute; the per-block one may report 64 KiB there), HIP's
+ * per-block attribute elsewhere; 0 if it cannot be read.
  * Kernels that size their LDS at launch (per-channel IF staging) check it. */
 int gnsscorr_device_lds_bytes(int device);
 /* PCI bus id ("0000:xx:00.0") of a device, for run records. */

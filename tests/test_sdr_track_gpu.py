@@ -126,6 +126,30 @@ def test_track_split_launches(gpu, loop):
     assert len(n1) + len(n2) == len(L["out"]["events"])
 
 
+@pytest.mark.parametrize("cpw", ["5", "7", "16"])
+def test_track_channels_per_wave_equal_one(gpu, loop, cpw, monkeypatch):
+    """cpw > 1 (several channels per wavefront: each lane runs its channel's
+    scalar chain, the wave runs the posted Accum segments one channel after
+    the other -- the bench's 3072-channel shape) equals the cpw = 1 launch of
+    the fixture bit for bit: states, correlations, Channel objects, the per-dump
+    log and the subframe events.  24 channels are not a multiple of 5, 7 or 16,
+    so the last wave runs a partial set."""
+    L = loop
+    monkeypatch.setenv("GNSSCORR_SDR_LOOP_CPW", cpw)
+    st, corr, ch = L["st0"].copy(), np.zeros(len(L["chans"]), gpu.SDR_CORR), L["ch0"].copy()
+    out = L["ctx"].track(L["pk"], st, corr, ch, rx=L["rx"], log_per_ch=2 * L["K"] + 2)
+    assert st.tobytes() == L["st"].tobytes()
+    assert corr.tobytes() == L["corr"].tobytes()
+    assert ch.tobytes() == L["ch"].tobytes()
+    ref = L["out"]
+    np.testing.assert_array_equal(out["n_log"], ref["n_log"])
+    for c in range(len(L["chans"])):
+        m = int(ref["n_log"][c])
+        assert out["log"][c, :m].tobytes() == ref["log"][c, :m].tobytes(), c
+    key = lambda e: (int(e["chan"]), int(e["sv"]), int(e["subframe"]), e["word_buff"].tobytes())
+    assert sorted(map(key, out["events"])) == sorted(map(key, ref["events"]))
+
+
 def test_track_channel_kill(gpu):
     """A channel killed by the channel (state EMPTY -> kill) stops its correlator
     as ProcessFeedback's memset does; the other channels are unaffected."""

@@ -81,6 +81,48 @@ def test_open_loop_epoch_matches_oracle(gpu, system, file_type, switch, threads,
     assert (ch["code_freq"] == ch0["code_freq"]).all()
 
 
+@pytest.mark.parametrize("fs", [4.096e6, 2.048e6])
+@pytest.mark.parametrize("system", [1, 0])
+def test_open_loop_low_rate_unclamped_path(gpu, system, fs):
+    """Low sample rates (fewer than ~15 samples per chip): the chunked path does
+    not apply and the per-sample index path runs without its clamp (in_table),
+    reading the code table by the exact ceil(remCode -/+ spc + k*step) indices;
+    remCode over the whole [0, step) range.  Indices and state bit-exact, sums
+    within 1e-6 (tracking.sci:281-302)."""
+    gc = gpu
+    rng = np.random.default_rng(int(fs) % 1000 + system)
+    n = int(fs * 0.012)
+    IF = gc.ifgen(n, [], fs=fs, seed=44)
+    d_if = gc.DevBuf.from_array(IF)
+    ctx = gc.SgtCtx(system, samplingFreq=fs)
+    s = S.settings(system, samplingFreq=fs)
+    C = 64
+    ids = rng.integers(-7, 7, C) if system == 1 else rng.integers(1, 33, C)
+    ch = np.zeros(C, gc.SGT_CHAN)
+    ch["code_id"] = ids
+    ch["pos"] = rng.integers(0, n - int(fs * 0.0012), C)
+    ch["code_freq"] = s["codeFreqBasis"] + rng.uniform(-40, 40, C)
+    step = ch["code_freq"] / fs
+    ch["rem_code"] = rng.uniform(0, 1, C) * step
+    ch["rem_code"][:4] = 0.0
+    ch["rem_code"][4:8] = np.nextafter(step[4:8], 0)
+    ch["rem_carr"] = rng.uniform(-6.2, 6.2, C)
+    ch["carr_freq"] = rng.uniform(-1e6, 1e6, C)
+    ch0 = ch.copy()
+    ep = ctx.track(d_if.ptr, 0, n, ch, 1, closed_loop=False)[:, 0]
+    for i in range(C):
+        pad = S.padded_code(system, int(ids[i]))
+        sums, blk, pos, rc, rcar = S.correlate(IF, s, pad, int(ch0["pos"][i]),
+                                               float(ch0["rem_code"][i]),
+                                               float(ch0["rem_carr"][i]),
+                                               float(ch0["code_freq"][i]),
+                                               float(ch0["carr_freq"][i]))
+        assert ep["status"][i] == 0 and ep["blksize"][i] == blk
+        assert ch["pos"][i] == pos and ch["rem_code"][i] == rc and ch["rem_carr"][i] == rcar
+        got = np.array([ep[f][i] for f in SUMS])
+        assert _close(got, sums).all(), (i, got, sums)
+
+
 @pytest.mark.parametrize("chunk", ["1", "0"])
 @pytest.mark.parametrize("system,file_type", [(1, 2), (0, 2), (1, 1)])
 def test_open_loop_crossings_on_exact_chips(gpu, system, file_type, chunk, monkeypatch):
