@@ -486,8 +486,38 @@ def run_fullsky(dist, dev, steps, warmup):
         res = merge(allres)
         found = sum(1 for p in gps if res[int(p) - 1][3]["metric"] > 2.5) + \
             sum(1 for k in glo if res[32 + int(k) + 7][3]["metric"] > 2.5)
+    proj = None
+    if dist.world == 1:
+        del fsky
+        proj = fullsky_shard_projection(dev, if_gps, if_glo, steps, dt / steps)
     return dict(dt=dt, steps=steps, found=found, n_planted=len(gps) + len(glo),
-                cells=46 * N_BINS * N * 10)
+                cells=46 * N_BINS * N * 10, projection=proj)
+
+
+def fullsky_shard_projection(dev, if_gps, if_glo, steps, t1):
+    """The strong-scaling curve of config 5 measured shard by shard on one GPU: for
+    world = 2, 4, 8 every rank's shard (gnsscorr/fullsky.py round-robin) is searched
+    alone, one after another, and the slowest rank sets that world's search time
+    (the shards share no data and need no collective, so a rank's time on its own
+    GPU is its time alone on this one)."""
+    from gnsscorr.fullsky import FullSky
+    out = {"world_1_ms": t1 * 1e3}
+    for w in (2, 4, 8):
+        per = []
+        for r in range(w):
+            f = FullSky(FS, 10, N_BINS, rank=r, world=w, device=dev)
+            f.load(if_gps, if_glo)
+            f.run()
+            f.sync()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                f.run()
+            f.sync()
+            per.append((time.perf_counter() - t0) / steps)
+            del f
+        out[f"world_{w}"] = {"max_rank_ms": max(per) * 1e3, "min_rank_ms": min(per) * 1e3,
+                             "speedup": t1 / max(per), "efficiency": t1 / max(per) / w}
+    return out
 
 
 GLO_COH, GLO_BAND_KHZ = 5, 12.0   # GLONASS initSettings.sci: acqCohIntegration 5, acqSearchBand 12
@@ -1305,6 +1335,7 @@ def main():
                           f"sharded round-robin over {W} GPU(s), results gathered over gloo",
                 "planted_found": f"{sky['found']}/{sky['n_planted']}",
                 "dtype": "f64",
+                "shard_projection": sky["projection"],
                 "roofline": {"bound": "valu", "kernel": "acq64_corr_kernel<PlanA, NONCOHERENT>",
                              "achieved": sky_flop / (sky_ms * 1e-3) / 1e12 / W,
                              "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64, per GPU)",

@@ -24,6 +24,7 @@
 // One workgroup = one channel x one call.  256 threads x 64 samples covers a
 // 1-ms chunk at 16.368 Msps; IF is read as 16-byte vector loads.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <limits.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -45,6 +46,13 @@
 #ifndef TRACK_PSTAMP
 #define TRACK_PSTAMP(i) \
   do {                  \
+  } while (0)
+#endif
+
+// Diagnostic hook of osg_stream_kernel (tools/trk_stream_stamps.hip; a no-op here)
+#ifndef STREAM_PSTAMP
+#define STREAM_PSTAMP(i) \
+  do {                   \
   } while (0)
 #endif
 
@@ -1050,6 +1058,386 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
 
 
 
+// ============================================================================
+// osg_stream_kernel: ONE WAVEFRONT PER CHANNEL AND CALL (interleaved I,Q
+// streams, int8 or 2-bit packed; round 4).
+//
+// The wave walks its channel's call in pieces of 2048 samples (lane l takes
+// the contiguous samples [2048 p + 32 l, +32) of piece p), with the next
+// piece already on its way while the current one is correlated:
+//   * int8: LDS-DMA (global_load_lds_dwordx4, 4 wave-instructions of 1 KiB of
+//     consecutive IF each) into the wave's 4 KiB slot; after the piece has
+//     landed the lanes copy their 64 bytes to registers and the DMA of the
+//     next piece is issued into the same slot;
+//   * packed: the lane's 16 bytes straight into registers, one piece ahead.
+// Each piece runs the branch-free interval form of run_pieces (pair2 /
+// interval_end: at most one code carry per 6 samples) when a half-chip lasts
+// >= 6 samples and the channel's E/P/L row fits the LDS stage, else the
+// per-sample reference recurrence.  A lane carries ONE set of six running sums
+// (its current epoch) across all its pieces; at an epoch change -- a dump
+// inside its samples, or a later piece that starts in a later epoch -- it adds
+// them into the wave's per-epoch LDS sums with LDS atomics (behind a
+// wave-uniform branch: dumps are rare) and starts over.  No cross-lane
+// reduction and no workgroup barrier: the epoch sums are complete when the
+// wave is, and lane 0 runs the channel's epilogue (correlator.c:243-316).
+//
+// Against the per-call workgroup kernel (4 waves of 64-sample lanes per
+// channel): the per-wave fixed work (reduction, epilogue, state setup) is
+// paid once per channel-call instead of four times, the IF of the next piece
+// streams in while the current one computes, and a lane holds at most one
+// dump per piece (32 samples << D >= 2046 half-chips) at every sample rate.
+// Channels sharing a stream (receivers) read it through L2, which the
+// XCD-aware channel order keeps on one XCD.
+// ============================================================================
+constexpr int kStreamCh = 4;      // channels per workgroup
+constexpr int kStreamWpc = 2;     // waves per channel
+
+__device__ __forceinline__ void flush_epoch(Acc& acc, int e, int32_t* s_sum) {
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    atomicAdd(&s_sum[e * 6 + k], (int)acc.a[k]);
+    acc.a[k] = 0;
+  }
+}
+
+// LDS per channel: E/P/L row + epoch sums; per workgroup: [IF slot per wave
+// (int8)] [kStreamCh channels] [64 LO word pairs]
+__host__ __device__ constexpr int stream_ch_lds(int nsamp) {
+  return kPk8Stage + (((nsamp / GNSSCORR_OSG_ROW + 2) * 24 + 15) & ~15);
+}
+__host__ __device__ constexpr int stream_wg_lds(bool pk, int nsamp, int wpc) {
+  return (pk ? 0 : kStreamCh * wpc * kStage2Bytes) + kStreamCh * stream_ch_lds(nsamp) + 512;
+}
+
+// interval end (see interval_end): flush the part before the carry, carry the
+// rest, step the half-chip; a dump adds the epoch's sums to the LDS and
+// starts the next epoch
+__device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, int& e,
+                                               int32_t* s_sum, const uint8_t* __restrict__ row) {
+  seg_flush(g.pi, g.pq, g.lb, g.pb, g.eb, acc);
+  const int ri = g.ti - g.pi, rq = g.tq - g.pq;
+  g.ti = g.pi = ri;
+  g.tq = g.pq = rq;
+  const bool cy = g.carried;
+  g.hc += cy ? 1u : 0u;
+  g.ld = cy ? g.hc : g.ld;
+  g.carried = false;
+  const bool dump = cy && g.hc >= c.D;   // correlator.c:251-281
+  uint64_t any = __builtin_amdgcn_ballot_w64(dump);
+  asm volatile("" : "+s"(any));          // a uniform branch: the flush stays off the common path
+  if (any) {
+    if (dump) {
+      flush_epoch(acc, e, s_sum);
+      e++;
+      g.hc = 0;        // the bits of half-chip 0 come from the pre-reset index ld
+    }
+  }
+  unpack8(row[g.ld], g.lb, g.pb, g.eb);
+}
+
+// one sample of the reference recurrence (correlator.c:200-283) on the
+// running sums; ROW: the E/P/L bits from the LDS row, else the global table
+template <bool ROW>
+__device__ __forceinline__ void corr_sample_s(int I, int Q, uint32_t& phase, uint32_t& kph,
+                                              const Chan& c, uint32_t& hc, int& lb, int& pb,
+                                              int& eb, Acc& acc, int& e, int32_t* s_sum,
+                                              const uint8_t* row, const uint32_t* __restrict__ pk) {
+  const uint32_t off = (phase >> 27) & 0x1Cu;
+  const int il = __builtin_amdgcn_sbfe((int)kLutI, off, 4);
+  const int ql = __builtin_amdgcn_sbfe((int)kLutQ, off, 4);
+  const int ival = il * I + ql * Q;   // correlator.c:215
+  const int qval = ql * I - il * Q;   // correlator.c:214
+  acc.a[0] += (uint32_t)(lb * ival);
+  acc.a[1] += (uint32_t)(lb * qval);
+  acc.a[2] += (uint32_t)(pb * ival);
+  acc.a[3] += (uint32_t)(pb * qval);
+  acc.a[4] += (uint32_t)(eb * ival);
+  acc.a[5] += (uint32_t)(eb * qval);
+  phase += c.cinc;
+  const uint32_t nk = kph + c.kinc2;
+  const bool carry = nk < kph;
+  kph = nk;
+  if (carry) {
+    hc = (hc + 1u) & 0xFFFFu;
+    const uint32_t ld = hc;
+    if (hc >= c.D) {
+      flush_epoch(acc, e, s_sum);
+      e++;
+      hc = 0;
+    }
+    if constexpr (ROW) {
+      unpack8(row[ld], lb, pb, eb);
+    } else {
+      const uint32_t w = pk[c.base + (int)ld];
+      lb = (int)(int8_t)(w & 0xFFu);
+      pb = (int)(int8_t)((w >> 8) & 0xFFu);
+      eb = (int)(int8_t)((w >> 16) & 0xFFu);
+    }
+  }
+}
+
+// channel state and NCO words of one call (correlator.c:177-189)
+__device__ __forceinline__ bool load_chan(int chn, const gnsscorr_nco_cmd* __restrict__ cmds,
+                                          const gnsscorr_chan_state* __restrict__ state,
+                                          gnsscorr_nco_cmd& cmd, gnsscorr_chan_state& st, Chan& c) {
+  cmd = cmds[chn];
+  st = state[chn];
+  if (cmd.epoch_load >= 0) {  // epoch set, correlator.c:177-182
+    const int v = cmd.epoch_load & 0xFFFF;
+    st.msbit_reg = v;
+    st.ms_counter = v & 0xff;
+    st.bit_counter = v >> 8;
+  }
+  const bool active = cmd.prn > 0 && cmd.prn <= 32;   // correlator.c:185
+  c.P0 = st.carrier_phase;
+  c.K0 = st.code_phase;
+  c.cinc = cmd.carrier_incr;
+  c.kinc2 = cmd.code_incr << 1;
+  c.hc0 = st.half_chip & 0xFFFFu;
+  c.D = (cmd.slew & 0xFFFFu) + 2046u;
+  const uint32_t h1 = (c.hc0 + 1u) & 0xFFFFu;
+  if (h1 >= c.D) c.j1 = 1;
+  else if (c.D <= 0xFFFFu) c.j1 = 1ull + (c.D - h1);
+  else c.j1 = kNever;
+  c.base = (active ? cmd.prn : 0) * GNSSCORR_OSG_ROW;
+  return active;
+}
+
+// WPC waves per channel: wave h of a channel takes pieces h, h + WPC, ...
+template <bool PK, int WPC>
+__global__ __launch_bounds__(64 * kStreamCh * WPC) void osg_stream_kernel(
+    const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp, int n_channels,
+    const gnsscorr_nco_cmd* __restrict__ cmds, gnsscorr_chan_state* __restrict__ state,
+    gnsscorr_track_result* __restrict__ res, int32_t* __restrict__ all_dumps, int max_dumps,
+    const uint32_t* __restrict__ pk, const uint8_t* __restrict__ pk8, int64_t tic_count) {
+  extern __shared__ uint4 s_dyn[];
+  constexpr int kWaves = kStreamCh * WPC;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int q = wave / WPC, h = wave - q * WPC;     // channel slot, wave of the channel
+  const int lane = (int)threadIdx.x & 63;
+  const int ep_cap = nsamp / GNSSCORR_OSG_ROW + 2;
+  const int ch_bytes = stream_ch_lds(nsamp);
+  uint8_t* base8 = reinterpret_cast<uint8_t*>(s_dyn);
+  uint4* slot = reinterpret_cast<uint4*>(base8 + wave * kStage2Bytes);   // int8 only
+  uint8_t* cbase = base8 + (PK ? 0 : kWaves * kStage2Bytes) + q * ch_bytes;
+  uint8_t* s_row = cbase;
+  int32_t* s_sum = reinterpret_cast<int32_t*>(cbase + kPk8Stage);
+  uint2* s_lo = reinterpret_cast<uint2*>(base8 + (PK ? 0 : kWaves * kStage2Bytes) +
+                                         kStreamCh * ch_bytes);
+
+  STREAM_PSTAMP(0);
+  const int grp = xcd_channel(blockIdx.x, gridDim.x);
+  const int chn = grp * kStreamCh + q;
+  const bool have = chn < n_channels;
+  gnsscorr_nco_cmd cmd = {};
+  gnsscorr_chan_state st = {};
+  Chan c = {};
+  const bool active = have && load_chan(chn, cmds, state, cmd, st, c);
+  const int64_t e_stream = (int64_t)cmd.stream * stream_stride * 2;   // element offset
+  const int n_pieces = (nsamp + kPieceSpan - 1) / kPieceSpan;
+  // ---- the wave's first piece on its way first
+  uint2 pq0 = make_uint2(0u, 0u), pq1 = make_uint2(0u, 0u);   // packed: the next piece's 16 B
+  auto fetch_packed = [&](int p) {
+    const int n0 = p * kPieceSpan + lane * kPieceLen;
+    if (n0 + kPieceLen <= nsamp) {
+      const uint2* b = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(ifbuf) +
+                                                      ((e_stream + 2 * (int64_t)n0) >> 2));
+      pq0 = b[0];
+      pq1 = b[1];
+    } else {
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(ifbuf) + ((e_stream + 2 * (int64_t)n0) >> 2);
+      const int L = max(0, nsamp - n0);
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+      for (int k = 0; 2 * k < L; k++) w[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
+      pq0 = make_uint2(w[0], w[1]);
+      pq1 = make_uint2(w[2], w[3]);
+    }
+  };
+  auto dma_piece = [&](int p) {   // int8: chunk r*64 + lane (16 B = 8 samples) of piece p
+    const int n_piece = p * kPieceSpan;
+    const int valid = min(kPieceSpan, nsamp - n_piece);
+    const int full_chunks = valid / 8;
+    const int8_t* g8 = ifbuf + e_stream + 2 * (int64_t)n_piece;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = r * 64 + lane;
+      if (i < full_chunks)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(g8 + 16 * i),
+            (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
+    }
+  };
+  if (active && h < n_pieces) {
+    if constexpr (PK) fetch_packed(h);
+    else dma_piece(h);
+  }
+  // ---- LO words (wave 0), epoch sums and E/P/L row (wave 0 of each channel)
+  if (wave == 0) {
+    const int a = lane & 7, b = lane >> 3;   // LO words of the sample pair (a, b)
+    const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
+    const uint32_t qa = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * a, 4) & 0xFFu;
+    const uint32_t ib = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * b, 4) & 0xFFu;
+    const uint32_t qb = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * b, 4) & 0xFFu;
+    s_lo[lane] = make_uint2(ia | qa << 8 | ib << 16 | qb << 24,
+                            qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24);
+  }
+  const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
+  const bool pk_lds = active && c.j1 != kNever && pk_hi < 3072u;
+  if (h == 0) {
+    for (int i = lane; i < ep_cap * 6; i += 64) s_sum[i] = 0;
+    if (pk_lds) {
+      const uint32_t* g32 = reinterpret_cast<const uint32_t*>(pk8) + (c.base >> 2);
+      uint32_t* l32 = reinterpret_cast<uint32_t*>(s_row);
+      const int n32 = (int)((pk_hi + (uint32_t)(c.base & 3)) >> 2) + 1;
+      for (int i = lane; i < n32; i += 64) l32[i] = g32[i];
+    }
+  }
+  __syncthreads();
+  STREAM_PSTAMP(1);
+  const uint8_t* row = s_row + (c.base & 3);
+  const bool fast = pk_lds && c.kinc2 <= kFastKinc2;
+  const float invD = 1.0f / (float)c.D;
+
+  Acc acc;
+#pragma unroll
+  for (int k = 0; k < 6; k++) acc.a[k] = 0;
+  int e = -1;   // epoch of acc (-1: nothing yet)
+  Seg g;
+  for (int p = h; active && p < n_pieces; p += WPC) {
+    const int n0 = p * kPieceSpan + lane * kPieceLen;
+    const int L = max(0, min(kPieceLen, nsamp - n0));
+    // ---- this lane's 32 samples as 16 pair words (4 chunks of 4)
+    uint4 ch4[4];
+    if constexpr (PK) {
+      ch4[0] = if2_expand_word(pq0.x);
+      ch4[1] = if2_expand_word(pq0.y);
+      ch4[2] = if2_expand_word(pq1.x);
+      ch4[3] = if2_expand_word(pq1.y);
+      if (p + WPC < n_pieces) fetch_packed(p + WPC);
+    } else {
+      if (p * kPieceSpan + kPieceSpan > nsamp && (nsamp & 7)) {
+        // the call's partial last chunk (nsamp not a multiple of 8): whole
+        // words and the odd sample by ordinary loads, never past nsamp
+        const int n_piece = p * kPieceSpan;
+        const int valid = nsamp - n_piece;
+        const int i = valid / 8;
+        if (lane == (i & 63)) {
+          const int rem = valid - i * 8;
+          const uint32_t* g32 = reinterpret_cast<const uint32_t*>(ifbuf + e_stream + 2 * (int64_t)n_piece) + 4 * i;
+          uint32_t t[4] = {0u, 0u, 0u, 0u};
+          for (int k = 0; k < rem / 2; k++) t[k] = g32[k];
+          if (rem & 1) t[rem / 2] = (uint32_t)reinterpret_cast<const uint16_t*>(g32)[rem - 1];
+          slot[i] = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // piece p has landed in the slot
+      if (p == h) STREAM_PSTAMP(2);
+#pragma unroll
+      for (int j = 0; j < 4; j++) ch4[j] = slot[4 * lane + j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers
+      if (p + WPC < n_pieces) dma_piece(p + WPC);
+    }
+    if (L == 0) continue;
+    const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
+    const uint64_t r0 = X >> 32;
+    g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
+    g.kph = (uint32_t)X;
+    uint32_t ep;
+    if (fast) hc_after_fast(c, r0, invD, g.hc, g.ld, ep);
+    else hc_after(c, r0, g.hc, g.ld, ep);
+    {   // a piece that starts in a later epoch than the lane's sums (rare)
+      uint64_t any = __builtin_amdgcn_ballot_w64((int)ep != e);
+      asm volatile("" : "+s"(any));
+      if (any) {
+        if ((int)ep != e) {
+          if (e >= 0) flush_epoch(acc, e, s_sum);
+          e = (int)ep;
+        }
+      }
+    }
+    if (fast) {
+      unpack8(row[g.ld], g.lb, g.pb, g.eb);
+      g.ti = g.tq = g.pi = g.pq = 0;
+      g.carried = false;
+      if (__all(L == kPieceLen)) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int k = 4 * j + i;
+            pair2<false>(words[i], c, g, s_lo);
+            if (k % 3 == 2 || k == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+          }
+        }
+      } else {
+        const int np = L >> 1;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int k = 4 * j + i;
+            if (k < np) pair2<false>(words[i], c, g, s_lo);
+            else if (k == np && (L & 1)) pair2<true>(words[i] & 0xFFFFu, c, g, s_lo);
+            if (k % 3 == 2 || k == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+          }
+        }
+      }
+      seg_flush(g.ti, g.tq, g.lb, g.pb, g.eb, acc);   // the open segment
+    } else {
+      uint32_t hc = g.hc;
+      int lb, pb, eb;
+      if (pk_lds) {
+        unpack8(row[g.ld], lb, pb, eb);
+      } else {
+        const uint32_t tw = pk[c.base + (int)g.ld];
+        lb = (int)(int8_t)(tw & 0xFFu);
+        pb = (int)(int8_t)((tw >> 8) & 0xFFu);
+        eb = (int)(int8_t)((tw >> 16) & 0xFFu);
+      }
+      uint32_t phase = g.p0, kph = g.kph;
+      auto per_sample = [&](auto row_tag) {
+        constexpr bool kRow = decltype(row_tag)::value;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++)
+              if (2 * (4 * j + i) + hh < L)
+                corr_sample_s<kRow>(sbyte((int)words[i], 2 * hh), sbyte((int)words[i], 2 * hh + 1),
+                                    phase, kph, c, hc, lb, pb, eb, acc, e, s_sum, row, pk);
+        }
+      };
+      if (pk_lds) per_sample(std::true_type{});
+      else per_sample(std::false_type{});
+    }
+  }
+  if (e >= 0) flush_epoch(acc, e, s_sum);
+  STREAM_PSTAMP(3);
+  __syncthreads();
+  STREAM_PSTAMP(4);
+  // ---- the kStreamCh channel epilogues side by side: lane j of wave 0 runs channel j
+  if (wave == 0 && lane < kStreamCh) {
+    const int cj = grp * kStreamCh + lane;
+    if (cj < n_channels) {
+      gnsscorr_nco_cmd cmdj;
+      gnsscorr_chan_state stj;
+      Chan cc;
+      const bool actj = load_chan(cj, cmds, state, cmdj, stj, cc);
+      const uint64_t Rtot = ((uint64_t)cc.K0 + (uint64_t)nsamp * cc.kinc2) >> 32;
+      const int32_t* sj = reinterpret_cast<const int32_t*>(
+          base8 + (PK ? 0 : kWaves * kStage2Bytes) + lane * ch_bytes + kPk8Stage);
+      channel_epilogue(cc, cmdj, stj, cj, actj, actj ? n_dumps_after(cc, Rtot) : 0u, Rtot, nsamp,
+                       tic_count, [&](int i) { return (uint32_t)sj[i]; }, res, state, all_dumps,
+                       max_dumps);
+    }
+  }
+  STREAM_PSTAMP(5);
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1071,6 +1459,9 @@ struct gnsscorr_track_ctx {
   int stage_if = 1;   // GNSSCORR_TRACK_STAGE_IF=0: lanes read their IF runs from global memory
   int cpw_override = 0;   // GNSSCORR_TRACK_CPW: channels per workgroup
   int pieces_all = 0;     // GNSSCORR_TRACK_PIECES=1: the piece path for receivers too (A/B)
+  int stream_kernel = 1;  // GNSSCORR_TRACK_STREAM=0: IQ calls on the per-call workgroup
+                          // kernel instead of osg_stream_kernel (A/B)
+  int stream_wpc = kStreamWpc;   // GNSSCORR_TRACK_WPC=1/2/4: waves per channel (A/B)
   int v1 = 0;             // GNSSCORR_TRACK_V1=1: workgroups whose channels read different
                           // streams use the round-2 per-lane global reads, not the piece path (A/B)
   size_t lds_max = 0;     // LDS bytes a workgroup may allocate (gnsscorr_device_lds_bytes)
@@ -1118,6 +1509,11 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   if (const char* e = getenv("GNSSCORR_TRACK_CPW")) c->cpw_override = atoi(e);
   if (const char* e = getenv("GNSSCORR_TRACK_V1")) c->v1 = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_PIECES")) c->pieces_all = atoi(e) != 0;
+  if (const char* e = getenv("GNSSCORR_TRACK_STREAM")) c->stream_kernel = atoi(e) != 0;
+  if (const char* e = getenv("GNSSCORR_TRACK_WPC")) {
+    const int v = atoi(e);
+    if (v == 1 || v == 2 || v == 4) c->stream_wpc = v;
+  }
   const int C = cfg->n_channels;
   auto fail = [&](int code) {
     gnsscorr_track_destroy(c);
@@ -1206,6 +1602,30 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
     return GNSSCORR_EINVAL;
   }
   const int C = c->cfg.n_channels;
+  if (iq && c->stream_kernel) {
+    // osg_stream_kernel: wpc wavefronts per channel, kStreamCh channels per workgroup
+    const int wpc = c->stream_wpc;
+    const size_t dyn = (size_t)stream_wg_lds(pk, (int)nsamp, wpc);
+    if (dyn + 1024 <= c->lds_max) {
+      dim3 grid((C + kStreamCh - 1) / kStreamCh), block(64 * kStreamCh * wpc);
+#define STREAM_LAUNCH(PK, W)                                                                  \
+  hipLaunchKernelGGL((osg_stream_kernel<PK, W>), grid, block, dyn, c->stream, d_if, stride,   \
+                     (int)nsamp, C, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps, c->d_pk, \
+                     c->d_pk8, tic_count)
+      if (pk) {
+        if (wpc == 1) STREAM_LAUNCH(true, 1);
+        else if (wpc == 2) STREAM_LAUNCH(true, 2);
+        else STREAM_LAUNCH(true, 4);
+      } else {
+        if (wpc == 1) STREAM_LAUNCH(false, 1);
+        else if (wpc == 2) STREAM_LAUNCH(false, 2);
+        else STREAM_LAUNCH(false, 4);
+      }
+#undef STREAM_LAUNCH
+      HIP_TRY(hipGetLastError());
+      return GNSSCORR_OK;
+    }
+  }
   int threads = (int)((nsamp + kRun - 1) / kRun);
   threads = (threads + 63) & ~63;
   const size_t stage_bytes = (size_t)((nsamp + kRun - 1) / kRun) * kPitch * 16;
