@@ -48,6 +48,9 @@ FLOP_PER_CELL_BLOCK = 5.0 * np.log2(N) + 6 + 3 + 1
 PEAK_FP32_TFLOPS = 157.3                       # MI355X_MICROARCH.md (vector == matrix f32)
 ACQ64_KERNEL = "acq64_corr_kernel<Plan<16368, 16, 33, 31, 512, true>, 0, false>"  # best-of-blocks
 PEAK_HBM_GBS = 8000.0
+# the OSG tracking correlator of IQ streams (track.hip osg_stream_kernel<packed, waves/channel>)
+TRACK_KERNEL = "osg_stream_kernel<false, 1>"
+TRACK_KERNEL_PK = "osg_stream_kernel<true, 1>"
 PEAK_INT_TOPS = 78.6                           # 256 CU x 128 lanes x 2.4 GHz, 32-bit VALU
 TRACK_RX, TRACK_CH, TRACK_NS = 256, 12, 16368
 SGT_RX, SGT_FS = 256, 16.0e6                   # GLONASS records: initSettings.sci fs = 16 MHz
@@ -1100,6 +1103,26 @@ def hbm_fields(traffic_bytes, seconds):
     return {"hbm_GBs": gbs, "hbm_frac": gbs / PEAK_HBM_GBS}
 
 
+def pmc_section_bytes(section, prefix):
+    """HBM bytes per launch of the kernel instance whose name starts with `prefix`
+    in a per-section rocprofv3 --pmc pass (profiles/pmc_traffic.json "section/kernel",
+    tools/gpu_round.sh), or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    except (OSError, ValueError):
+        return None
+    keys = sorted(k for k in d if k.startswith(f"{section}/{prefix}"))
+    return d[keys[0]]["hbm_bytes_per_launch"] if keys else None
+
+
+def pmc_hbm(section, prefix, seconds):
+    """{traffic, hbm_GBs, hbm_frac}: a kernel's rocprof HBM bytes per launch (its
+    section's own pass) over its measured launch time, against the 8 TB/s peak."""
+    b = pmc_section_bytes(section, prefix)
+    return {"traffic": b, "traffic_source": f"profiles/pmc_traffic.json {section}/{prefix}*",
+            **hbm_fields(b, seconds)}
+
+
 def pmc_traffic(kernel, section=None):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, if any:
     the pass over that bench section alone ("section/kernel") when recorded,
@@ -1234,22 +1257,23 @@ def main():
                 "config": f"{TRACK_RX} receivers x {TRACK_CH} GP2021 channels per GPU, own "
                           f"int8 IQ stream each, 1-ms calls (BASELINE config 3 scaled out)",
                 "realtime_channels_per_gpu": C * 1.0 / trk["kern_ms"],
-                "roofline": {"bound": "valu", "kernel": "osg_track_kernel",
+                "roofline": {"bound": "valu", "kernel": TRACK_KERNEL,
                              "achieved": ops_launch / k_s / 1e12, "peak": PEAK_INT_TOPS,
                              "unit": "Tops/s (int32, 20 ops/sample model)",
                              "frac": ops_launch / k_s / 1e12 / PEAK_INT_TOPS,
                              "hbm_algorithmic_GBs": bytes_launch / k_s / 1e9,
-                             "hbm_frac": bytes_launch / k_s / 1e9 / PEAK_HBM_GBS,
-                             "traffic": pmc_traffic("osg_track_kernel", "track"),
+                             "hbm_algorithmic_frac": bytes_launch / k_s / 1e9 / PEAK_HBM_GBS,
+                             **pmc_hbm("track", TRACK_KERNEL, k_s),
                              "kernel_ms_per_launch": trk["kern_ms"]},
                 "dumps_sane": trk["dumps_ok"],
                 "closed_loop": {
                     "metric": "1ms E/P/L correlations/sec with the gpsisr channel loops on the GPU",
                     "value": C * steps_t * W / trk["dt_cl"],
                     "unit": "channel-ms/s",
-                    "config": f"{C} channels, per 1-ms call: osg_track_kernel + osg_isr_kernel "
-                              "(acquisition / confirm / pull-in / tracking state machine, "
-                              "NCO words fed back on the device, no host round trip)",
+                    "config": f"{C} channels, per 1-ms call: {TRACK_KERNEL} with every "
+                              "channel's gpsisr step (acquisition / confirm / pull-in / tracking "
+                              "state machine) fused after its epilogue: one launch per call, NCO "
+                              "words fed back on the device, no host round trip",
                     "ms_per_call": trk["cl_ms"],
                 },
             }
@@ -1266,11 +1290,14 @@ def main():
                     "value": r["channels"] * steps_t * W / r["dt"], "unit": "channel-ms/s",
                     "kernel_ms_per_launch": r["kern_ms"],
                     "realtime_channels_per_gpu": r["channels"] / r["kern_ms"],
-                    "roofline": {"bound": "hbm", "kernel": "osg_track_kernel",
+                    "roofline": {"bound": "hbm",
+                                 "kernel": TRACK_KERNEL_PK if "packed" in key else TRACK_KERNEL,
                                  "achieved": r["bytes_launch"] / k_s / 1e9, "peak": PEAK_HBM_GBS,
                                  "unit": "GB/s (algorithmic: IF bytes + 64 B state/command/"
                                          "result per channel)",
                                  "frac": r["bytes_launch"] / k_s / 1e9 / PEAK_HBM_GBS,
+                                 **pmc_hbm(f"trk_{key}", TRACK_KERNEL_PK if "packed" in key
+                                           else TRACK_KERNEL, k_s),
                                  "int_ops_frac": r["channels"] * TRACK_NS * TRACK_OPS_PER_SAMPLE
                                  / k_s / 1e12 / PEAK_INT_TOPS},
                 }
@@ -1313,7 +1340,7 @@ def main():
                              "frac": dp / k_s / 1e12 / PEAK_FP64_TFLOPS,
                              "hbm_algorithmic_GBs": C * sgt["steps"] * sgt["fs"] / 1000 * 2 / 14
                              / k_s / 1e9,
-                             "traffic": pmc_traffic("sgt_track_kernel"),
+                             **pmc_hbm("sgt", "sgt_track_kernel", k_s),
                              "kernel_ms_per_launch": sgt["kern_ms"]},
                 "epochs_sane": sgt["ok"],
             }
@@ -1386,7 +1413,7 @@ def main():
                              "achieved": ops / (sdr["ms_acq"] * 1e-3) / 1e12, "peak": PEAK_INT_TOPS,
                              "unit": "Tops/s (int32 op model, DESIGN.md)",
                              "frac": ops / (sdr["ms_acq"] * 1e-3) / 1e12 / PEAK_INT_TOPS,
-                             "traffic": pmc_traffic("sdr_strong_kernel")},
+                             **pmc_hbm("sdr", "sdr_strong_kernel", sdr["ms_acq"] * 1e-3)},
             }
             out["sdr_tracking"] = {
                 "metric": "1ms E/P/L correlations/sec (GPS-SDR Correlator::Accum, bit-exact)",
@@ -1401,7 +1428,7 @@ def main():
                                      "share per channel)",
                              "frac": SDR_CORR_CH * SDR_ACCUM_BYTES / (sdr["ms_corr"] * 1e-3) / 1e9
                              / PEAK_HBM_GBS,
-                             "traffic": pmc_traffic("sdr_accum_kernel")},
+                             **pmc_hbm("sdr", "sdr_accum_kernel", sdr["ms_corr"] * 1e-3)},
             }
             for kind, m in sdr["mw"].items():
                 cells = SDR_SV * SDR_MW_ROWS[kind] * 10 * SDR_N
@@ -1419,7 +1446,11 @@ def main():
                     "roofline": {"bound": "valu", "kernel": "sdr_coh_kernel",
                                  "achieved": ops / (m["ms"] * 1e-3) / 1e12, "peak": PEAK_INT_TOPS,
                                  "unit": "Tops/s (int32 op model, DESIGN.md)",
-                                 "frac": ops / (m["ms"] * 1e-3) / 1e12 / PEAK_INT_TOPS},
+                                 "frac": ops / (m["ms"] * 1e-3) / 1e12 / PEAK_INT_TOPS,
+                                 # rocprof HBM bytes of the request's correlation launch
+                                 # over the whole request time (a lower bound)
+                                 **pmc_hbm("sdr", "sdr_coh_kernel<%s>" % str(kind == "weak").lower(),
+                                           m["ms"] * 1e-3)},
                 }
             out["sdr_channel"] = {
                 "metric": "Channel::Accum calls/sec (GPS-SDR channel: bit lock, frame sync, "
@@ -1429,6 +1460,9 @@ def main():
                 "config": f"{SDR_CHAN_N} channels x {SDR_CHAN_MS} consecutive 1-ms calls per "
                           "launch (one thread per channel), synthetic 50 bps navigation streams",
                 "kernel_ms_per_launch": sdr["ms_ch"],
+                "roofline": {"bound": "latency (serial per-channel chains)",
+                             "kernel": "sdr_channel_kernel",
+                             **pmc_hbm("sdr", "sdr_channel_kernel", sdr["ms_ch"] * 1e-3)},
             }
             lp = sdr["loop"]
             out["sdr_closed_loop"] = {
@@ -1442,6 +1476,9 @@ def main():
                 "kernel_ms_per_launch": lp["ms"],
                 "channels_live_at_end": lp["live"], "channels_stopped": lp["stopped"],
                 "realtime_channels_per_gpu": lp["dumps"] / lp["steps"] / lp["ms"],
+                "roofline": {"bound": "latency (serial per-channel chains)",
+                             "kernel": "sdr_track_kernel",
+                             **pmc_hbm("sdr", "sdr_track_kernel", lp["ms"] * 1e-3)},
             }
             fe_in = SDR_FE_BLOCKS * gc.GN3S_BLOCK_IN
             fe_bytes = fe_in // 4 + SDR_FE_BLOCKS * gc.GN3S_BLOCK_OUT * 4
@@ -1456,7 +1493,7 @@ def main():
                 "roofline": {"bound": "hbm", "achieved": fe_bytes / (sdr["ms_fe"] * 1e-3) / 1e9,
                              "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": fe_bytes / (sdr["ms_fe"] * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                             "traffic": pmc_traffic("gn3s_kernel")},
+                             **pmc_hbm("sdr", "gn3s_kernel", sdr["ms_fe"] * 1e-3)},
             }
         if W == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_acq(acq["meta"])

@@ -23,6 +23,18 @@ void gnsscorr_osg_table_image(int8_t *img);
 void gnsscorr_osg_packed_table(uint32_t *pk);
 void gnsscorr_set_error(const char *fmt, ...);
 int gnsscorr_track_iq(const gnsscorr_track_ctx *ctx);
+/* n_calls closed-loop calls in ONE launch (track.hip osg_stream_kernel): each
+ * channel's wave correlates call k, runs its gpsisr step and goes on to call
+ * k+1 with the new command words; d_res / d_loop_hist receive every call.
+ * GNSSCORR_TRACK_NOT_FUSED when that kernel does not serve the context (I-only
+ * streams, A/B switches, shapes) or n_loops differs from the context's channel
+ * count; the caller then runs the calls as correlator + osg_isr_kernel launches. */
+#define GNSSCORR_TRACK_NOT_FUSED 1
+int gnsscorr_track_dev_isr(gnsscorr_track_ctx *ctx, const int8_t *d_if, int64_t stream_stride,
+                           int64_t nsamp, int n_calls, gnsscorr_nco_cmd *d_cmds,
+                           gnsscorr_track_result *d_res, int n_loops,
+                           const gnsscorr_osg_loop_cfg *cfg, gnsscorr_osg_loop *d_loops,
+                           gnsscorr_osg_loop *d_loop_hist);
 /* GPS-SDR tables (sdr_host.c): packed (i, q) int16 pairs, N = 2048 */
 void gnsscorr_sdr_twiddles(int16_t *w, int16_t *iw);
 void gnsscorr_sdr_code_gen(int sv, uint8_t *chips);

@@ -55,6 +55,21 @@ constexpr int kMaxWaves = 16;
 #ifndef SGT_WPE
 #define SGT_WPE 3
 #endif
+#ifndef SGT_PREFIX
+#define SGT_PREFIX 1
+#endif
+// chunked path, SGT_PREFIX: per-lane prefix sums of W_n*raw over sub-blocks of
+// kSub samples staged in LDS (kSub x 64 x 16 B per wave), read back at each
+// arm's crossing, instead of a code select and two FMAs per arm and sample
+#ifndef SGT_KSUB
+#define SGT_KSUB 16
+#endif
+constexpr int kSub = SGT_KSUB;
+constexpr int kPfWaveBytes = kSub * 64 * 16;
+__host__ __device__ constexpr bool sgt_prefix(int maxt) { return SGT_PREFIX && maxt <= 256; }
+__host__ __device__ constexpr size_t sgt_tab_bytes(int code_length) {
+  return ((size_t)(code_length + 3) * sizeof(double) + 15) & ~(size_t)15;   // s_sgn + guard
+}
 
 struct SgtParams {
   int system, file_type, switch_iq, code_length, chunked;
@@ -184,7 +199,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Wave mode asks for 3 waves per SIMD (<= 168 VGPRs): measured 3 % faster than
 // the 2 the chunked path otherwise compiles to.
 template <int FT, bool CLOSED, int MAXT>
-__global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kernel(
+// (the prefix columns limit a CU to 7 wave-mode workgroups: 2 waves per SIMD)
+__global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) : 1) void sgt_track_kernel(
     SgtParams p, const int8_t* __restrict__ ifbuf, int64_t stride, int64_t n_samples,
     const uint32_t* __restrict__ codes, gnsscorr_sgt_chan* __restrict__ chans, int n_epochs,
     gnsscorr_sgt_epoch* __restrict__ out) {
@@ -196,7 +212,12 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
   __shared__ double2 s_w[32];   // chunked path: exp(i*A*n/fs), n < kC
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
   constexpr bool WAVE = MAXT == 64;
+  constexpr bool kPrefix = sgt_prefix(MAXT);
   const int T = WAVE ? 64 : blockDim.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // this lane's prefix column (kPrefix): entry m at s_pf[m * 64]
+  double2* s_pf = reinterpret_cast<double2*>(reinterpret_cast<uint8_t*>(s_sgn) +
+                                             sgt_tab_bytes(p.code_length) +
+                                             (size_t)wave * kPfWaveBytes) + lane;
   const int nw = T >> 6;
   gnsscorr_sgt_chan c = chans[ch];
   const int L = p.code_length;
@@ -431,6 +452,48 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? SGT_WPE : 1) void sgt_track_kern
         // them from being hoisted out of the chunk loop (16 complex in VGPRs)
         int wo = 0;
         asm volatile("" : "+v"(wo));
+        if constexpr (kPrefix) {
+          // U_x = g1 T + (g0 - g1) B_x per sub-block: T its sum of W_n*raw, B_x
+          // the sum over its samples before arm x's crossing (a prefix read
+          // back from LDS at the crossing); g0 - g1 is 0 or +-2, exact
+          double dg[3];
+#pragma unroll
+          for (int x = 0; x < 3; x++) dg[x] = g0[x] - g1[x];
+#pragma unroll
+          for (int h = 0; h < kC / kSub; h++) {
+            double Pr = 0.0, Pi = 0.0;
+#pragma unroll
+            for (int m = 0; m < kSub; m++) {
+              const int n = h * kSub + m;
+              double ur, ui;
+              if constexpr (FT == 2) {
+                const uint32_t w = wd[n >> 1];
+                const int sh = (n & 1) * 16;
+                const double re = (double)(int)__builtin_amdgcn_sbfe(w, sh + sh_re, 8);
+                const double im = (double)(int)__builtin_amdgcn_sbfe(w, sh + sh_im, 8);
+                const double2 W = s_w[n + wo];   // broadcast read
+                ur = fma(W.x, re, -(W.y * im));
+                ui = fma(W.x, im, W.y * re);
+              } else {
+                const double re = (double)(int)__builtin_amdgcn_sbfe(wd[n >> 2], (n & 3) * 8, 8);
+                const double2 W = s_w[n + wo];
+                ur = W.x * re;
+                ui = W.y * re;
+              }
+              Pr += ur;
+              Pi += ui;
+              s_pf[m * 64] = make_double2(Pr, Pi);
+            }
+#pragma unroll
+            for (int x = 0; x < 3; x++) {
+              const int bl = beta[x] - h * kSub;   // this sub-block's samples before the crossing
+              const double2 B = s_pf[min(max(bl - 1, 0), kSub - 1) * 64];
+              const double br = bl > 0 ? B.x : 0.0, bi = bl > 0 ? B.y : 0.0;
+              Ur[x] = fma(dg[x], br, fma(g1[x], Pr, Ur[x]));
+              Ui[x] = fma(dg[x], bi, fma(g1[x], Pi, Ui[x]));
+            }
+          }
+        } else
 #pragma unroll
         for (int n = 0; n < kC; n++) {
           double ur, ui;
@@ -704,14 +767,17 @@ extern "C" int gnsscorr_sgt_track_dev(gnsscorr_sgt_ctx* c, const int8_t* d_if, i
     if (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) T = v;
   }
   dim3 grid(n_ch), block(T);
-  const size_t tab = (size_t)(c->p.code_length + 3) * sizeof(double);   // s_sgn + guard
+  const size_t tab = sgt_tab_bytes(c->p.code_length);
+  // + the prefix columns of the chunked path (64- and 256-thread shapes)
+  const size_t tab_pf = tab + (sgt_prefix(T) ? (size_t)(T / 64) * kPfWaveBytes : 0);
 #define SGT_LAUNCH(FT, CL)                                                                     \
   do {                                                                                         \
     if (T == 64)                                                                               \
-      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 64>), grid, block, tab, c->stream, c->p,   \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 64>), grid, block, tab_pf, c->stream, c->p,\
                          d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
     else if (T <= 256)                                                                         \
-      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 256>), grid, block, tab, c->stream, c->p,  \
+      hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 256>), grid, block, tab_pf, c->stream,     \
+                         c->p,                                                                 \
                          d_if, stride, n_samples, c->d_codes, d_chan, n_epochs, d_ep);         \
     else                                                                                       \
       hipLaunchKernelGGL((sgt_track_kernel<FT, CL, 1024>), grid, block, tab, c->stream, c->p, \

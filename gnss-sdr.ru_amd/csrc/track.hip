@@ -31,6 +31,7 @@
 #include <string.h>
 #include "gnsscorr_internal.h"
 #include "if2.h"
+#include "osg_isr.h"
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -299,15 +300,14 @@ __device__ __forceinline__ void corr_pair(uint32_t x, uint32_t& p0, uint32_t& kp
 
 // Per-channel epilogue of a call (one thread): dumps, ms/bit counters, TIC latch,
 // carrier cycles and the new channel state (correlator.c:243-316).  sum(i):
-// the call's epoch sums, word i = epoch * 6 + k (LDS or global).
+// the call's epoch sums, word i = epoch * 6 + k (LDS or global).  st_out (if
+// given) receives the new state as well.
 template <typename SumAt>
-__device__ __forceinline__ void channel_epilogue(const Chan& c, const gnsscorr_nco_cmd& cmd,
-                                                 gnsscorr_chan_state st, int chn, bool active,
-                                                 uint32_t ndump, uint64_t Rtot, int nsamp,
-                                                 int64_t tic_count, SumAt sum,
-                                                 gnsscorr_track_result* __restrict__ res,
-                                                 gnsscorr_chan_state* __restrict__ state,
-                                                 int32_t* __restrict__ all_dumps, int max_dumps) {
+__device__ __forceinline__ gnsscorr_track_result channel_epilogue(
+    const Chan& c, const gnsscorr_nco_cmd& cmd, gnsscorr_chan_state st, int chn, bool active,
+    uint32_t ndump, uint64_t Rtot, int nsamp, int64_t tic_count, SumAt sum,
+    gnsscorr_track_result* __restrict__ res, gnsscorr_chan_state* __restrict__ state,
+    int32_t* __restrict__ all_dumps, int max_dumps, gnsscorr_chan_state* st_out = nullptr) {
   if (!active) {   // idle channel: only the epoch load (correlator.c:177-185)
     gnsscorr_track_result r;
     memset(&r, 0, sizeof r);
@@ -315,7 +315,8 @@ __device__ __forceinline__ void channel_epilogue(const Chan& c, const gnsscorr_n
     r.msbit_reg = st.msbit_reg;
     res[chn] = r;
     state[chn] = st;
-    return;
+    if (st_out) *st_out = st;
+    return r;
   }
   gnsscorr_track_result r;
   memset(&r, 0, sizeof r);
@@ -381,6 +382,8 @@ __device__ __forceinline__ void channel_epilogue(const Chan& c, const gnsscorr_n
   st.bit_counter = bit;
   st.msbit_reg = msbit;
   state[chn] = st;
+  if (st_out) *st_out = st;
+  return r;
 }
 
 // Epoch-segmented reduction of the per-thread sums and the per-channel epilogue
@@ -1089,8 +1092,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
 // Channels sharing a stream (receivers) read it through L2, which the
 // XCD-aware channel order keeps on one XCD.
 // ============================================================================
-constexpr int kStreamCh = 4;      // channels per workgroup
-constexpr int kStreamWpc = 2;     // waves per channel
+constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 
 __device__ __forceinline__ void flush_epoch(Acc& acc, int e, int32_t* s_sum) {
 #pragma unroll
@@ -1100,14 +1102,35 @@ __device__ __forceinline__ void flush_epoch(Acc& acc, int e, int32_t* s_sum) {
   }
 }
 
-// LDS per channel: E/P/L row + epoch sums; per workgroup: [IF slot per wave
-// (int8)] [kStreamCh channels] [64 LO word pairs]
-__host__ __device__ constexpr int stream_ch_lds(int nsamp) {
-  return kPk8Stage + (((nsamp / GNSSCORR_OSG_ROW + 2) * 24 + 15) & ~15);
+// LDS per wavefront: [IF slot (int8)] [E/P/L row] [epoch sums] [64 LO word pairs]
+__host__ __device__ constexpr int stream_sum_bytes(int nsamp) {
+  return (((nsamp / GNSSCORR_OSG_ROW + 2) * 24 + 15) & ~15);
 }
-__host__ __device__ constexpr int stream_wg_lds(bool pk, int nsamp, int wpc) {
-  return (pk ? 0 : kStreamCh * wpc * kStage2Bytes) + kStreamCh * stream_ch_lds(nsamp) + 512;
+__host__ __device__ constexpr int stream_wave_lds(bool pk, int nsamp) {
+  return (pk ? 0 : kStage2Bytes) + kPk8Stage + stream_sum_bytes(nsamp) + 512;
 }
+
+// Arguments of one osg_stream_kernel launch: n_calls consecutive calls of
+// every channel (replay or closed loop) or one call.
+struct StreamArgs {
+  const int8_t* ifbuf;
+  int64_t stream_stride;      // samples
+  int64_t call_elems;         // int8 elements of one call within a stream (call k at + k*call_elems)
+  int nsamp, n_channels, n_calls, cmd_step;   // call k's commands: cmds + k*cmd_step
+  gnsscorr_nco_cmd* cmds;
+  gnsscorr_chan_state* state;
+  gnsscorr_track_result* res;  // call k: res + k*n_channels
+  int32_t* all_dumps;          // single calls only
+  int max_dumps;
+  const uint32_t* pk;
+  const uint8_t* pk8;
+  int64_t tic, tic_ref;        // tic_explicit: call 0's TIC sample; else the TIC counter
+  int tic_explicit;            // before call 0, stepped as gnsscorr_track_next_tic does
+  int xcall_prefetch;          // prefetch the next call's first piece during this call's last
+  gnsscorr_osg_loop_cfg lk;    // closed loop (loops != nullptr): gpsisr after every call
+  gnsscorr_osg_loop* loops;
+  gnsscorr_osg_loop* hist;     // call k: hist + k*n_channels (optional)
+};
 
 // interval end (see interval_end): flush the part before the carry, carry the
 // rest, step the half-chip; a dump adds the epoch's sums to the LDS and
@@ -1177,11 +1200,8 @@ __device__ __forceinline__ void corr_sample_s(int I, int Q, uint32_t& phase, uin
 }
 
 // channel state and NCO words of one call (correlator.c:177-189)
-__device__ __forceinline__ bool load_chan(int chn, const gnsscorr_nco_cmd* __restrict__ cmds,
-                                          const gnsscorr_chan_state* __restrict__ state,
-                                          gnsscorr_nco_cmd& cmd, gnsscorr_chan_state& st, Chan& c) {
-  cmd = cmds[chn];
-  st = state[chn];
+__device__ __forceinline__ bool chan_setup(const gnsscorr_nco_cmd& cmd, gnsscorr_chan_state& st,
+                                           Chan& c) {
   if (cmd.epoch_load >= 0) {  // epoch set, correlator.c:177-182
     const int v = cmd.epoch_load & 0xFFFF;
     st.msbit_reg = v;
@@ -1203,76 +1223,23 @@ __device__ __forceinline__ bool load_chan(int chn, const gnsscorr_nco_cmd* __res
   return active;
 }
 
-// WPC waves per channel: wave h of a channel takes pieces h, h + WPC, ...
-template <bool PK, int WPC>
-__global__ __launch_bounds__(64 * kStreamCh * WPC) void osg_stream_kernel(
-    const int8_t* __restrict__ ifbuf, int64_t stream_stride, int nsamp, int n_channels,
-    const gnsscorr_nco_cmd* __restrict__ cmds, gnsscorr_chan_state* __restrict__ state,
-    gnsscorr_track_result* __restrict__ res, int32_t* __restrict__ all_dumps, int max_dumps,
-    const uint32_t* __restrict__ pk, const uint8_t* __restrict__ pk8, int64_t tic_count) {
+template <bool PK, bool CLOSED>
+__global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A) {
   extern __shared__ uint4 s_dyn[];
-  constexpr int kWaves = kStreamCh * WPC;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int q = wave / WPC, h = wave - q * WPC;     // channel slot, wave of the channel
   const int lane = (int)threadIdx.x & 63;
+  const int nsamp = A.nsamp;
   const int ep_cap = nsamp / GNSSCORR_OSG_ROW + 2;
-  const int ch_bytes = stream_ch_lds(nsamp);
-  uint8_t* base8 = reinterpret_cast<uint8_t*>(s_dyn);
-  uint4* slot = reinterpret_cast<uint4*>(base8 + wave * kStage2Bytes);   // int8 only
-  uint8_t* cbase = base8 + (PK ? 0 : kWaves * kStage2Bytes) + q * ch_bytes;
-  uint8_t* s_row = cbase;
-  int32_t* s_sum = reinterpret_cast<int32_t*>(cbase + kPk8Stage);
-  uint2* s_lo = reinterpret_cast<uint2*>(base8 + (PK ? 0 : kWaves * kStage2Bytes) +
-                                         kStreamCh * ch_bytes);
-
+  uint8_t* wb = reinterpret_cast<uint8_t*>(s_dyn) + wave * stream_wave_lds(PK, nsamp);
+  uint4* slot = reinterpret_cast<uint4*>(wb);                      // int8 only
+  uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes);
+  int32_t* s_sum = reinterpret_cast<int32_t*>(s_row + kPk8Stage);
+  uint2* s_lo = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(s_sum) + stream_sum_bytes(nsamp));
   STREAM_PSTAMP(0);
-  const int grp = xcd_channel(blockIdx.x, gridDim.x);
-  const int chn = grp * kStreamCh + q;
-  const bool have = chn < n_channels;
-  gnsscorr_nco_cmd cmd = {};
-  gnsscorr_chan_state st = {};
-  Chan c = {};
-  const bool active = have && load_chan(chn, cmds, state, cmd, st, c);
-  const int64_t e_stream = (int64_t)cmd.stream * stream_stride * 2;   // element offset
-  const int n_pieces = (nsamp + kPieceSpan - 1) / kPieceSpan;
-  // ---- the wave's first piece on its way first
-  uint2 pq0 = make_uint2(0u, 0u), pq1 = make_uint2(0u, 0u);   // packed: the next piece's 16 B
-  auto fetch_packed = [&](int p) {
-    const int n0 = p * kPieceSpan + lane * kPieceLen;
-    if (n0 + kPieceLen <= nsamp) {
-      const uint2* b = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(ifbuf) +
-                                                      ((e_stream + 2 * (int64_t)n0) >> 2));
-      pq0 = b[0];
-      pq1 = b[1];
-    } else {
-      const uint8_t* b = reinterpret_cast<const uint8_t*>(ifbuf) + ((e_stream + 2 * (int64_t)n0) >> 2);
-      const int L = max(0, nsamp - n0);
-      uint32_t w[4] = {0u, 0u, 0u, 0u};
-      for (int k = 0; 2 * k < L; k++) w[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
-      pq0 = make_uint2(w[0], w[1]);
-      pq1 = make_uint2(w[2], w[3]);
-    }
-  };
-  auto dma_piece = [&](int p) {   // int8: chunk r*64 + lane (16 B = 8 samples) of piece p
-    const int n_piece = p * kPieceSpan;
-    const int valid = min(kPieceSpan, nsamp - n_piece);
-    const int full_chunks = valid / 8;
-    const int8_t* g8 = ifbuf + e_stream + 2 * (int64_t)n_piece;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int i = r * 64 + lane;
-      if (i < full_chunks)
-        __builtin_amdgcn_global_load_lds(
-            (const void*)(g8 + 16 * i),
-            (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
-    }
-  };
-  if (active && h < n_pieces) {
-    if constexpr (PK) fetch_packed(h);
-    else dma_piece(h);
-  }
-  // ---- LO words (wave 0), epoch sums and E/P/L row (wave 0 of each channel)
-  if (wave == 0) {
+  const int C = A.n_channels;
+  const int chn = xcd_channel(blockIdx.x, gridDim.x) * kStreamCh + wave;
+  if (chn >= C) return;   // wave-uniform; no workgroup barrier in this kernel
+  {
     const int a = lane & 7, b = lane >> 3;   // LO words of the sample pair (a, b)
     const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
     const uint32_t qa = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * a, 4) & 0xFFu;
@@ -1281,158 +1248,251 @@ __global__ __launch_bounds__(64 * kStreamCh * WPC) void osg_stream_kernel(
     s_lo[lane] = make_uint2(ia | qa << 8 | ib << 16 | qb << 24,
                             qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24);
   }
-  const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
-  const bool pk_lds = active && c.j1 != kNever && pk_hi < 3072u;
-  if (h == 0) {
+  constexpr bool closed = CLOSED;   // A.loops != nullptr: gpsisr after every call
+  gnsscorr_chan_state st = A.state[chn];
+  gnsscorr_nco_cmd cmd = A.cmds[chn];
+  int64_t tic = A.tic;
+  const int n_pieces = (nsamp + kPieceSpan - 1) / kPieceSpan;
+
+  // ---- the piece in flight: LDS-DMA into the wave's slot (int8), or the lane's
+  // 16 bytes in registers (packed).  inflight = k * n_pieces + p, -1 none.
+  int inflight = -1;
+  uint2 pq0 = make_uint2(0u, 0u), pq1 = make_uint2(0u, 0u);
+  auto issue = [&](int k, int p, int64_t e_call) {   // e_call: element offset of call k's stream
+    const int n_piece = p * kPieceSpan;
+    if constexpr (PK) {
+      const int n0 = n_piece + lane * kPieceLen;
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(A.ifbuf) + ((e_call + 2 * (int64_t)n0) >> 2);
+      if (n0 + kPieceLen <= nsamp) {
+        pq0 = reinterpret_cast<const uint2*>(b)[0];
+        pq1 = reinterpret_cast<const uint2*>(b)[1];
+      } else {
+        const int L = max(0, nsamp - n0);
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int q = 0; 2 * q < L; q++) w[q >> 2] |= (uint32_t)b[q] << (8 * (q & 3));
+        pq0 = make_uint2(w[0], w[1]);
+        pq1 = make_uint2(w[2], w[3]);
+      }
+    } else {
+      const int valid = min(kPieceSpan, nsamp - n_piece);
+      const int full_chunks = valid / 8;
+      const int8_t* g8 = A.ifbuf + e_call + 2 * (int64_t)n_piece;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = r * 64 + lane;
+        if (i < full_chunks)
+          __builtin_amdgcn_global_load_lds(
+              (const void*)(g8 + 16 * i),
+              (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
+      }
+    }
+    inflight = k * n_pieces + p;
+  };
+
+  for (int k = 0; k < A.n_calls; k++) {
+    // TIC of this call (gnsscorr_track_next_tic, correlator.c:155-165)
+    int64_t tic_k;
+    if (A.tic_explicit) {
+      tic_k = tic;
+    } else if (tic < nsamp) {
+      tic_k = tic;
+      tic += A.tic_ref - nsamp;
+    } else {
+      tic -= nsamp;
+      tic_k = -1;
+    }
+    if (k > 0 && !closed) cmd = A.cmds[(int64_t)k * A.cmd_step + chn];
+    Chan c;
+    const bool active = chan_setup(cmd, st, c);
+    const int64_t e_call = (int64_t)cmd.stream * A.stream_stride * 2 + (int64_t)k * A.call_elems;
     for (int i = lane; i < ep_cap * 6; i += 64) s_sum[i] = 0;
+    const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
+    const bool pk_lds = active && c.j1 != kNever && pk_hi < 3072u;
+    if (active && inflight != k * n_pieces) issue(k, 0, e_call);
     if (pk_lds) {
-      const uint32_t* g32 = reinterpret_cast<const uint32_t*>(pk8) + (c.base >> 2);
+      const uint32_t* g32 = reinterpret_cast<const uint32_t*>(A.pk8) + (c.base >> 2);
       uint32_t* l32 = reinterpret_cast<uint32_t*>(s_row);
       const int n32 = (int)((pk_hi + (uint32_t)(c.base & 3)) >> 2) + 1;
       for (int i = lane; i < n32; i += 64) l32[i] = g32[i];
     }
-  }
-  __syncthreads();
-  STREAM_PSTAMP(1);
-  const uint8_t* row = s_row + (c.base & 3);
-  const bool fast = pk_lds && c.kinc2 <= kFastKinc2;
-  const float invD = 1.0f / (float)c.D;
+    STREAM_PSTAMP(1);
+    const uint8_t* row = s_row + (c.base & 3);
+    const bool fast = pk_lds && c.kinc2 <= kFastKinc2;
+    const float invD = 1.0f / (float)c.D;
+    // the next call's first piece (prefetched during this call's last piece)
+    int64_t e_next = -1;
+    if (k + 1 < A.n_calls && A.xcall_prefetch) {
+      if (closed) {
+        if (active) e_next = e_call + A.call_elems;   // gpsisr keeps prn and stream
+      } else {
+        const gnsscorr_nco_cmd& nc = A.cmds[(int64_t)(k + 1) * A.cmd_step + chn];
+        if (nc.prn > 0 && nc.prn <= 32)
+          e_next = (int64_t)nc.stream * A.stream_stride * 2 + (int64_t)(k + 1) * A.call_elems;
+      }
+    }
 
-  Acc acc;
+    Acc acc;
 #pragma unroll
-  for (int k = 0; k < 6; k++) acc.a[k] = 0;
-  int e = -1;   // epoch of acc (-1: nothing yet)
-  Seg g;
-  for (int p = h; active && p < n_pieces; p += WPC) {
-    const int n0 = p * kPieceSpan + lane * kPieceLen;
-    const int L = max(0, min(kPieceLen, nsamp - n0));
-    // ---- this lane's 32 samples as 16 pair words (4 chunks of 4)
-    uint4 ch4[4];
-    if constexpr (PK) {
-      ch4[0] = if2_expand_word(pq0.x);
-      ch4[1] = if2_expand_word(pq0.y);
-      ch4[2] = if2_expand_word(pq1.x);
-      ch4[3] = if2_expand_word(pq1.y);
-      if (p + WPC < n_pieces) fetch_packed(p + WPC);
-    } else {
-      if (p * kPieceSpan + kPieceSpan > nsamp && (nsamp & 7)) {
-        // the call's partial last chunk (nsamp not a multiple of 8): whole
-        // words and the odd sample by ordinary loads, never past nsamp
-        const int n_piece = p * kPieceSpan;
-        const int valid = nsamp - n_piece;
-        const int i = valid / 8;
-        if (lane == (i & 63)) {
-          const int rem = valid - i * 8;
-          const uint32_t* g32 = reinterpret_cast<const uint32_t*>(ifbuf + e_stream + 2 * (int64_t)n_piece) + 4 * i;
-          uint32_t t[4] = {0u, 0u, 0u, 0u};
-          for (int k = 0; k < rem / 2; k++) t[k] = g32[k];
-          if (rem & 1) t[rem / 2] = (uint32_t)reinterpret_cast<const uint16_t*>(g32)[rem - 1];
-          slot[i] = make_uint4(t[0], t[1], t[2], t[3]);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // piece p has landed in the slot
-      if (p == h) STREAM_PSTAMP(2);
-#pragma unroll
-      for (int j = 0; j < 4; j++) ch4[j] = slot[4 * lane + j];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers
-      if (p + WPC < n_pieces) dma_piece(p + WPC);
-    }
-    if (L == 0) continue;
-    const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
-    const uint64_t r0 = X >> 32;
-    g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
-    g.kph = (uint32_t)X;
-    uint32_t ep;
-    if (fast) hc_after_fast(c, r0, invD, g.hc, g.ld, ep);
-    else hc_after(c, r0, g.hc, g.ld, ep);
-    {   // a piece that starts in a later epoch than the lane's sums (rare)
-      uint64_t any = __builtin_amdgcn_ballot_w64((int)ep != e);
-      asm volatile("" : "+s"(any));
-      if (any) {
-        if ((int)ep != e) {
-          if (e >= 0) flush_epoch(acc, e, s_sum);
-          e = (int)ep;
-        }
-      }
-    }
-    if (fast) {
-      unpack8(row[g.ld], g.lb, g.pb, g.eb);
-      g.ti = g.tq = g.pi = g.pq = 0;
-      g.carried = false;
-      if (__all(L == kPieceLen)) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int k = 4 * j + i;
-            pair2<false>(words[i], c, g, s_lo);
-            if (k % 3 == 2 || k == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+    for (int q = 0; q < 6; q++) acc.a[q] = 0;
+    int e = -1;   // epoch of acc (-1: nothing yet)
+    Seg g;
+    for (int p = 0; active && p < n_pieces; p++) {
+      const int n0 = p * kPieceSpan + lane * kPieceLen;
+      const int L = max(0, min(kPieceLen, nsamp - n0));
+      // ---- this lane's 32 samples as 16 pair words (4 chunks of 4)
+      uint4 ch4[4];
+      if constexpr (PK) {
+        ch4[0] = if2_expand_word(pq0.x);
+        ch4[1] = if2_expand_word(pq0.y);
+        ch4[2] = if2_expand_word(pq1.x);
+        ch4[3] = if2_expand_word(pq1.y);
+      } else {
+        if (p * kPieceSpan + kPieceSpan > nsamp && (nsamp & 7)) {
+          // the call's partial last chunk (nsamp not a multiple of 8; single
+          // calls only): whole words and the odd sample by ordinary loads
+          const int n_piece = p * kPieceSpan;
+          const int valid = nsamp - n_piece;
+          const int i = valid / 8;
+          if (lane == (i & 63)) {
+            const int rem = valid - i * 8;
+            const uint32_t* g32 =
+                reinterpret_cast<const uint32_t*>(A.ifbuf + e_call + 2 * (int64_t)n_piece) + 4 * i;
+            uint32_t t[4] = {0u, 0u, 0u, 0u};
+            for (int q = 0; q < rem / 2; q++) t[q] = g32[q];
+            if (rem & 1) t[rem / 2] = (uint32_t)reinterpret_cast<const uint16_t*>(g32)[rem - 1];
+            slot[i] = make_uint4(t[0], t[1], t[2], t[3]);
           }
         }
-      } else {
-        const int np = L >> 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the piece has landed in the slot
+        if (p == 0) STREAM_PSTAMP(2);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int k = 4 * j + i;
-            if (k < np) pair2<false>(words[i], c, g, s_lo);
-            else if (k == np && (L & 1)) pair2<true>(words[i] & 0xFFFFu, c, g, s_lo);
-            if (k % 3 == 2 || k == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+        for (int j = 0; j < 4; j++) ch4[j] = slot[4 * lane + j];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers
+      }
+      if (p + 1 < n_pieces) issue(k, p + 1, e_call);
+      else if (e_next >= 0) issue(k + 1, 0, e_next);
+      if (L == 0) continue;
+      const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
+      const uint64_t r0 = X >> 32;
+      g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
+      g.kph = (uint32_t)X;
+      uint32_t ep;
+      if (fast) hc_after_fast(c, r0, invD, g.hc, g.ld, ep);
+      else hc_after(c, r0, g.hc, g.ld, ep);
+      {   // a piece that starts in a later epoch than the lane's sums (rare)
+        uint64_t any = __builtin_amdgcn_ballot_w64((int)ep != e);
+        asm volatile("" : "+s"(any));
+        if (any) {
+          if ((int)ep != e) {
+            if (e >= 0) flush_epoch(acc, e, s_sum);
+            e = (int)ep;
           }
         }
       }
-      seg_flush(g.ti, g.tq, g.lb, g.pb, g.eb, acc);   // the open segment
-    } else {
-      uint32_t hc = g.hc;
-      int lb, pb, eb;
-      if (pk_lds) {
-        unpack8(row[g.ld], lb, pb, eb);
-      } else {
-        const uint32_t tw = pk[c.base + (int)g.ld];
-        lb = (int)(int8_t)(tw & 0xFFu);
-        pb = (int)(int8_t)((tw >> 8) & 0xFFu);
-        eb = (int)(int8_t)((tw >> 16) & 0xFFu);
-      }
-      uint32_t phase = g.p0, kph = g.kph;
-      auto per_sample = [&](auto row_tag) {
-        constexpr bool kRow = decltype(row_tag)::value;
+      if (fast) {
+        unpack8(row[g.ld], g.lb, g.pb, g.eb);
+        g.ti = g.tq = g.pi = g.pq = 0;
+        g.carried = false;
+        if (__all(L == kPieceLen)) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
+          for (int j = 0; j < 4; j++) {
+            const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
 #pragma unroll
-          for (int i = 0; i < 4; i++)
+            for (int i = 0; i < 4; i++) {
+              const int q = 4 * j + i;
+              pair2<false>(words[i], c, g, s_lo);
+              if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+            }
+          }
+        } else {
+          const int np = L >> 1;
 #pragma unroll
-            for (int hh = 0; hh < 2; hh++)
-              if (2 * (4 * j + i) + hh < L)
-                corr_sample_s<kRow>(sbyte((int)words[i], 2 * hh), sbyte((int)words[i], 2 * hh + 1),
-                                    phase, kph, c, hc, lb, pb, eb, acc, e, s_sum, row, pk);
+          for (int j = 0; j < 4; j++) {
+            const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const int q = 4 * j + i;
+              if (q < np) pair2<false>(words[i], c, g, s_lo);
+              else if (q == np && (L & 1)) pair2<true>(words[i] & 0xFFFFu, c, g, s_lo);
+              if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+            }
+          }
         }
-      };
-      if (pk_lds) per_sample(std::true_type{});
-      else per_sample(std::false_type{});
+        seg_flush(g.ti, g.tq, g.lb, g.pb, g.eb, acc);   // the open segment
+      } else {
+        uint32_t hc = g.hc;
+        int lb, pb, eb;
+        if (pk_lds) {
+          unpack8(row[g.ld], lb, pb, eb);
+        } else {
+          const uint32_t tw = A.pk[c.base + (int)g.ld];
+          lb = (int)(int8_t)(tw & 0xFFu);
+          pb = (int)(int8_t)((tw >> 8) & 0xFFu);
+          eb = (int)(int8_t)((tw >> 16) & 0xFFu);
+        }
+        uint32_t phase = g.p0, kph = g.kph;
+        auto per_sample = [&](auto row_tag) {
+          constexpr bool kRow = decltype(row_tag)::value;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+              for (int hh = 0; hh < 2; hh++)
+                if (2 * (4 * j + i) + hh < L)
+                  corr_sample_s<kRow>(sbyte((int)words[i], 2 * hh),
+                                      sbyte((int)words[i], 2 * hh + 1), phase, kph, c, hc, lb, pb,
+                                      eb, acc, e, s_sum, row, A.pk);
+          }
+        };
+        if (pk_lds) per_sample(std::true_type{});
+        else per_sample(std::false_type{});
+      }
     }
-  }
-  if (e >= 0) flush_epoch(acc, e, s_sum);
-  STREAM_PSTAMP(3);
-  __syncthreads();
-  STREAM_PSTAMP(4);
-  // ---- the kStreamCh channel epilogues side by side: lane j of wave 0 runs channel j
-  if (wave == 0 && lane < kStreamCh) {
-    const int cj = grp * kStreamCh + lane;
-    if (cj < n_channels) {
-      gnsscorr_nco_cmd cmdj;
-      gnsscorr_chan_state stj;
-      Chan cc;
-      const bool actj = load_chan(cj, cmds, state, cmdj, stj, cc);
-      const uint64_t Rtot = ((uint64_t)cc.K0 + (uint64_t)nsamp * cc.kinc2) >> 32;
-      const int32_t* sj = reinterpret_cast<const int32_t*>(
-          base8 + (PK ? 0 : kWaves * kStage2Bytes) + lane * ch_bytes + kPk8Stage);
-      channel_epilogue(cc, cmdj, stj, cj, actj, actj ? n_dumps_after(cc, Rtot) : 0u, Rtot, nsamp,
-                       tic_count, [&](int i) { return (uint32_t)sj[i]; }, res, state, all_dumps,
-                       max_dumps);
+    if (e >= 0) flush_epoch(acc, e, s_sum);
+    if (!active && inflight >= 0 && !PK) {
+      // a prefetch for a call that turned out idle must land before the slot is reused
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      inflight = -1;
+    }
+    STREAM_PSTAMP(3);
+    // ---- the channel's epilogue (and closed loop: its gpsisr step) on lane 0; the
+    // epoch sums are complete (the LDS operations of a wave execute in order)
+    // lane 0's new state and command go to every lane by readfirstlane (an LDS
+    // round trip would need a fence: without one the compiler may hoist the
+    // other lanes' reads above lane 0's writes)
+    uint32_t bw[20];
+#pragma unroll
+    for (int i = 0; i < 20; i++) bw[i] = 0u;
+    if (lane == 0) {
+      const uint64_t Rtot = ((uint64_t)c.K0 + (uint64_t)nsamp * c.kinc2) >> 32;
+      gnsscorr_chan_state nst;
+      const gnsscorr_track_result rr = channel_epilogue(
+          c, cmd, st, chn, active, active ? n_dumps_after(c, Rtot) : 0u, Rtot, nsamp, tic_k,
+          [&](int i) { return (uint32_t)s_sum[i]; }, A.res + (int64_t)k * C, A.state,
+          A.n_calls == 1 ? A.all_dumps : nullptr, A.max_dumps, &nst);
+      gnsscorr_nco_cmd r = cmd;
+      if constexpr (CLOSED) {   // osgpsisr.c:360-768, osg_isr_kernel's body
+        gnsscorr_osg_loop lc = A.loops[chn];
+        osgisr::isr_step(A.lk, lc, r, rr);
+        A.loops[chn] = lc;
+        if (A.hist) A.hist[(int64_t)k * C + chn] = lc;
+        if (k + 1 == A.n_calls) A.cmds[chn] = r;
+      }
+      memcpy(bw, &nst, sizeof nst);
+      memcpy(bw + 14, &r, sizeof r);
+    }
+    {
+      static_assert(sizeof(gnsscorr_chan_state) == 56 && sizeof(gnsscorr_nco_cmd) == 24, "bw");
+      uint32_t* sv = reinterpret_cast<uint32_t*>(&st);
+#pragma unroll
+      for (int i = 0; i < 14; i++) sv[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)bw[i]);
+      if (closed) {
+        uint32_t* rv = reinterpret_cast<uint32_t*>(&cmd);
+#pragma unroll
+        for (int i = 0; i < 6; i++) rv[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)bw[14 + i]);
+      }
     }
   }
   STREAM_PSTAMP(5);
@@ -1461,7 +1521,9 @@ struct gnsscorr_track_ctx {
   int pieces_all = 0;     // GNSSCORR_TRACK_PIECES=1: the piece path for receivers too (A/B)
   int stream_kernel = 1;  // GNSSCORR_TRACK_STREAM=0: IQ calls on the per-call workgroup
                           // kernel instead of osg_stream_kernel (A/B)
-  int stream_wpc = kStreamWpc;   // GNSSCORR_TRACK_WPC=1/2/4: waves per channel (A/B)
+  int balance = 1;
+  int xcall_prefetch = 1;  // GNSSCORR_TRACK_XPF=0: no cross-call piece prefetch (A/B)        // GNSSCORR_TRACK_BALANCE=0: no LDS padding for an even spread (A/B)
+  int n_cu = 256;
   int v1 = 0;             // GNSSCORR_TRACK_V1=1: workgroups whose channels read different
                           // streams use the round-2 per-lane global reads, not the piece path (A/B)
   size_t lds_max = 0;     // LDS bytes a workgroup may allocate (gnsscorr_device_lds_bytes)
@@ -1510,10 +1572,12 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   if (const char* e = getenv("GNSSCORR_TRACK_V1")) c->v1 = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_PIECES")) c->pieces_all = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_STREAM")) c->stream_kernel = atoi(e) != 0;
-  if (const char* e = getenv("GNSSCORR_TRACK_WPC")) {
-    const int v = atoi(e);
-    if (v == 1 || v == 2 || v == 4) c->stream_wpc = v;
-  }
+  if (const char* e = getenv("GNSSCORR_TRACK_BALANCE")) c->balance = atoi(e) != 0;
+  if (const char* e = getenv("GNSSCORR_TRACK_XPF")) c->xcall_prefetch = atoi(e) != 0;
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device) !=
+          hipSuccess || c->n_cu < 1)
+    c->n_cu = 256;
+
   const int C = cfg->n_channels;
   auto fail = [&](int code) {
     gnsscorr_track_destroy(c);
@@ -1587,6 +1651,79 @@ extern "C" int64_t gnsscorr_track_next_tic(gnsscorr_track_ctx* c, int64_t nsamp)
   return -1;
 }
 
+// osg_stream_kernel: n_calls consecutive calls of every channel in one launch
+// (call k reads the IF at + k * nsamp samples of each stream and the commands
+// at d_cmds + k * cmd_step; the results go to d_res + k * n_channels).  tic: the
+// first call's TIC sample (tic_explicit) or the TIC counter to step per call.
+// lcfg/d_loops: the closed loop, every channel's gpsisr step after each call.
+// Returns GNSSCORR_TRACK_NOT_FUSED when the kernel does not serve the context
+// or the shape (I-only streams, LDS, alignment of later calls).
+static int launch_stream(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int64_t nsamp,
+                         int n_calls, gnsscorr_nco_cmd* d_cmds, int cmd_step,
+                         gnsscorr_track_result* d_res, int32_t* d_dumps, int64_t tic,
+                         int tic_explicit, const gnsscorr_osg_loop_cfg* lcfg,
+                         gnsscorr_osg_loop* d_loops, gnsscorr_osg_loop* d_hist) {
+  const bool pk = packed(c), iq = bps_of(c) == 2;
+  if (!iq || !c->stream_kernel) return GNSSCORR_TRACK_NOT_FUSED;
+  if (nsamp < 1 || nsamp > c->cfg.max_nsamp) {
+    gnsscorr_set_error("nsamp %lld outside [1, max_nsamp=%d]", (long long)nsamp, c->cfg.max_nsamp);
+    return GNSSCORR_EINVAL;
+  }
+  if (((uintptr_t)d_if & (pk ? 7 : 15)) || ((stride * 2) & (pk ? 31 : 15))) {
+    gnsscorr_set_error("IF base and stream stride must be %d-byte aligned", pk ? 8 : 16);
+    return GNSSCORR_EINVAL;
+  }
+  // later calls start at + k * nsamp samples: the same alignment, and whole
+  // 8-sample chunks (the partial-chunk path is for single calls)
+  if (n_calls > 1 && ((nsamp * 2) & (pk ? 31 : 15))) return GNSSCORR_TRACK_NOT_FUSED;
+  const int C = c->cfg.n_channels;
+  size_t dyn = (size_t)stream_wave_lds(pk, (int)nsamp) * kStreamCh;
+  if (dyn + 1024 > c->lds_max) return GNSSCORR_TRACK_NOT_FUSED;
+  // A launch takes as long as its busiest CU.  The dispatcher fills a CU with
+  // as many workgroups as its resources allow, so at 768 workgroups on 256 CUs
+  // some CUs got 4-5 while others got 2 (wave stamps: pieces p10 16.6 / p90
+  // 27 us).  Asking for enough LDS that at most ceil(workgroups / CUs) fit on
+  // a CU spreads them evenly.
+  const int n_wg = (C + kStreamCh - 1) / kStreamCh;
+  const int per_cu = (n_wg + c->n_cu - 1) / c->n_cu;
+  if (c->balance) {
+    const size_t cap = c->lds_max / (size_t)(per_cu + 1) + 16;   // per_cu + 1 no longer fit
+    if (cap > dyn && cap * per_cu + 1024 * per_cu <= c->lds_max) dyn = cap;
+  }
+  StreamArgs A;
+  memset(&A, 0, sizeof A);
+  A.ifbuf = d_if;
+  A.stream_stride = stride;
+  A.call_elems = nsamp * 2;
+  A.nsamp = (int)nsamp;
+  A.n_channels = C;
+  A.n_calls = n_calls;
+  A.cmd_step = cmd_step;
+  A.cmds = d_cmds;
+  A.state = c->d_state;
+  A.res = d_res;
+  A.all_dumps = d_dumps;
+  A.max_dumps = c->max_dumps;
+  A.pk = c->d_pk;
+  A.pk8 = c->d_pk8;
+  A.tic = tic;
+  A.tic_ref = c->tic_ref;
+  A.tic_explicit = tic_explicit;
+  A.xcall_prefetch = c->xcall_prefetch;
+  if (lcfg) A.lk = *lcfg;
+  A.loops = d_loops;
+  A.hist = d_hist;
+  dim3 grid(n_wg), block(64 * kStreamCh);
+  // the closed loop's gpsisr in its own instantiation: its registers stay out of
+  // the open-loop kernel
+  if (pk && d_loops) hipLaunchKernelGGL((osg_stream_kernel<true, true>), grid, block, dyn, c->stream, A);
+  else if (pk) hipLaunchKernelGGL((osg_stream_kernel<true, false>), grid, block, dyn, c->stream, A);
+  else if (d_loops) hipLaunchKernelGGL((osg_stream_kernel<false, true>), grid, block, dyn, c->stream, A);
+  else hipLaunchKernelGGL((osg_stream_kernel<false, false>), grid, block, dyn, c->stream, A);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
 static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int64_t nsamp,
                   const gnsscorr_nco_cmd* d_cmds, gnsscorr_track_result* d_res,
                   int32_t* d_dumps, int64_t tic_count) {
@@ -1603,28 +1740,9 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   }
   const int C = c->cfg.n_channels;
   if (iq && c->stream_kernel) {
-    // osg_stream_kernel: wpc wavefronts per channel, kStreamCh channels per workgroup
-    const int wpc = c->stream_wpc;
-    const size_t dyn = (size_t)stream_wg_lds(pk, (int)nsamp, wpc);
-    if (dyn + 1024 <= c->lds_max) {
-      dim3 grid((C + kStreamCh - 1) / kStreamCh), block(64 * kStreamCh * wpc);
-#define STREAM_LAUNCH(PK, W)                                                                  \
-  hipLaunchKernelGGL((osg_stream_kernel<PK, W>), grid, block, dyn, c->stream, d_if, stride,   \
-                     (int)nsamp, C, d_cmds, c->d_state, d_res, d_dumps, c->max_dumps, c->d_pk, \
-                     c->d_pk8, tic_count)
-      if (pk) {
-        if (wpc == 1) STREAM_LAUNCH(true, 1);
-        else if (wpc == 2) STREAM_LAUNCH(true, 2);
-        else STREAM_LAUNCH(true, 4);
-      } else {
-        if (wpc == 1) STREAM_LAUNCH(false, 1);
-        else if (wpc == 2) STREAM_LAUNCH(false, 2);
-        else STREAM_LAUNCH(false, 4);
-      }
-#undef STREAM_LAUNCH
-      HIP_TRY(hipGetLastError());
-      return GNSSCORR_OK;
-    }
+    const int rs = launch_stream(c, d_if, stride, nsamp, 1, const_cast<gnsscorr_nco_cmd*>(d_cmds),
+                                 0, d_res, d_dumps, tic_count, 1, nullptr, nullptr, nullptr);
+    if (rs != GNSSCORR_TRACK_NOT_FUSED) return rs;
   }
   int threads = (int)((nsamp + kRun - 1) / kRun);
   threads = (threads + 63) & ~63;
@@ -1756,6 +1874,25 @@ extern "C" int gnsscorr_track_dev(gnsscorr_track_ctx* c, const int8_t* d_if, int
   return launch(c, d_if, stride, nsamp, d_cmds, d_res, d_all_dumps, tic_count);
 }
 
+extern "C" int gnsscorr_track_dev_isr(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride,
+                                      int64_t nsamp, int n_calls, gnsscorr_nco_cmd* d_cmds,
+                                      gnsscorr_track_result* d_res, int n_loops,
+                                      const gnsscorr_osg_loop_cfg* cfg, gnsscorr_osg_loop* d_loops,
+                                      gnsscorr_osg_loop* d_hist) {
+  if (!c || !d_if || !d_cmds || !d_res || !cfg || !d_loops || n_calls < 1) {
+    gnsscorr_set_error("gnsscorr_track_dev_isr: bad arguments");
+    return GNSSCORR_EINVAL;
+  }
+  if (n_loops != c->cfg.n_channels) return GNSSCORR_TRACK_NOT_FUSED;
+  int rc = set_dev(c->cfg.device);
+  if (rc) return rc;
+  rc = launch_stream(c, d_if, stride, nsamp, n_calls, d_cmds, 0, d_res, nullptr, c->tic, 0, cfg,
+                     d_loops, d_hist);
+  if (rc == GNSSCORR_OK)   // the kernel stepped the TIC counter once per call; so does the host
+    for (int k = 0; k < n_calls; k++) (void)gnsscorr_track_next_tic(c, nsamp);
+  return rc;
+}
+
 extern "C" int gnsscorr_track_replay_dev(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride,
                                          int64_t nsamp, int n_steps,
                                          const gnsscorr_nco_cmd* d_cmds,
@@ -1767,6 +1904,14 @@ extern "C" int gnsscorr_track_replay_dev(gnsscorr_track_ctx* c, const int8_t* d_
   int rc = set_dev(c->cfg.device);
   if (rc) return rc;
   const int C = c->cfg.n_channels;
+  // every call in one osg_stream_kernel launch where it serves the context
+  rc = launch_stream(c, d_if, stride, nsamp, n_steps, const_cast<gnsscorr_nco_cmd*>(d_cmds), C,
+                     d_res, nullptr, c->tic, 0, nullptr, nullptr, nullptr);
+  if (rc == GNSSCORR_OK) {
+    for (int k = 0; k < n_steps; k++) (void)gnsscorr_track_next_tic(c, nsamp);
+    return GNSSCORR_OK;
+  }
+  if (rc != GNSSCORR_TRACK_NOT_FUSED) return rc;
   for (int k = 0; k < n_steps; k++) {
     const int64_t tic = gnsscorr_track_next_tic(c, nsamp);
     rc = launch(c, d_if + gnsscorr_track_if_bytes(c, (int64_t)k * nsamp), stride, nsamp,

@@ -98,8 +98,11 @@ _CH_CORE = [("carrier_nco", "<f8"), ("code_nco", "<f8"), ("len", "<i4"), ("count
             ("frame_lock", "<i4"), ("frame_lock_pend", "<i4"), ("bit_number", "<i4"),
             ("subframe", "<i4"), ("freq_lock", "<i4"), ("freq_lock_ticks", "<i4"),
             ("pll", "<f4", (17,)), ("dll", "<f4", (7,))]
-SDR_CHANNEL_CORE = np.dtype(_CH_CORE, align=True)
-SDR_CHANNEL = np.dtype(_CH_CORE + [("fft_buff", "<u4", (512,))], align=True)
+# the C structs' trailing alignment padding as named fields: numpy copies
+# (copy(), element assignment) skip unnamed padding bytes, which then hold
+# whatever np.empty left there and make byte comparisons of copies flaky
+SDR_CHANNEL_CORE = np.dtype(_CH_CORE + [("_pad", "<u4")], align=True)
+SDR_CHANNEL = np.dtype(_CH_CORE + [("fft_buff", "<u4", (512,)), ("_pad", "<u4")], align=True)
 SDR_SUBFRAME = np.dtype([("sv", "<i4"), ("subframe", "<i4"), ("word_buff", "<u4", (12,)),
                          ("chan", "<i4"), ("ms", "<i4")])
 SDR_FEEDBACK = np.dtype([("carrier_nco", "<f8"), ("code_nco", "<f8"), ("kill", "<u4"),

@@ -191,3 +191,41 @@ def test_closed_loop_twelve_channels_vs_reference_receiver(gpu, tmp_path):
             for p in prns[:8]]
     ref, rh, lh = _closed_loop(gpu, tmp_path, 2000, sigs, prns, seed=11)
     _compare(ref, rh, lh, 12)
+
+
+def test_fused_closed_loop_equals_two_launches(gpu, monkeypatch):
+    """The closed loop with gpsisr fused into the correlator launch (one launch
+    per call, osg_stream_kernel) equals the two-launch form (correlator, then
+    osg_isr_kernel; GNSSCORR_OSG_FUSED=0) byte for byte: every call's results,
+    loop states and the final commands, 96 channels x 400 calls on 8 receivers."""
+    calls, n, n_rx = 400, 96, 8
+    rng = np.random.default_rng(21)
+    recs = []
+    for r in range(n_rx):
+        prns = rng.choice(np.arange(1, 33), 6, replace=False)
+        sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
+                     doppler=float(rng.uniform(-400, 400)), cn0=50.0, data_bits=1) for p in prns]
+        recs.append(gpu.ifgen(8192 * calls, sigs, fs=16.0e6, if_gps=2.42e6, seed=40 + r))
+    stride = len(recs[0]) // 2
+    IF = np.concatenate(recs)
+    cfg = gpu.osg_loop_cfg()
+    prns = rng.integers(1, 33, n)
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("GNSSCORR_OSG_FUSED", fused)
+        loops, cmds = gpu.osg_loop_reset(cfg, prns)
+        cmds["stream"] = np.arange(n) // 12
+        trk = gpu.TrackCtx(n, iq=True, samp_rate=16.0e6, max_nsamp=8192)
+        d_if = gpu.DevBuf.from_array(IF)
+        d_l, d_c = gpu.DevBuf.from_array(loops), gpu.DevBuf.from_array(cmds)
+        d_rh = gpu.DevBuf(calls * n * gpu.TRACK_RESULT.itemsize)
+        d_lh = gpu.DevBuf(calls * n * gpu.OSG_LOOP.itemsize)
+        gpu.osg_closed_loop_dev(trk, cfg, d_if.ptr, stride, 8192, calls, n, d_l.ptr, d_c.ptr,
+                                d_rh.ptr, d_lh.ptr)
+        trk.sync()
+        out.append((d_rh.download(np.uint8), d_lh.download(np.uint8), d_l.download(np.uint8),
+                    d_c.download(np.uint8)))
+    for a, b, name in zip(out[0], out[1], ("results", "loop history", "loops", "commands")):
+        assert np.array_equal(a, b), name
+    lh = out[0][1].view(gpu.OSG_LOOP).reshape(calls, n)
+    assert (lh["state"][-1] >= 2).sum() >= 8     # some channels went past acquisition

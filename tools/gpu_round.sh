@@ -43,4 +43,23 @@ for S in acq track fullsky glo_coherent; do
   python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S --runs 13
   echo "pmc section $S ok"
 done
+# the tracking layouts one at a time (the layouts share kernel instantiations)
+for L in cs1_int8 cs1_packed2 rx12_packed2; do
+  mkdir -p $O/pmc_trk_$L
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_trk_$L/$C -o run -- \
+      python3 tools/trk_layout.py $L 10 > $O/pmc_trk_$L/$C.log 2>&1
+  done
+  python tools/pmc_summary.py $O/pmc_trk_$L $O/pmc_summary_trk_$L.json --traffic $O/pmc_traffic.json --section trk_$L
+  echo "pmc layout $L ok"
+done
+for S in sgt sdr; do
+  mkdir -p $O/pmc_$S
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
+      python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1
+  done
+  python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S
+  echo "pmc section $S ok"
+done
 echo "== done"

@@ -5,7 +5,7 @@ set -e
 cd ${GRAFT_REPO_ROOT:-.}
 LAYOUTS=${1:-"cs1_int8 cs1_packed2 rx12_int8 rx12_packed2"}
 REPS=${2:-2}
-VARS=${3:-"0:1 1:1 1:2 1:4"}
+VARS=${3:-"0:1 1:1"}
 for L in $LAYOUTS; do
   for i in $(seq $REPS); do
     for V in $VARS; do

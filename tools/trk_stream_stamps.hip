@@ -1,7 +1,7 @@
 // tools/trk_stream_stamps.hip -- diagnostic build of osg_stream_kernel with
-// s_memrealtime stamps (100 MHz) per wave (lane 0): 0 start, 1 prologue barrier
-// passed, 2 first piece landed, 3 pieces done, 4 epilogue barrier passed,
-// 5 end.  Not part of the library; on the GPU box: bash tools/trk_stream_stamps.sh
+// s_memrealtime stamps (100 MHz) per wave (lane 0): 0 start, 1 call set up (the
+// last call of the launch), 2 its first piece landed, 3 its pieces done, 5 end
+// of the launch (all K calls: the tool replays K = 4 calls in one launch).  Not part of the library; on the GPU box: bash tools/trk_stream_stamps.sh
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,8 +21,7 @@ __device__ unsigned long long* g_stamps;
 int main(int argc, char** argv) {
   const bool cs1 = argc > 2 && argv[2][0] == 'c';   // "cs1": one stream per channel
   const int C = argc > 1 ? atoi(argv[1]) : 3072, NS = 16368, RX = cs1 ? C : (C + 11) / 12, K = 4;
-  const char* w = getenv("GNSSCORR_TRACK_WPC");
-  const int wpc = w ? atoi(w) : kStreamWpc;
+  const int wpc = 1;
   gnsscorr_track_cfg cfg = {};
   cfg.n_channels = C;
   cfg.max_nsamp = NS;
@@ -63,16 +62,16 @@ int main(int argc, char** argv) {
     t0 = std::min(t0, st[(size_t)b * NW * 8]);
     t1 = std::max(t1, st[(size_t)b * NW * 8 + 5]);
   }
-  const char* nm[6] = {"start", "prologue+barrier", "first piece landed", "pieces", "epilogue barrier", "epilogue (wave 0)"};
+  const char* nm[6] = {"start", "last call set up", "first piece landed", "pieces", "-", "to end"};
   printf("%s C=%d wpc=%d kernel span %.1f us\n", cs1 ? "cs1" : "rx12", C, wpc, (t1 - t0) / 100.0);
   for (int i = 0; i < 6; i++) {
     std::vector<double> v;
     for (int b = 0; b < W; b++)
       for (int wv = 0; wv < NW; wv++) {
         const unsigned long long* a = &st[((size_t)b * NW + wv) * 8];
-        if (i == 5 && wv != 0) continue;
-        if (!a[0] || !a[i]) continue;
-        v.push_back(i == 0 ? (double)(a[0] - t0) : (double)(a[i] - (i == 2 ? a[1] : a[i - 1])));
+        if (!a[0] || !a[i] || i == 4) continue;
+        v.push_back(i == 0 ? (double)(a[0] - t0)
+                           : (double)(a[i] - (i == 5 ? a[3] : a[i - 1])));
       }
     std::sort(v.begin(), v.end());
     if (v.empty()) continue;
