@@ -49,8 +49,12 @@ PEAK_FP32_TFLOPS = 157.3                       # MI355X_MICROARCH.md (vector == 
 ACQ64_KERNEL = "acq64_corr_kernel<Plan<16368, 16, 33, 31, 512, true>, 0, false>"  # best-of-blocks
 PEAK_HBM_GBS = 8000.0
 # the OSG tracking correlator of IQ streams (track.hip osg_stream_kernel<packed, waves/channel>)
-TRACK_KERNEL = "osg_stream_kernel<false, 1>"
-TRACK_KERNEL_PK = "osg_stream_kernel<true, 1>"
+TRACK_KERNEL = "osg_stream_kernel<false, false>"      # int8 IQ, open loop
+TRACK_KERNEL_PK = "osg_stream_kernel<true, false>"    # 2-bit packed IQ
+TRACK_KERNEL_CL = "osg_stream_kernel<false, true>"    # closed loop: gpsisr fused
+# calls per osg_stream_kernel launch in the tracking lines (replay and closed loop run
+# n calls per launch; a fixed count keeps rocprof per-launch figures comparable)
+TRACK_CPL = 10
 PEAK_INT_TOPS = 78.6                           # 256 CU x 128 lanes x 2.4 GHz, 32-bit VALU
 TRACK_RX, TRACK_CH, TRACK_NS = 256, 12, 16368
 SGT_RX, SGT_FS = 256, 16.0e6                   # GLONASS records: initSettings.sci fs = 16 MHz
@@ -225,8 +229,26 @@ def run_acq_generic(dist, dev, steps, warmup, fs=GENERIC_FS):
                 conv=1 << int(np.ceil(np.log2(2 * n - 1))))
 
 
+def _track_steps(steps):
+    """timed calls rounded up to whole TRACK_CPL-call launches"""
+    return -(-steps // TRACK_CPL) * TRACK_CPL
+
+
+def _replay_launches(ctx, d_if, stride, if_step_bytes, d_cmds, d_res, C, start, n):
+    """calls [start, start + n) as launches of TRACK_CPL consecutive calls each"""
+    for s in range(start, start + n, TRACK_CPL):
+        m = min(TRACK_CPL, start + n - s)
+        ctx.replay_dev(d_if.ptr + s * if_step_bytes, stride, TRACK_NS, m,
+                       d_cmds.ptr + s * C * gc.NCO_CMD.itemsize,
+                       d_res.ptr + s * C * gc.TRACK_RESULT.itemsize)
+
+
 def run_track(dist, dev, steps, warmup):
+    """The main tracking line: 256 receivers x 12 channels, 1-ms calls replayed on the
+    device, TRACK_CPL calls per launch; warmup: one launch (warmup is rounded to it)."""
     C = TRACK_RX * TRACK_CH
+    steps = _track_steps(steps)
+    warmup = TRACK_CPL
     K = steps + warmup
     stride = K * TRACK_NS                                        # samples per stream
     d_if = gc.DevBuf(TRACK_RX * stride * 2, dev)
@@ -242,16 +264,15 @@ def run_track(dist, dev, steps, warmup):
     d_cmds = gc.DevBuf.from_array(cmds, dev)
     d_res = gc.DevBuf(K * C * gc.TRACK_RESULT.itemsize, dev)
     ctx = gc.TrackCtx(C, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS)
-    ctx.replay_dev(d_if.ptr, stride, TRACK_NS, warmup, d_cmds.ptr, d_res.ptr)
+    step_b = ctx.if_bytes(TRACK_NS)
+    _replay_launches(ctx, d_if, stride, step_b, d_cmds, d_res, C, 0, warmup)
     ctx.sync()
     e0, e1 = gc.Event(dev), gc.Event(dev)
     dist.barrier()
     gc.dev_synchronize(dev)
     t0 = time.perf_counter()
     e0.record(ctx.stream)
-    ctx.replay_dev(d_if.ptr + warmup * TRACK_NS * 2, stride, TRACK_NS, steps,
-                   d_cmds.ptr + warmup * C * gc.NCO_CMD.itemsize,
-                   d_res.ptr + warmup * C * gc.TRACK_RESULT.itemsize)
+    _replay_launches(ctx, d_if, stride, step_b, d_cmds, d_res, C, warmup, steps)
     e1.record(ctx.stream)
     ctx.sync()
     gc.dev_synchronize(dev)
@@ -268,33 +289,37 @@ def run_track(dist, dev, steps, warmup):
     d_l, d_c = gc.DevBuf.from_array(loops, dev), gc.DevBuf.from_array(cl_cmds, dev)
     d_rh = gc.DevBuf(K * C * gc.TRACK_RESULT.itemsize, dev)
     ctx2 = gc.TrackCtx(C, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS)
-    gc.osg_closed_loop_dev(ctx2, cfg, d_if.ptr, stride, TRACK_NS, warmup, C, d_l.ptr, d_c.ptr,
-                           d_rh.ptr)
+
+    def closed(start, n):
+        for s0 in range(start, start + n, TRACK_CPL):
+            m = min(TRACK_CPL, start + n - s0)
+            gc.osg_closed_loop_dev(ctx2, cfg, d_if.ptr + s0 * step_b, stride, TRACK_NS, m, C,
+                                   d_l.ptr, d_c.ptr, d_rh.ptr + s0 * C * gc.TRACK_RESULT.itemsize)
+    closed(0, warmup)
     ctx2.sync()
     dist.barrier()
     t0 = time.perf_counter()
     e0.record(ctx2.stream)
-    gc.osg_closed_loop_dev(ctx2, cfg, d_if.ptr + warmup * TRACK_NS * 2, stride, TRACK_NS, steps, C,
-                           d_l.ptr, d_c.ptr, d_rh.ptr)
+    closed(warmup, steps)
     e1.record(ctx2.stream)
     ctx2.sync()
     dt_cl = dist.max(time.perf_counter() - t0)
     cl_ms = dist.max(e0.elapsed_ms(e1) / steps)
-    return dict(dt=dt, kern_ms=kern_ms, channels=C, dumps_ok=dumps_ok, dt_cl=dt_cl, cl_ms=cl_ms)
+    return dict(dt=dt, kern_ms=kern_ms, channels=C, dumps_ok=dumps_ok, dt_cl=dt_cl, cl_ms=cl_ms,
+                steps=steps)
 
 
 def _replay_timed(dist, dev, ctx, d_if, stride, if_step_bytes, d_cmds, d_res, C, steps, warmup):
-    """warmup + steps replayed 1-ms calls; returns (wall s, kernel ms per call, results)."""
-    ctx.replay_dev(d_if.ptr, stride, TRACK_NS, warmup, d_cmds.ptr, d_res.ptr)
+    """warmup + steps replayed 1-ms calls (TRACK_CPL per launch; the caller sizes the
+    buffers for warmup + steps calls); returns (wall s, kernel ms per call, results)."""
+    _replay_launches(ctx, d_if, stride, if_step_bytes, d_cmds, d_res, C, 0, warmup)
     ctx.sync()
     e0, e1 = gc.Event(dev), gc.Event(dev)
     dist.barrier()
     gc.dev_synchronize(dev)
     t0 = time.perf_counter()
     e0.record(ctx.stream)
-    ctx.replay_dev(d_if.ptr + warmup * if_step_bytes, stride, TRACK_NS, steps,
-                   d_cmds.ptr + warmup * C * gc.NCO_CMD.itemsize,
-                   d_res.ptr + warmup * C * gc.TRACK_RESULT.itemsize)
+    _replay_launches(ctx, d_if, stride, if_step_bytes, d_cmds, d_res, C, warmup, steps)
     e1.record(ctx.stream)
     ctx.sync()
     gc.dev_synchronize(dev)
@@ -322,6 +347,8 @@ def run_track_io(dist, dev, steps, warmup):
     * config 3 as the reference runs it: 12 channels, Sim_GP2021_int per 512-us
       interrupt (osgnss_next_step.c:150,168-184) through the legacy shim, per-call latency."""
     out = {}
+    steps = _track_steps(steps)
+    warmup = TRACK_CPL
     K = steps + warmup
     rng = np.random.default_rng(17 + dist.rank)
     C1 = 3072
@@ -403,6 +430,7 @@ def run_track_io(dist, dev, steps, warmup):
                                   p50_us=float(np.percentile(lat, 50) * 1e6),
                                   p99_us=float(np.percentile(lat, 99) * 1e6),
                                   max_us=float(lat.max() * 1e6))
+    out["steps"] = steps
     return out
 
 
@@ -1246,11 +1274,12 @@ def main():
             }
         if trk:
             C = trk["channels"]
-            steps_t = max(a.steps, 20)
+            steps_t = trk["steps"]
             tvalue = C * steps_t * W / trk["dt"]
             bytes_launch = C * (2.0 * TRACK_NS / TRACK_CH + 64)
             ops_launch = C * TRACK_NS * TRACK_OPS_PER_SAMPLE
-            k_s = trk["kern_ms"] * 1e-3
+            k_s = trk["kern_ms"] * 1e-3          # per call
+            L_s = k_s * TRACK_CPL                 # per launch (TRACK_CPL calls)
             out["tracking"] = {
                 "metric": "1ms E/P/L correlations/sec", "value": tvalue, "unit": "channel-ms/s",
                 "steps": steps_t, "channels_per_gpu": C,
@@ -1263,18 +1292,23 @@ def main():
                              "frac": ops_launch / k_s / 1e12 / PEAK_INT_TOPS,
                              "hbm_algorithmic_GBs": bytes_launch / k_s / 1e9,
                              "hbm_algorithmic_frac": bytes_launch / k_s / 1e9 / PEAK_HBM_GBS,
-                             **pmc_hbm("track", TRACK_KERNEL, k_s),
-                             "kernel_ms_per_launch": trk["kern_ms"]},
+                             **pmc_hbm("track", TRACK_KERNEL, L_s),
+                             "calls_per_launch": TRACK_CPL,
+                             "kernel_ms_per_call": trk["kern_ms"],
+                             "kernel_ms_per_launch": trk["kern_ms"] * TRACK_CPL},
                 "dumps_sane": trk["dumps_ok"],
                 "closed_loop": {
                     "metric": "1ms E/P/L correlations/sec with the gpsisr channel loops on the GPU",
                     "value": C * steps_t * W / trk["dt_cl"],
                     "unit": "channel-ms/s",
-                    "config": f"{C} channels, per 1-ms call: {TRACK_KERNEL} with every "
-                              "channel's gpsisr step (acquisition / confirm / pull-in / tracking "
-                              "state machine) fused after its epilogue: one launch per call, NCO "
-                              "words fed back on the device, no host round trip",
+                    "config": f"{C} channels, 1-ms calls: {TRACK_KERNEL_CL} runs "
+                              f"{TRACK_CPL} consecutive calls per launch, every channel's gpsisr "
+                              "step (acquisition / confirm / pull-in / tracking state machine) "
+                              "after its epilogue in the same wave, NCO words fed back on the "
+                              "device, no host round trip",
                     "ms_per_call": trk["cl_ms"],
+                    "kernel": TRACK_KERNEL_CL, "calls_per_launch": TRACK_CPL,
+                    **pmc_hbm("track", TRACK_KERNEL_CL, trk["cl_ms"] * 1e-3 * TRACK_CPL),
                 },
             }
         if tio:
@@ -1285,10 +1319,14 @@ def main():
                                                "2-bit packed IQ streams")):
                 r = tio[key]
                 k_s = r["kern_ms"] * 1e-3
+                L_s = k_s * TRACK_CPL
                 lay[key] = {
                     "config": f"{r['channels']} channels, {desc}, distinct IF every call",
-                    "value": r["channels"] * steps_t * W / r["dt"], "unit": "channel-ms/s",
-                    "kernel_ms_per_launch": r["kern_ms"],
+                    "value": r["channels"] * tio["steps"] * W / r["dt"],
+                    "unit": "channel-ms/s",
+                    "calls_per_launch": TRACK_CPL,
+                    "kernel_ms_per_call": r["kern_ms"],
+                    "kernel_ms_per_launch": r["kern_ms"] * TRACK_CPL,
                     "realtime_channels_per_gpu": r["channels"] / r["kern_ms"],
                     "roofline": {"bound": "hbm",
                                  "kernel": TRACK_KERNEL_PK if "packed" in key else TRACK_KERNEL,
@@ -1297,7 +1335,7 @@ def main():
                                          "result per channel)",
                                  "frac": r["bytes_launch"] / k_s / 1e9 / PEAK_HBM_GBS,
                                  **pmc_hbm(f"trk_{key}", TRACK_KERNEL_PK if "packed" in key
-                                           else TRACK_KERNEL, k_s),
+                                           else TRACK_KERNEL, L_s),
                                  "int_ops_frac": r["channels"] * TRACK_NS * TRACK_OPS_PER_SAMPLE
                                  / k_s / 1e12 / PEAK_INT_TOPS},
                 }

@@ -522,6 +522,37 @@ __device__ __forceinline__ void pair2(uint32_t x, const Chan& c, Seg& g, const u
   g.pq = dot4(xm, lo.y, g.pq);
 }
 
+// pair2 with the LO word pairs as two 256-byte tables (ival words, qval words):
+// a ds_read_b32 of 64 lanes then touches each bank at most once per distinct
+// entry (64 entries x 4 B = the 64 banks), where the 512-byte uint2 table put
+// entries e and e + 32 on the same banks
+template <bool ONE>
+__device__ __forceinline__ void pair2s(uint32_t x, const Chan& c, Seg& g,
+                                       const uint32_t* __restrict__ lox,
+                                       const uint32_t* __restrict__ loy) {
+  const uint32_t p1 = g.p0 + c.cinc;
+  const uint32_t idx = (g.p0 >> 29) | ((p1 >> 26) & 0x38u);
+  const uint32_t lo_x = lox[idx], lo_y = loy[idx];
+  g.p0 = p1 + c.cinc;
+  const uint32_t k0 = g.kph + c.kinc2;
+  const bool c0 = k0 < g.kph;
+  uint32_t k1 = k0;
+  bool c1 = false;
+  if (!ONE) {
+    k1 = k0 + c.kinc2;
+    c1 = k1 < k0;
+  }
+  g.kph = k1;
+  uint32_t m = c0 ? 0xFFFFu : 0xFFFFFFFFu;
+  m = g.carried ? 0u : m;
+  g.carried = g.carried | c0 | c1;
+  const uint32_t xm = x & m;
+  g.ti = dot4(x, lo_x, g.ti);
+  g.tq = dot4(x, lo_y, g.tq);
+  g.pi = dot4(xm, lo_x, g.pi);
+  g.pq = dot4(xm, lo_y, g.pq);
+}
+
 // end of an interval: flush the part before the carry with the current bits,
 // carry the rest into the next segment, step the half-chip (correlator.c:243-283)
 __device__ __forceinline__ void interval_end(const Chan& c, Seg& g, Acc& cur, Acc& first,
@@ -1093,6 +1124,9 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
 // XCD-aware channel order keeps on one XCD.
 // ============================================================================
 constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
+#ifndef TRACK_LO_SPLIT
+#define TRACK_LO_SPLIT 1          // LO words as two 256-byte tables (pair2s)
+#endif
 
 __device__ __forceinline__ void flush_epoch(Acc& acc, int e, int32_t* s_sum) {
 #pragma unroll
@@ -1245,14 +1279,25 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
     const uint32_t qa = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * a, 4) & 0xFFu;
     const uint32_t ib = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * b, 4) & 0xFFu;
     const uint32_t qb = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * b, 4) & 0xFFu;
+#if TRACK_LO_SPLIT
+    uint32_t* lt = reinterpret_cast<uint32_t*>(s_lo);
+    lt[lane] = ia | qa << 8 | ib << 16 | qb << 24;
+    lt[64 + lane] = qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24;
+#else
     s_lo[lane] = make_uint2(ia | qa << 8 | ib << 16 | qb << 24,
                             qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24);
+#endif
   }
+  const uint32_t* lox = reinterpret_cast<const uint32_t*>(s_lo);
+  const uint32_t* loy = lox + 64;
+  (void)lox;
+  (void)loy;
   constexpr bool closed = CLOSED;   // A.loops != nullptr: gpsisr after every call
   gnsscorr_chan_state st = A.state[chn];
   gnsscorr_nco_cmd cmd = A.cmds[chn];
   int64_t tic = A.tic;
   const int n_pieces = (nsamp + kPieceSpan - 1) / kPieceSpan;
+  int row_base = -1, row_n32 = 0;   // the E/P/L row words staged in s_row (uniform)
 
   // ---- the piece in flight: LDS-DMA into the wave's slot (int8), or the lane's
   // 16 bytes in registers (packed).  inflight = k * n_pieces + p, -1 none.
@@ -1310,10 +1355,16 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
     const bool pk_lds = active && c.j1 != kNever && pk_hi < 3072u;
     if (active && inflight != k * n_pieces) issue(k, 0, e_call);
     if (pk_lds) {
-      const uint32_t* g32 = reinterpret_cast<const uint32_t*>(A.pk8) + (c.base >> 2);
-      uint32_t* l32 = reinterpret_cast<uint32_t*>(s_row);
+      // the staged row serves later calls of the same PRN (replay, closed loop)
+      // as far as it reaches
       const int n32 = (int)((pk_hi + (uint32_t)(c.base & 3)) >> 2) + 1;
-      for (int i = lane; i < n32; i += 64) l32[i] = g32[i];
+      if (c.base != row_base || n32 > row_n32) {
+        const uint32_t* g32 = reinterpret_cast<const uint32_t*>(A.pk8) + (c.base >> 2);
+        uint32_t* l32 = reinterpret_cast<uint32_t*>(s_row);
+        for (int i = lane; i < n32; i += 64) l32[i] = g32[i];
+        row_base = c.base;
+        row_n32 = n32;
+      }
     }
     STREAM_PSTAMP(1);
     const uint8_t* row = s_row + (c.base & 3);
@@ -1400,7 +1451,11 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
 #pragma unroll
             for (int i = 0; i < 4; i++) {
               const int q = 4 * j + i;
+#if TRACK_LO_SPLIT
+              pair2s<false>(words[i], c, g, lox, loy);
+#else
               pair2<false>(words[i], c, g, s_lo);
+#endif
               if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
             }
           }
@@ -1412,8 +1467,13 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
 #pragma unroll
             for (int i = 0; i < 4; i++) {
               const int q = 4 * j + i;
+#if TRACK_LO_SPLIT
+              if (q < np) pair2s<false>(words[i], c, g, lox, loy);
+              else if (q == np && (L & 1)) pair2s<true>(words[i] & 0xFFFFu, c, g, lox, loy);
+#else
               if (q < np) pair2<false>(words[i], c, g, s_lo);
               else if (q == np && (L & 1)) pair2<true>(words[i] & 0xFFFFu, c, g, s_lo);
+#endif
               if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
             }
           }

@@ -283,6 +283,36 @@ def test_replay_equals_sequential(gpu):
     np.testing.assert_array_equal(rep.get_state()["acc"], seq.get_state()["acc"])
 
 
+def test_replay_prn_and_slew_change_between_calls(gpu):
+    """n calls in one osg_stream_kernel launch keep a channel's staged E/P/L row while
+    its PRN and the row's reach stay the same: calls that switch PRN (or go idle and
+    come back) or raise the slew must restage it -- equal to one call per launch."""
+    rng = np.random.default_rng(21)
+    C, K, nsamp = 96, 5, 16368
+    IF = S.synth_if(nsamp * K, 78, [(3, 20, 0, 3)])
+    cmds = _random_cmds(rng, K, C, 1, slew=True)
+    for k in range(1, K):
+        sw = rng.random(C) < 0.3
+        cmds[k]["prn"][sw] = rng.integers(0, 33, sw.sum())
+        cmds[k]["slew"] = np.where(rng.random(C) < 0.3, rng.integers(0, 1200, C), cmds[k]["slew"])
+    seq = gpu.TrackCtx(C, max_nsamp=nsamp)
+    seq_res = []
+    for k in range(K):
+        r, _ = seq.track(IF[k * nsamp * 2:(k + 1) * nsamp * 2], nsamp, cmds[k])
+        seq_res.append(r)
+    rep = gpu.TrackCtx(C, max_nsamp=nsamp)
+    d_if = gpu.DevBuf.from_array(IF)
+    d_cmds = gpu.DevBuf.from_array(cmds)
+    d_res = gpu.DevBuf(K * C * gpu.TRACK_RESULT.itemsize)
+    rep.replay_dev(d_if.ptr, 0, nsamp, K, d_cmds.ptr, d_res.ptr)
+    rep.sync()
+    got = d_res.download(gpu.TRACK_RESULT).reshape(K, C)
+    for k in range(K):
+        assert got[k].tobytes() == seq_res[k].tobytes(), k
+    for f in ("carrier_phase", "code_phase", "half_chip", "acc", "ms_counter"):
+        np.testing.assert_array_equal(rep.get_state()[f], seq.get_state()[f])
+
+
 def test_track_rejects_bad_prn(gpu):
     ctx = gpu.TrackCtx(4, max_nsamp=1024)
     cm = _random_cmds(np.random.default_rng(0), 1, 4, 1)[0]

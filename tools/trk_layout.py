@@ -11,8 +11,8 @@ import bench  # noqa: E402
 from bench import gc  # noqa: E402
 
 layout = sys.argv[1]
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-warmup = 2
+steps = bench._track_steps(int(sys.argv[2]) if len(sys.argv) > 2 else 20)
+warmup = bench.TRACK_CPL   # one launch (bench.py's tracking lines: TRACK_CPL calls per launch)
 K = steps + warmup
 packed = layout.endswith("packed2")
 cs1 = layout.startswith("cs1")
