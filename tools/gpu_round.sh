@@ -1,14 +1,21 @@
 # One GPU session: parity tests, bench, kernel-trace stats, PMC passes.
-# usage (via gpurun): bash tools/gpu_round.sh <tag>
+# usage (via gpurun): bash tools/gpu_round.sh <tag> [main|pmc|all]
+#   main: tests, smoke, bench, kernel-trace stats; pmc: counter passes and the tracking A/B
 # Every GPU step has its own time limit; the first failure ends the script.
 set -eu
 TAG=${1:-r1}
+PART=${2:-all}
 O=gpurun_out/$TAG
 mkdir -p $O/pmc $O/pmc_acq $O/pmc_track $O/pmc_fullsky $O/pmc_glo_coherent
 export TMPDIR=/tmp
+if [ $PART != pmc ]; then
 echo "== pytest -m gpu"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
+# test failures (rc 1) are recorded and the session goes on; a timeout, abort or
+# crash ends it
+rc=0
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || rc=$?
 tail -3 $O/pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc"; exit $rc; fi
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 tail -1 $O/smoke.log
@@ -23,6 +30,8 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
   python3 bench.py --no-cpu-baseline > $O/prof.log 2>&1
 python3 tools/trace_by_grid.py $O/prof acq64_corr_kernel $O/acq64_trace_by_grid.json \
   "rocprofv3 --kernel-trace of python3 bench.py --no-cpu-baseline ($TAG)"
+fi
+if [ $PART = main ]; then echo "== done (main)"; exit 0; fi
 echo "== pmc"
 B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
 i=0
@@ -61,5 +70,22 @@ for S in sgt sdr; do
   done
   python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S
   echo "pmc section $S ok"
+done
+echo "== tracking A/B (same box): stream kernel, TRACK_LO_SPLIT=0 build, per-call workgroup kernel"
+for L in cs1_int8 cs1_packed2 rx12_int8 rx12_packed2; do
+  for V in new lo0 wg; do
+    case $V in
+      new) unset GNSSCORR_LIB; S=1;;
+      lo0) export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/gnsscorr/libgnsscorr_lo0.so; S=1;;
+      wg) unset GNSSCORR_LIB; S=0;;
+    esac
+    [ $V = lo0 ] && [ ! -f gnss-sdr.ru_amd/gnsscorr/libgnsscorr_lo0.so ] && continue
+    echo "$L $V: $(GNSSCORR_TRACK_STREAM=$S timeout -k 10 120 python3 tools/trk_layout.py $L 40)" | tee -a $O/trk_ab.log
+  done
+done
+unset GNSSCORR_LIB
+for F in 1 0; do
+  GNSSCORR_OSG_FUSED=$F timeout -k 10 200 python -u tools/bench_part.py track 40 > $O/track_fused$F.log 2>&1
+  echo "closed loop fused=$F $(tail -1 $O/track_fused$F.log | cut -c1-200)" | tee -a $O/trk_ab.log
 done
 echo "== done"
