@@ -21,9 +21,16 @@ receiver on its own 16.368 Msps int8 IQ stream in HBM, one 1-ms correlator
 call per step (NCO words replayed from a command schedule: the DLL/PLL is
 host code and not part of the hot path).
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N>1 the driver uses
-torch.distributed.run (one rank per GPU); ranks synchronise over gloo (CPU)
-only for the barrier and the max-over-ranks time.
+Run: python bench.py [--gpus N --steps K --warmup W].  For N>1 under
+torch.distributed.run the launcher's RANK/WORLD_SIZE env is used; without it
+bench.py starts the N rank processes itself (launch_ranks).  Ranks synchronise
+over gloo (CPU) only for the barrier, the max-over-ranks time and a small
+result gather.
+
+Output: ONE JSON line on rank 0 -- the contract's keys first, then every
+secondary section without its descriptive strings (floats to 4 significant
+digits), tracking lines last; the full result, descriptions included, goes to
+gpurun_out/bench_detail.json.
 """
 import argparse
 import json
@@ -66,7 +73,7 @@ METRIC = "1ms E/P/L correlations/sec + acquisition cells/sec @16.368Msps; 1/2/4/
 
 
 class Dist:
-    def __init__(self):
+    def __init__(self, load_lib=True):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -74,7 +81,8 @@ class Dist:
         if self.world > 1:
             # bind libgnsscorr.so (and the ROCm runtime it was built against)
             # before torch.distributed pulls in torch's own libamdhip64
-            gc.lib()
+            if load_lib:
+                gc.lib()
             import torch.distributed as td
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             td.init_process_group("gloo", rank=self.rank, world_size=self.world)
@@ -1165,6 +1173,145 @@ def pmc_traffic(kernel, section=None):
         return None
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` run without torch.distributed.run: start N child
+    processes of this script, one rank per GPU, with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, and wait for them.  The parent never loads
+    libgnsscorr.so or touches a GPU (children are started, not exec'd).  Rank 0
+    prints the JSON line (stdout is inherited).  If a rank fails, the others are
+    stopped (they would wait at the gloo barrier forever); the exit code is the
+    first non-zero one."""
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT", "0")) or _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r and not rc:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# Order of the sections in the printed line: the driver keeps the TAIL of stdout,
+# so the lines most worth reading (tracking, GLONASS tracking, full-sky shard
+# projection) come last.  The headline keys come first (the contract's keys).
+SECTION_ORDER = ("sdr_acquisition", "sdr_acquisition_medium", "sdr_acquisition_weak",
+                 "sdr_tracking", "sdr_channel", "sdr_closed_loop", "sdr_frontend",
+                 "acquisition_f32", "acquisition_generic", "glonass_acquisition_5ms",
+                 "executed_fp64", "single_search", "ranks", "fullsky", "glonass_tracking",
+                 "tracking")
+# descriptive strings moved out of the printed line into the detail file (DESIGN.md 6
+# describes every section's workload)
+DETAIL_KEYS = ("config", "note", "sample", "timing", "traffic_source", "source", "host",
+               "port_1core", "port_all_cores", "metric", "peak", "hbm_algorithmic_frac",
+               "int_ops_frac", "flop_per_launch", "cells_per_launch", "p50_us", "max_us", "steps",
+               "config4_realtime_factor", "min_rank_ms", "efficiency")
+
+
+def _round(x, sig=4):
+    if isinstance(x, bool) or not isinstance(x, float):
+        return x
+    return float(f"{x:.{sig}g}")
+
+
+def _round_all(d, sig):
+    if isinstance(d, dict):
+        return {k: _round_all(v, sig) for k, v in d.items()}
+    return _round(d, sig)
+
+
+def compact(d, key=None):
+    """A section without its descriptive strings, floats to 4 significant digits,
+    units without their parenthesised model notes; a section's cpu_baseline keeps
+    value, cores and kind."""
+    if isinstance(d, dict):
+        if key == "cpu_baseline":
+            return {k: _round(v) for k, v in d.items() if k in ("value", "cores", "kind")}
+        return {k: compact(v, k) for k, v in d.items() if k not in DETAIL_KEYS}
+    if isinstance(d, list):
+        return [compact(v) for v in d]
+    if isinstance(d, str) and key in ("unit", "bound"):
+        return d.split(" (")[0]
+    return _round(d)
+
+
+def result_line(out):
+    """The one printed JSON line: the contract's headline keys as assembled (the
+    workload string shortened), then every section compacted, in SECTION_ORDER."""
+    head = {k: v for k, v in out.items() if k not in SECTION_ORDER}
+    if isinstance(head.get("cpu_baseline"), dict):
+        head["cpu_baseline"] = {k: v for k, v in head["cpu_baseline"].items()
+                                if k in ("value", "unit", "cores", "kind", "sample")}
+    line = {k: (_round_all(v, 5) if isinstance(v, dict) else v) for k, v in head.items()}
+    for k in SECTION_ORDER:
+        if k in out:
+            line[k] = compact(out[k])
+    if "ranks" in line:   # one runtime path is enough; every rank's device and PCI id stay
+        line["ranks"] = [{k: v for k, v in r.items() if k != "hip_runtime" or r["rank"] == 0}
+                         for r in line["ranks"]]
+    g = line.get("glonass_tracking", {}).get("at_16368ksps")
+    if g:   # the same line at the other rate: its rate, latency and kernel time
+        line["glonass_tracking"]["at_16368ksps"] = {
+            "value": g.get("value"), "config4_ms_per_epoch_14ch": g.get("config4_ms_per_epoch_14ch"),
+            "frac": g.get("roofline", {}).get("frac"),
+            "kernel_ms_per_launch": g.get("roofline", {}).get("kernel_ms_per_launch")}
+    t = line.get("tracking", {})
+    for sub in list(t.get("layouts", {}).values()) + [t.get("closed_loop", {})]:
+        for k in ("unit", "calls_per_launch", "realtime_channels_per_gpu"):
+            sub.pop(k, None)   # = the tracking line's unit and TRACK_CPL
+    for sub in t.get("pcie_inclusive", {}).values():
+        sub.pop("unit", None)
+    return line
+
+
+def write_detail(out):
+    """The full result (every description, baseline sample and host field) to
+    gpurun_out/bench_detail.json; best effort."""
+    try:
+        d = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "bench_detail.json"), "w") as f:
+            json.dump(out, f, indent=1)
+    except OSError:
+        pass
+
+
+def stub_main(a):
+    """BENCH_STUB=1 (CPU test of the launcher): every rank joins the gloo group,
+    meets at the barrier and rank 0 prints n_gpus and the gathered ranks; no
+    library, no GPU."""
+    dist = Dist(load_lib=False)
+    dist.barrier()
+    info = dist.gather(dict(rank=dist.rank, local_rank=dist.local, pid=os.getpid()))
+    t = dist.max(float(dist.rank))
+    if dist.rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": dist.world, "steps": a.steps,
+                          "warmup": a.warmup, "ranks": info, "max_rank": t}))
+    dist.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1173,6 +1320,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-track", action="store_true")
     a = ap.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: one child process per rank, before any HIP call
+        raise SystemExit(launch_ranks(a.gpus, sys.argv[1:]))
+    if os.environ.get("BENCH_STUB") == "1":
+        return stub_main(a)
     gc.lib()           # the library binds its HIP runtime first (see Dist)
     dist = Dist()
     n_dev = gc.device_count()
@@ -1209,12 +1361,8 @@ def main():
             "data": "synthetic (deterministic 2-bit IQ with 8 planted GPS signals per rank)",
             "config": {"workload": "BASELINE config 2: 32-PRN x 41-bin cold-start acquisition, "
                                    "1 ms coherent, 2 blocks (acquisition.sci), 16.368 Msps, "
-                                   f"fp64 as the reference computes it; {R} consecutive 2-ms "
-                                   "records of one receiver per step, searched in one "
-                                   "correlation launch (gnsscorr_acq_set_records); the 32 "
-                                   "per-PRN code spectra conj(fft(code)) of acquisition.sci:95 "
-                                   "are a constant computed once by set_codes before the timed "
-                                   "steps (code_spectra_ms)",
+                                   f"fp64; {R} 2-ms records per step in one launch; code "
+                                   "spectra set once before the timed steps (code_spectra_ms)",
                        "code_spectra_ms": acq["meta"]["set_codes_ms"],
                        "prns": N_PRN, "bins": N_BINS, "blocks": N_BLK, "samples_per_code": N,
                        "cells_per_search": CELLS_PER_SEARCH, "records_per_step": R,
@@ -1555,7 +1703,8 @@ def main():
                 cb = cpu_baseline_sdr_channel(sdr["ch_corr"])
                 if cb:
                     out["sdr_channel"]["cpu_baseline"] = cb
-        print(json.dumps(out))
+        write_detail(out)
+        print(json.dumps(result_line(out), separators=(",", ":")), flush=True)
     dist.close()
 
 

@@ -1128,6 +1128,19 @@ constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 #define TRACK_LO_SPLIT 1          // LO words as two 256-byte tables (pair2s)
 #endif
 
+// Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
+// writes (plain stores and atomics) are visible to every lane's later LDS reads
+// and atomics.  The wave executes its LDS instructions in order, but without a
+// fence the compiler may move one lane's read above another lane's write: the
+// per-thread memory model knows nothing of the other lanes (the
+// round-4 state broadcast bug).  Wavefront-scope fences emit no instruction; the
+// wave barrier keeps the scheduler from moving memory operations across.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ void flush_epoch(Acc& acc, int e, int32_t* s_sum) {
 #pragma unroll
   for (int k = 0; k < 6; k++) {
@@ -1350,7 +1363,9 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
     Chan c;
     const bool active = chan_setup(cmd, st, c);
     const int64_t e_call = (int64_t)cmd.stream * A.stream_stride * 2 + (int64_t)k * A.call_elems;
+    wave_lds_sync();   // lane 0 read the previous call's sums: they are zeroed only after
     for (int i = lane; i < ep_cap * 6; i += 64) s_sum[i] = 0;
+    wave_lds_sync();   // ... and every lane's flushes add to zeroed sums
     const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
     const bool pk_lds = active && c.j1 != kNever && pk_hi < 3072u;
     if (active && inflight != k * n_pieces) issue(k, 0, e_call);
@@ -1365,6 +1380,7 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
         row_base = c.base;
         row_n32 = n32;
       }
+      wave_lds_sync();   // lanes read row words other lanes staged
     }
     STREAM_PSTAMP(1);
     const uint8_t* row = s_row + (c.base & 3);
@@ -1516,6 +1532,7 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       inflight = -1;
     }
+    wave_lds_sync();   // every lane's flushes land before lane 0 reads the sums
     STREAM_PSTAMP(3);
     // ---- the channel's epilogue (and closed loop: its gpsisr step) on lane 0; the
     // epoch sums are complete (the LDS operations of a wave execute in order)
@@ -1581,8 +1598,8 @@ struct gnsscorr_track_ctx {
   int pieces_all = 0;     // GNSSCORR_TRACK_PIECES=1: the piece path for receivers too (A/B)
   int stream_kernel = 1;  // GNSSCORR_TRACK_STREAM=0: IQ calls on the per-call workgroup
                           // kernel instead of osg_stream_kernel (A/B)
-  int balance = 1;
-  int xcall_prefetch = 1;  // GNSSCORR_TRACK_XPF=0: no cross-call piece prefetch (A/B)        // GNSSCORR_TRACK_BALANCE=0: no LDS padding for an even spread (A/B)
+  int balance = 1;         // GNSSCORR_TRACK_BALANCE=0: no LDS padding for an even spread (A/B)
+  int xcall_prefetch = 1;  // GNSSCORR_TRACK_XPF=0: no cross-call piece prefetch (A/B)
   int n_cu = 256;
   int v1 = 0;             // GNSSCORR_TRACK_V1=1: workgroups whose channels read different
                           // streams use the round-2 per-lane global reads, not the piece path (A/B)
@@ -1746,7 +1763,10 @@ static int launch_stream(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stri
   // a CU spreads them evenly.
   const int n_wg = (C + kStreamCh - 1) / kStreamCh;
   const int per_cu = (n_wg + c->n_cu - 1) / c->n_cu;
-  if (c->balance) {
+  // Only when the launch has more workgroups than CUs: with at most one per CU
+  // the dispatcher spreads them already, and the padding would only lock other
+  // streams' kernels out of those CUs' LDS (co-residency).
+  if (c->balance && n_wg > c->n_cu) {
     const size_t cap = c->lds_max / (size_t)(per_cu + 1) + 16;   // per_cu + 1 no longer fit
     if (cap > dyn && cap * per_cu + 1024 * per_cu <= c->lds_max) dyn = cap;
   }

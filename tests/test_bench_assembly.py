@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class _V(float):
-    def __new__(cls, x=2.0):
+    def __new__(cls, x=123456.789):   # printed like a real measurement (4 digits + exponent)
         return float.__new__(cls, x)
 
 
@@ -82,3 +82,29 @@ def test_bench_main_assembles_the_json_line(monkeypatch):
     for lay_key in ("cs1_int8", "cs1_packed2", "rx12_packed2"):
         r = t["layouts"][lay_key]["roofline"]
         assert {"hbm_GBs", "hbm_frac", "traffic"} <= set(r), lay_key
+    # the driver keeps the last ~8000 characters of stdout: the whole line must fit,
+    # with room for the cpu_baseline objects (off here) and N=8 ranks; tracking last
+    assert len(lines[0]) < 6600, len(lines[0])
+    assert list(d)[-1] == "tracking"
+    assert "glonass_tracking" in d and "fullsky" in d and "shard_projection" in d["fullsky"]
+
+
+def test_bench_launches_n_ranks_itself():
+    """`bench.py --gpus 2` without torch.distributed.run starts two rank processes
+    that meet at the gloo barrier (BENCH_STUB: no library, no GPU)."""
+    import subprocess
+    env = dict(os.environ, BENCH_STUB="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--warmup", "1"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert sorted(r["rank"] for r in d["ranks"]) == [0, 1]
+    assert [r["local_rank"] for r in d["ranks"]] == [0, 1]
+    assert len({r["pid"] for r in d["ranks"]}) == 2
+    assert d["max_rank"] == 1.0

@@ -313,6 +313,75 @@ def test_replay_prn_and_slew_change_between_calls(gpu):
         np.testing.assert_array_equal(rep.get_state()[f], seq.get_state()[f])
 
 
+def _unpack2(b):
+    """GNSSCORR_IF_PACKED2 bytes -> int8 levels (element e: bits 2(e%4) of byte e/4)."""
+    b = np.asarray(b, np.uint8)
+    codes = (b[:, None] >> (2 * np.arange(4, dtype=np.uint8))) & 3
+    return (2 * codes.astype(np.int8) - 3).ravel()
+
+
+@pytest.mark.parametrize("packed", [False, True], ids=["int8", "packed2"])
+def test_replay_many_streams_equals_single_calls(gpu, oracle, packed):
+    """The bench's C_s = 1 shape: 3072 channels, one IF stream each at a nonzero
+    stride, 10 calls in ONE replay_dev launch, with channels that switch stream, go
+    idle or change PRN between calls (the cross-call prefetch then reads another
+    stream's first piece).  Byte-identical to 10 single-call launches; 64 channels
+    spot-checked against the scalar oracle (oracle/osg_corr.c)."""
+    rng = np.random.default_rng(31 + packed)
+    C, K, nsamp = 3072, 10, 16368
+    stride = K * nsamp + 64                         # samples per stream (not a multiple of nsamp)
+    rep = gpu.TrackCtx(C, max_nsamp=nsamp, packed=packed)
+    seq = gpu.TrackCtx(C, max_nsamp=nsamp, packed=packed)
+    sb = rep.if_bytes(stride)
+    d_if = gpu.DevBuf(C * sb + 64)
+    d_if.fill_if2(0x5EED00A0 + packed)
+    cmds = _random_cmds(rng, K, C, C)
+    cmds[0]["stream"] = np.arange(C)
+    for k in range(1, K):
+        cmds[k]["stream"] = cmds[k - 1]["stream"]
+        sw = rng.random(C) < 0.1                    # another stream from this call on
+        cmds[k]["stream"][sw] = rng.integers(0, C, sw.sum())
+        idle = rng.random(C) < 0.05                 # idle for a call
+        cmds[k]["prn"][idle] = 0
+        np_ = rng.random(C) < 0.05                  # a new PRN
+        cmds[k]["prn"][np_] = rng.integers(1, 33, np_.sum())
+    d_cmds = gpu.DevBuf.from_array(cmds)
+    d_res = gpu.DevBuf(K * C * gpu.TRACK_RESULT.itemsize)
+    rep.replay_dev(d_if.ptr, stride, nsamp, K, d_cmds.ptr, d_res.ptr)
+    rep.sync()
+    got = d_res.download(gpu.TRACK_RESULT).reshape(K, C)
+    d_r1 = gpu.DevBuf(C * gpu.TRACK_RESULT.itemsize)
+    for k in range(K):
+        # one call per launch: the IF of call k starts k * nsamp samples into every stream
+        seq.track_dev(d_if.ptr + seq.if_bytes(k * nsamp), stride, nsamp,
+                      d_cmds.ptr + k * C * gpu.NCO_CMD.itemsize, d_r1.ptr, 0, seq.next_tic(nsamp))
+        seq.sync()
+        r = d_r1.download(gpu.TRACK_RESULT)
+        assert got[k].tobytes() == r.tobytes(), \
+            (k, np.flatnonzero((got[k]["dump"] != r["dump"]).any(axis=1))[:8])
+    sr, ss = rep.get_state(), seq.get_state()
+    for f in sr.dtype.names:
+        np.testing.assert_array_equal(sr[f], ss[f], err_msg=f)
+    # oracle spot check: 64 channels, their streams downloaded (and unpacked)
+    sel = np.sort(rng.choice(C, 64, replace=False))
+    used = np.unique(cmds[:, sel]["stream"])
+    host = {}
+    for s in used:
+        raw = d_if.download(np.int8 if not packed else np.uint8, sb, int(s) * sb)
+        host[int(s)] = _unpack2(raw)[:2 * stride] if packed else raw
+    sub = cmds[:, sel].copy()
+    want, nd, ref_state = _oracle_channels(oracle, host, nsamp, sub)
+    for k in range(K):
+        g = got[k][sel]
+        np.testing.assert_array_equal((g["n_dumps"] > 0).astype(np.int32), nd[k])
+        m = nd[k] == 1
+        np.testing.assert_array_equal(g["dump"][m], want[k][m])
+    st = rep.get_state()[sel]
+    for j in range(len(sel)):
+        for key in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+            np.testing.assert_array_equal(st[key][j], ref_state[j][key][0], err_msg=f"{key} {j}")
+
+
 def test_track_rejects_bad_prn(gpu):
     ctx = gpu.TrackCtx(4, max_nsamp=1024)
     cm = _random_cmds(np.random.default_rng(0), 1, 4, 1)[0]
