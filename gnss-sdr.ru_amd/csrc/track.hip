@@ -491,6 +491,7 @@ __device__ __forceinline__ void hc_after_fast(const Chan& c, uint64_t r, float i
 // Lane state through its pieces.
 struct Seg {
   uint32_t p0, kph, hc, ld;
+  uint32_t cb, nb;             // TRACK_PF: row byte of the current bits / of index hc + 1
   int lb, pb, eb;
   int ti, tq, pi, pq;          // interval sums: whole pairs / part before the carry
   bool carried;               // a code carry in the current interval
@@ -1127,6 +1128,9 @@ constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 #ifndef TRACK_LO_SPLIT
 #define TRACK_LO_SPLIT 1          // LO words as two 256-byte tables (pair2s)
 #endif
+#ifndef TRACK_PF
+#define TRACK_PF 1                // LO words and row bytes read ahead (pair2r, interval_end_s)
+#endif
 
 // Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
 // writes (plain stores and atomics) are visible to every lane's later LDS reads
@@ -1190,7 +1194,9 @@ __device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, 
   g.tq = g.pq = rq;
   const bool cy = g.carried;
   g.hc += cy ? 1u : 0u;
+#if !TRACK_PF
   g.ld = cy ? g.hc : g.ld;
+#endif
   g.carried = false;
   const bool dump = cy && g.hc >= c.D;   // correlator.c:251-281
   uint64_t any = __builtin_amdgcn_ballot_w64(dump);
@@ -1202,7 +1208,39 @@ __device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, 
       g.hc = 0;        // the bits of half-chip 0 come from the pre-reset index ld
     }
   }
+#if TRACK_PF
+  // a carry moves to index hc + 1 (the pre-reset index when it dumps): its row
+  // byte was read one interval ahead; the next one is read now
+  g.cb = cy ? g.nb : g.cb;
+  unpack8(g.cb, g.lb, g.pb, g.eb);
+  g.nb = row[g.hc + 1];
+#else
   unpack8(row[g.ld], g.lb, g.pb, g.eb);
+#endif
+}
+
+// pair2s with the pair's LO words already in registers (TRACK_PF: a piece's 16
+// LO word pairs are read from LDS before its first interval)
+template <bool ONE>
+__device__ __forceinline__ void pair2r(uint32_t x, uint32_t lo_x, uint32_t lo_y, const Chan& c,
+                                       Seg& g) {
+  const uint32_t k0 = g.kph + c.kinc2;
+  const bool c0 = k0 < g.kph;
+  uint32_t k1 = k0;
+  bool c1 = false;
+  if (!ONE) {
+    k1 = k0 + c.kinc2;
+    c1 = k1 < k0;
+  }
+  g.kph = k1;
+  uint32_t m = c0 ? 0xFFFFu : 0xFFFFFFFFu;
+  m = g.carried ? 0u : m;
+  g.carried = g.carried | c0 | c1;
+  const uint32_t xm = x & m;
+  g.ti = dot4(x, lo_x, g.ti);
+  g.tq = dot4(x, lo_y, g.tq);
+  g.pi = dot4(xm, lo_x, g.pi);
+  g.pq = dot4(xm, lo_y, g.pq);
 }
 
 // one sample of the reference recurrence (correlator.c:200-283) on the
@@ -1277,6 +1315,22 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
   const int lane = (int)threadIdx.x & 63;
   const int nsamp = A.nsamp;
   const int ep_cap = nsamp / GNSSCORR_OSG_ROW + 2;
+#if TRACK_PF
+  // the 64 (a, b) LO word pairs as two 256-byte tables at a fixed LDS address,
+  // shared by the workgroup's waves: a pair's words are one ds_read2_b32 whose
+  // address is the byte index 4 (a | b << 3) itself
+  __shared__ uint32_t s_lot[128];
+  if (threadIdx.x < 64) {
+    const int a = lane & 7, b = lane >> 3;
+    const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
+    const uint32_t qa = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * a, 4) & 0xFFu;
+    const uint32_t ib = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * b, 4) & 0xFFu;
+    const uint32_t qb = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * b, 4) & 0xFFu;
+    s_lot[lane] = ia | qa << 8 | ib << 16 | qb << 24;
+    s_lot[64 + lane] = qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24;
+  }
+  __syncthreads();   // the only workgroup barrier: before any wave leaves
+#endif
   uint8_t* wb = reinterpret_cast<uint8_t*>(s_dyn) + wave * stream_wave_lds(PK, nsamp);
   uint4* slot = reinterpret_cast<uint4*>(wb);                      // int8 only
   uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes);
@@ -1285,7 +1339,8 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
   STREAM_PSTAMP(0);
   const int C = A.n_channels;
   const int chn = xcd_channel(blockIdx.x, gridDim.x) * kStreamCh + wave;
-  if (chn >= C) return;   // wave-uniform; no workgroup barrier in this kernel
+  if (chn >= C) return;   // wave-uniform; no workgroup barrier from here on
+#if !TRACK_PF
   {
     const int a = lane & 7, b = lane >> 3;   // LO words of the sample pair (a, b)
     const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
@@ -1301,6 +1356,7 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
                             qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24);
 #endif
   }
+#endif
   const uint32_t* lox = reinterpret_cast<const uint32_t*>(s_lo);
   const uint32_t* loy = lox + 64;
   (void)lox;
@@ -1457,7 +1513,28 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
         }
       }
       if (fast) {
+#if TRACK_PF
+        // the piece's 16 LO word pairs: pair q's samples have carrier phases
+        // p0 + 2q cinc and p0 + (2q + 1) cinc (correlator.c:203-204)
+        uint32_t lwx[kPieceLen / 2], lwy[kPieceLen / 2];
+        {
+          uint32_t pa = g.p0;
+#pragma unroll
+          for (int q = 0; q < kPieceLen / 2; q++) {
+            const uint32_t pb = pa + c.cinc;
+            const uint32_t off = ((pa >> 27) & 0x1Cu) | ((pb >> 24) & 0xE0u);   // 4 (a | b << 3)
+            const uint8_t* t = reinterpret_cast<const uint8_t*>(s_lot) + off;
+            lwx[q] = *reinterpret_cast<const uint32_t*>(t);
+            lwy[q] = *reinterpret_cast<const uint32_t*>(t + 256);
+            pa = pb + c.cinc;
+          }
+        }
+        g.cb = row[g.ld];
+        g.nb = row[g.hc + 1];
+        unpack8(g.cb, g.lb, g.pb, g.eb);
+#else
         unpack8(row[g.ld], g.lb, g.pb, g.eb);
+#endif
         g.ti = g.tq = g.pi = g.pq = 0;
         g.carried = false;
         if (__all(L == kPieceLen)) {
@@ -1467,7 +1544,9 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
 #pragma unroll
             for (int i = 0; i < 4; i++) {
               const int q = 4 * j + i;
-#if TRACK_LO_SPLIT
+#if TRACK_PF
+              pair2r<false>(words[i], lwx[q], lwy[q], c, g);
+#elif TRACK_LO_SPLIT
               pair2s<false>(words[i], c, g, lox, loy);
 #else
               pair2<false>(words[i], c, g, s_lo);
@@ -1483,7 +1562,10 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
 #pragma unroll
             for (int i = 0; i < 4; i++) {
               const int q = 4 * j + i;
-#if TRACK_LO_SPLIT
+#if TRACK_PF
+              if (q < np) pair2r<false>(words[i], lwx[q], lwy[q], c, g);
+              else if (q == np && (L & 1)) pair2r<true>(words[i] & 0xFFFFu, lwx[q], lwy[q], c, g);
+#elif TRACK_LO_SPLIT
               if (q < np) pair2s<false>(words[i], c, g, lox, loy);
               else if (q == np && (L & 1)) pair2s<true>(words[i] & 0xFFFFu, c, g, lox, loy);
 #else

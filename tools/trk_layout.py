@@ -16,7 +16,7 @@ warmup = bench.TRACK_CPL   # one launch (bench.py's tracking lines: TRACK_CPL ca
 K = steps + warmup
 packed = layout.endswith("packed2")
 cs1 = layout.startswith("cs1")
-C = 3072
+C = int(os.environ.get("TRK_C", "3072"))   # channels (TRK_C: other launch sizes)
 n_streams = C if cs1 else C // 12
 stride = K * bench.TRACK_NS
 rng = np.random.default_rng(17)
@@ -29,4 +29,5 @@ ctx = gc.TrackCtx(C, iq=True, device=0, max_nsamp=bench.TRACK_NS, samp_rate=benc
                   packed=packed)
 dt, kms, res = bench._replay_timed(bench.Dist(), 0, ctx, d_if, stride, ctx.if_bytes(bench.TRACK_NS),
                                    d_cmds, d_res, C, steps, warmup)
-print(layout, "kernel ms per call %.4f" % kms)
+print(layout, "kernel ms per call %.4f" % kms, "channels", C,
+      "us per 3072 channel-ms %.2f" % (kms * 1e3 * 3072 / C))
