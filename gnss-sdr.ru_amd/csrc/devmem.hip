@@ -90,6 +90,12 @@ extern "C" int gnsscorr_event_record(void* ev, void* stream) {
   return GNSSCORR_OK;
 }
 
+extern "C" int gnsscorr_stream_wait_event(void* stream, void* ev) {
+  if (!ev) return GNSSCORR_EINVAL;
+  HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0));
+  return GNSSCORR_OK;
+}
+
 extern "C" int gnsscorr_event_elapsed_ms(void* start, void* stop, float* ms) {
   if (!ms) return GNSSCORR_EINVAL;
   HIP_TRY(hipEventSynchronize((hipEvent_t)stop));

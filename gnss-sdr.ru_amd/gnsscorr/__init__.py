@@ -190,6 +190,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_osg_closed_loop_dev",
     "gnsscorr_dev_alloc", "gnsscorr_dev_free", "gnsscorr_memcpy_htod", "gnsscorr_memcpy_dtoh",
     "gnsscorr_dev_synchronize", "gnsscorr_event_create", "gnsscorr_event_record",
+    "gnsscorr_stream_wait_event",
     "gnsscorr_event_elapsed_ms", "gnsscorr_event_destroy", "gnsscorr_dev_fill_if2",
     "gnsscorr_ifgen", "gnsscorr_ca_code", "gnsscorr_st_code", "gnsscorr_sample_code",
     "correlator_init", "Sim_GP2021_int", "gnsscorr_osg_configure", "gnsscorr_osg_get_state",
@@ -301,6 +302,7 @@ def lib() -> C.CDLL:
         "gnsscorr_dev_synchronize": (I, [I]),
         "gnsscorr_event_create": (I, [I, C.POINTER(P)]),
         "gnsscorr_event_record": (I, [P, P]),
+        "gnsscorr_stream_wait_event": (I, [P, P]),
         "gnsscorr_event_elapsed_ms": (I, [P, P, C.POINTER(C.c_float)]),
         "gnsscorr_event_destroy": (I, [P]),
         "gnsscorr_dev_fill_if2": (I, [I, P, C.c_size_t, U64]),
@@ -444,6 +446,10 @@ class Event:
 
     def record(self, stream: int):
         _check(lib().gnsscorr_event_record(self.h, stream), "gnsscorr_event_record")
+
+    def wait_on(self, stream: int):
+        """Work queued on `stream` from now on waits for this event."""
+        _check(lib().gnsscorr_stream_wait_event(stream, self.h), "gnsscorr_stream_wait_event")
 
     def elapsed_ms(self, end: "Event") -> float:
         ms = C.c_float()

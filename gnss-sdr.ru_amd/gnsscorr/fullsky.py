@@ -92,7 +92,11 @@ class FullSky:
             p["d_if"].upload(np.ascontiguousarray(rec[:need], np.int8))
 
     def run(self):
-        """Enqueue the search (asynchronous on each context's stream)."""
+        """Enqueue the search (asynchronous on each context's stream).  The two
+        parts (GPS and GLONASS) run on their own streams with no join: joining
+        them (both spectra first, then both correlation launches together) was
+        measured slower at world 4 and 8 -- 246 workgroups from two concurrent
+        launches do not all fit one round of the CUs."""
         for p in self.parts:
             G = len(p["ids"])
             p["ctx"].spectra_dev(p["d_if"].ptr, self.n_ms, p["n_freqs"], p["d_freqs"].ptr)

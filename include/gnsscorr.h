@@ -738,6 +738,9 @@ int gnsscorr_memcpy_dtoh(int device, void *h_dst, const void *d_src, size_t byte
 int gnsscorr_dev_synchronize(int device);
 int gnsscorr_event_create(int device, void **ev);
 int gnsscorr_event_record(void *ev, void *stream);
+/* Work queued on `stream` after this call waits until `ev` has completed
+ * (joins two context streams without a host synchronisation). */
+int gnsscorr_stream_wait_event(void *stream, void *ev);
 int gnsscorr_event_elapsed_ms(void *start, void *stop, float *ms);
 int gnsscorr_event_destroy(void *ev);
 /* Fill a device buffer with pseudo-random 2-bit levels {-3,-1,1,3}
