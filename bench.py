@@ -63,7 +63,12 @@ TRACK_KERNEL_CL = "osg_stream_kernel<false, true>"    # closed loop: gpsisr fuse
 # n calls per launch; a fixed count keeps rocprof per-launch figures comparable)
 TRACK_CPL = 10
 PEAK_INT_TOPS = 78.6                           # 256 CU x 128 lanes x 2.4 GHz, 32-bit VALU
-TRACK_RX, TRACK_CH, TRACK_NS = 256, 12, 16368
+# 1024 receivers x 12 channels per GPU: 12288 channel-waves give 4 waves per SIMD
+# (3072 give 3; the kernel is latency bound there: rx12 int8 29-30 -> 24-25 us per
+# 3072 channel-ms at 12288, same box, profiles/r5/fullsky_join_and_trk_scan_r5c.log)
+TRACK_RX, TRACK_CH, TRACK_NS = 1024, 12, 16368
+TRACK_C1 = TRACK_RX * TRACK_CH   # channels of the one-stream-per-channel layouts
+TRACK_RX_HOST = 256              # receivers of the PCIe-inclusive host-buffer lines
 SGT_RX, SGT_FS = 256, 16.0e6                   # GLONASS records: initSettings.sci fs = 16 MHz
 SGT_DP_PER_SAMPLE = 27                         # fp64 ops/sample of sgt_track_kernel
 PEAK_FP64_TFLOPS = 78.6                        # MI355X FP64 vector (AMD spec; not in the guide)
@@ -349,7 +354,7 @@ def _track_cmds(rng, C, streams):
 def run_track_io(dist, dev, steps, warmup):
     """Tracking layouts beside the main line (all 16.368 Msps, 1-ms calls):
     * one IF stream PER CHANNEL (C_s = 1: the layout where HBM bytes bind), int8 and
-      2-bit packed (GNSSCORR_IF_PACKED2), 3072 channels, distinct data every call;
+      2-bit packed (GNSSCORR_IF_PACKED2), TRACK_C1 channels, distinct data every call;
     * the main 256 x 12 layout with packed streams;
     * PCIe-inclusive: gnsscorr_track from host buffers (256 x 12 channels per call);
     * config 3 as the reference runs it: 12 channels, Sim_GP2021_int per 512-us
@@ -359,7 +364,7 @@ def run_track_io(dist, dev, steps, warmup):
     warmup = TRACK_CPL
     K = steps + warmup
     rng = np.random.default_rng(17 + dist.rank)
-    C1 = 3072
+    C1 = TRACK_C1
     for packed in (False, True):
         stride = K * TRACK_NS
         bytes_stream = stride * 2 // (4 if packed else 1)
@@ -394,26 +399,28 @@ def run_track_io(dist, dev, steps, warmup):
     ctx.close()
     d_if.free()
     # PCIe-inclusive: host IF (pageable numpy) -> gnsscorr_track -> host results, per call
+    Ch = TRACK_RX_HOST * TRACK_CH
+    cmdh = _track_cmds(rng, Ch, np.repeat(np.arange(TRACK_RX_HOST), TRACK_CH))
     for packed in (False, True):
-        ctx = gc.TrackCtx(C, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS, packed=packed)
-        h_if = np.random.default_rng(3).integers(-128, 128, TRACK_RX * ctx.if_bytes(TRACK_NS),
+        ctx = gc.TrackCtx(Ch, iq=True, device=dev, max_nsamp=TRACK_NS, samp_rate=FS, packed=packed)
+        h_if = np.random.default_rng(3).integers(-128, 128, TRACK_RX_HOST * ctx.if_bytes(TRACK_NS),
                                                  dtype=np.int8)
         if not packed:
             h_if = np.random.default_rng(3).choice(np.array([-3, -1, 1, 3], np.int8), h_if.size)
         n_calls = max(steps, 20)
         for _ in range(3):
-            ctx.track(h_if, TRACK_NS, cmd1, n_streams=TRACK_RX, stream_stride=TRACK_NS)
+            ctx.track(h_if, TRACK_NS, cmdh, n_streams=TRACK_RX_HOST, stream_stride=TRACK_NS)
         lat = []
         dist.barrier()
         for _ in range(n_calls):
             t0 = time.perf_counter()
-            ctx.track(h_if, TRACK_NS, cmd1, n_streams=TRACK_RX, stream_stride=TRACK_NS)
+            ctx.track(h_if, TRACK_NS, cmdh, n_streams=TRACK_RX_HOST, stream_stride=TRACK_NS)
             lat.append(time.perf_counter() - t0)
         lat = np.array(lat)
         out["host_packed2" if packed else "host_int8"] = dict(
-            channels=C, calls=n_calls, mean_ms=dist.max(float(lat.mean()) * 1e3),
+            channels=Ch, calls=n_calls, mean_ms=dist.max(float(lat.mean()) * 1e3),
             p99_ms=dist.max(float(np.percentile(lat, 99)) * 1e3),
-            h2d_bytes=TRACK_RX * ctx.if_bytes(TRACK_NS))
+            h2d_bytes=TRACK_RX_HOST * ctx.if_bytes(TRACK_NS))
         ctx.close()
     # config 3 through the legacy shim: 12 channels, 512-us interrupts
     ns = int(FS * 512 / 1.0e6)                   # osgnss_next_step.c:150 (nsamp = fs*interr_int)
@@ -1281,6 +1288,8 @@ def result_line(out):
     for sub in list(t.get("layouts", {}).values()) + [t.get("closed_loop", {})]:
         for k in ("unit", "calls_per_launch", "realtime_channels_per_gpu"):
             sub.pop(k, None)   # = the tracking line's unit and TRACK_CPL
+    for sub in t.get("layouts", {}).values():
+        sub.get("roofline", {}).pop("kernel", None)   # packed layouts: <true, false>
     for sub in t.get("pcie_inclusive", {}).values():
         sub.pop("unit", None)
     return line
@@ -1443,7 +1452,8 @@ def main():
                              **pmc_hbm("track", TRACK_KERNEL, L_s),
                              "calls_per_launch": TRACK_CPL,
                              "kernel_ms_per_call": trk["kern_ms"],
-                             "kernel_ms_per_launch": trk["kern_ms"] * TRACK_CPL},
+                             "kernel_ms_per_launch": trk["kern_ms"] * TRACK_CPL,
+                             "us_per_3072_channel_ms": trk["kern_ms"] * 1e3 * 3072 / C},
                 "dumps_sane": trk["dumps_ok"],
                 "closed_loop": {
                     "metric": "1ms E/P/L correlations/sec with the gpsisr channel loops on the GPU",
@@ -1455,6 +1465,7 @@ def main():
                               "after its epilogue in the same wave, NCO words fed back on the "
                               "device, no host round trip",
                     "ms_per_call": trk["cl_ms"],
+                    "us_per_3072_channel_ms": trk["cl_ms"] * 1e3 * 3072 / C,
                     "kernel": TRACK_KERNEL_CL, "calls_per_launch": TRACK_CPL,
                     **pmc_hbm("track", TRACK_KERNEL_CL, trk["cl_ms"] * 1e-3 * TRACK_CPL),
                 },
@@ -1475,6 +1486,7 @@ def main():
                     "calls_per_launch": TRACK_CPL,
                     "kernel_ms_per_call": r["kern_ms"],
                     "kernel_ms_per_launch": r["kern_ms"] * TRACK_CPL,
+                    "us_per_3072_channel_ms": r["kern_ms"] * 1e3 * 3072 / r["channels"],
                     "realtime_channels_per_gpu": r["channels"] / r["kern_ms"],
                     "roofline": {"bound": "hbm",
                                  "kernel": TRACK_KERNEL_PK if "packed" in key else TRACK_KERNEL,
@@ -1492,7 +1504,7 @@ def main():
             out["tracking"]["layouts"] = lay
             out["tracking"]["pcie_inclusive"] = {
                 k: {"config": f"gnsscorr_track from pageable host buffers: {r['channels']} "
-                              f"channels on {TRACK_RX} streams, {r['h2d_bytes']} B H2D + results "
+                              f"channels on {TRACK_RX_HOST} streams, {r['h2d_bytes']} B H2D + results "
                               "D2H + stream sync per 1-ms call",
                     "value": r["channels"] / (r["mean_ms"] * 1e-3), "unit": "channel-ms/s",
                     "mean_ms_per_call": r["mean_ms"], "p99_ms_per_call": r["p99_ms"],

@@ -656,7 +656,6 @@ __device__ __forceinline__ void run_pieces(const int8_t* __restrict__ ifbuf, int
       // ---- lane state at its first sample
       const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
       const uint64_t r0 = X >> 32;
-      g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
       g.kph = (uint32_t)X;
       if (fast) {
         // closed form at the piece start; a dump between the lane's two pieces
@@ -1125,9 +1124,6 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
 // XCD-aware channel order keeps on one XCD.
 // ============================================================================
 constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
-#ifndef TRACK_LO_SPLIT
-#define TRACK_LO_SPLIT 1          // LO words as two 256-byte tables (pair2s)
-#endif
 #ifndef TRACK_PF
 #define TRACK_PF 1                // LO words and row bytes read ahead (pair2r, interval_end_s)
 #endif
@@ -1186,6 +1182,7 @@ struct StreamArgs {
 // interval end (see interval_end): flush the part before the carry, carry the
 // rest, step the half-chip; a dump adds the epoch's sums to the LDS and
 // starts the next epoch
+template <bool PF>
 __device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, int& e,
                                                int32_t* s_sum, const uint8_t* __restrict__ row) {
   seg_flush(g.pi, g.pq, g.lb, g.pb, g.eb, acc);
@@ -1194,9 +1191,7 @@ __device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, 
   g.tq = g.pq = rq;
   const bool cy = g.carried;
   g.hc += cy ? 1u : 0u;
-#if !TRACK_PF
-  g.ld = cy ? g.hc : g.ld;
-#endif
+  if constexpr (!PF) g.ld = cy ? g.hc : g.ld;
   g.carried = false;
   const bool dump = cy && g.hc >= c.D;   // correlator.c:251-281
   uint64_t any = __builtin_amdgcn_ballot_w64(dump);
@@ -1208,15 +1203,15 @@ __device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, 
       g.hc = 0;        // the bits of half-chip 0 come from the pre-reset index ld
     }
   }
-#if TRACK_PF
-  // a carry moves to index hc + 1 (the pre-reset index when it dumps): its row
-  // byte was read one interval ahead; the next one is read now
-  g.cb = cy ? g.nb : g.cb;
-  unpack8(g.cb, g.lb, g.pb, g.eb);
-  g.nb = row[g.hc + 1];
-#else
-  unpack8(row[g.ld], g.lb, g.pb, g.eb);
-#endif
+  if constexpr (PF) {
+    // a carry moves to index hc + 1 (the pre-reset index when it dumps): its row
+    // byte was read one interval ahead; the next one is read now
+    g.cb = cy ? g.nb : g.cb;
+    unpack8(g.cb, g.lb, g.pb, g.eb);
+    g.nb = row[g.hc + 1];
+  } else {
+    unpack8(row[g.ld], g.lb, g.pb, g.eb);
+  }
 }
 
 // pair2s with the pair's LO words already in registers (TRACK_PF: a piece's 16
@@ -1308,19 +1303,31 @@ __device__ __forceinline__ bool chan_setup(const gnsscorr_nco_cmd& cmd, gnsscorr
   return active;
 }
 
+// Open loop: at least 4 waves per SIMD (<= 128 VGPRs; the build takes 117, no
+// spills): 3072 channels put 3 waves on a SIMD, 12288 put 4; same-box A/B
+// 3 % faster than the unbounded build at 3072 channels.  The closed loop (gpsisr
+// inlined, ~150 VGPRs) keeps the default bound.
+#ifndef TRACK_STREAM_WAVES
+#define TRACK_STREAM_WAVES 4
+#endif
 template <bool PK, bool CLOSED>
-__global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A) {
+__global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) void osg_stream_kernel(
+    StreamArgs A) {
+  // the LO words read ahead (TRACK_PF) in the open loop only: in the closed loop
+  // their 32 registers pushed the kernel from 151 to 183 VGPRs (2 waves per SIMD:
+  // 32.6 -> 42.7 us per 3072-channel call, same box)
+  constexpr bool kPF = TRACK_PF && !CLOSED;
   extern __shared__ uint4 s_dyn[];
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = (int)threadIdx.x & 63;
   const int nsamp = A.nsamp;
   const int ep_cap = nsamp / GNSSCORR_OSG_ROW + 2;
-#if TRACK_PF
   // the 64 (a, b) LO word pairs as two 256-byte tables at a fixed LDS address,
   // shared by the workgroup's waves: a pair's words are one ds_read2_b32 whose
-  // address is the byte index 4 (a | b << 3) itself
+  // address is the byte index 4 (a | b << 3) itself (kPF); without the read-ahead
+  // each wave keeps its own copy beside its sums (s_lo)
   __shared__ uint32_t s_lot[128];
-  if (threadIdx.x < 64) {
+  if (kPF && threadIdx.x < 64) {
     const int a = lane & 7, b = lane >> 3;
     const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
     const uint32_t qa = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * a, 4) & 0xFFu;
@@ -1329,8 +1336,7 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
     s_lot[lane] = ia | qa << 8 | ib << 16 | qb << 24;
     s_lot[64 + lane] = qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24;
   }
-  __syncthreads();   // the only workgroup barrier: before any wave leaves
-#endif
+  if (kPF) __syncthreads();   // the only workgroup barrier: before any wave leaves
   uint8_t* wb = reinterpret_cast<uint8_t*>(s_dyn) + wave * stream_wave_lds(PK, nsamp);
   uint4* slot = reinterpret_cast<uint4*>(wb);                      // int8 only
   uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes);
@@ -1340,23 +1346,16 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
   const int C = A.n_channels;
   const int chn = xcd_channel(blockIdx.x, gridDim.x) * kStreamCh + wave;
   if (chn >= C) return;   // wave-uniform; no workgroup barrier from here on
-#if !TRACK_PF
-  {
+  if constexpr (!kPF) {
     const int a = lane & 7, b = lane >> 3;   // LO words of the sample pair (a, b)
     const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
     const uint32_t qa = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * a, 4) & 0xFFu;
     const uint32_t ib = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * b, 4) & 0xFFu;
     const uint32_t qb = (uint32_t)__builtin_amdgcn_sbfe((int)kLutQ, 4 * b, 4) & 0xFFu;
-#if TRACK_LO_SPLIT
     uint32_t* lt = reinterpret_cast<uint32_t*>(s_lo);
     lt[lane] = ia | qa << 8 | ib << 16 | qb << 24;
     lt[64 + lane] = qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24;
-#else
-    s_lo[lane] = make_uint2(ia | qa << 8 | ib << 16 | qb << 24,
-                            qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24);
-#endif
   }
-#endif
   const uint32_t* lox = reinterpret_cast<const uint32_t*>(s_lo);
   const uint32_t* loy = lox + 64;
   (void)lox;
@@ -1462,6 +1461,23 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
     for (int p = 0; active && p < n_pieces; p++) {
       const int n0 = p * kPieceSpan + lane * kPieceLen;
       const int L = max(0, min(kPieceLen, nsamp - n0));
+      g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
+      // the piece's 16 LO word pairs (pair q: carrier phases p0 + 2q cinc and
+      // p0 + (2q + 1) cinc, correlator.c:203-204), read before the piece's IF
+      // wait so that both LDS round trips overlap
+      uint32_t lwx[kPieceLen / 2], lwy[kPieceLen / 2];
+      if (kPF && fast) {
+        uint32_t pa = g.p0;
+#pragma unroll
+        for (int q = 0; q < kPieceLen / 2; q++) {
+          const uint32_t pb = pa + c.cinc;
+          const uint32_t off = ((pa >> 27) & 0x1Cu) | ((pb >> 24) & 0xE0u);   // 4 (a | b << 3)
+          const uint8_t* t = reinterpret_cast<const uint8_t*>(s_lot) + off;
+          lwx[q] = *reinterpret_cast<const uint32_t*>(t);
+          lwy[q] = *reinterpret_cast<const uint32_t*>(t + 256);
+          pa = pb + c.cinc;
+        }
+      }
       // ---- this lane's 32 samples as 16 pair words (4 chunks of 4)
       uint4 ch4[4];
       if constexpr (PK) {
@@ -1497,7 +1513,6 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
       if (L == 0) continue;
       const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
       const uint64_t r0 = X >> 32;
-      g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
       g.kph = (uint32_t)X;
       uint32_t ep;
       if (fast) hc_after_fast(c, r0, invD, g.hc, g.ld, ep);
@@ -1513,28 +1528,13 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
         }
       }
       if (fast) {
-#if TRACK_PF
-        // the piece's 16 LO word pairs: pair q's samples have carrier phases
-        // p0 + 2q cinc and p0 + (2q + 1) cinc (correlator.c:203-204)
-        uint32_t lwx[kPieceLen / 2], lwy[kPieceLen / 2];
-        {
-          uint32_t pa = g.p0;
-#pragma unroll
-          for (int q = 0; q < kPieceLen / 2; q++) {
-            const uint32_t pb = pa + c.cinc;
-            const uint32_t off = ((pa >> 27) & 0x1Cu) | ((pb >> 24) & 0xE0u);   // 4 (a | b << 3)
-            const uint8_t* t = reinterpret_cast<const uint8_t*>(s_lot) + off;
-            lwx[q] = *reinterpret_cast<const uint32_t*>(t);
-            lwy[q] = *reinterpret_cast<const uint32_t*>(t + 256);
-            pa = pb + c.cinc;
-          }
+        if constexpr (kPF) {
+          g.cb = row[g.ld];
+          g.nb = row[g.hc + 1];
+          unpack8(g.cb, g.lb, g.pb, g.eb);
+        } else {
+          unpack8(row[g.ld], g.lb, g.pb, g.eb);
         }
-        g.cb = row[g.ld];
-        g.nb = row[g.hc + 1];
-        unpack8(g.cb, g.lb, g.pb, g.eb);
-#else
-        unpack8(row[g.ld], g.lb, g.pb, g.eb);
-#endif
         g.ti = g.tq = g.pi = g.pq = 0;
         g.carried = false;
         if (__all(L == kPieceLen)) {
@@ -1544,14 +1544,9 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
 #pragma unroll
             for (int i = 0; i < 4; i++) {
               const int q = 4 * j + i;
-#if TRACK_PF
-              pair2r<false>(words[i], lwx[q], lwy[q], c, g);
-#elif TRACK_LO_SPLIT
-              pair2s<false>(words[i], c, g, lox, loy);
-#else
-              pair2<false>(words[i], c, g, s_lo);
-#endif
-              if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+              if constexpr (kPF) pair2r<false>(words[i], lwx[q], lwy[q], c, g);
+              else pair2s<false>(words[i], c, g, lox, loy);
+              if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s<kPF>(c, g, acc, e, s_sum, row);
             }
           }
         } else {
@@ -1562,17 +1557,14 @@ __global__ __launch_bounds__(64 * kStreamCh) void osg_stream_kernel(StreamArgs A
 #pragma unroll
             for (int i = 0; i < 4; i++) {
               const int q = 4 * j + i;
-#if TRACK_PF
-              if (q < np) pair2r<false>(words[i], lwx[q], lwy[q], c, g);
-              else if (q == np && (L & 1)) pair2r<true>(words[i] & 0xFFFFu, lwx[q], lwy[q], c, g);
-#elif TRACK_LO_SPLIT
-              if (q < np) pair2s<false>(words[i], c, g, lox, loy);
-              else if (q == np && (L & 1)) pair2s<true>(words[i] & 0xFFFFu, c, g, lox, loy);
-#else
-              if (q < np) pair2<false>(words[i], c, g, s_lo);
-              else if (q == np && (L & 1)) pair2<true>(words[i] & 0xFFFFu, c, g, s_lo);
-#endif
-              if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s(c, g, acc, e, s_sum, row);
+              if constexpr (kPF) {
+                if (q < np) pair2r<false>(words[i], lwx[q], lwy[q], c, g);
+                else if (q == np && (L & 1)) pair2r<true>(words[i] & 0xFFFFu, lwx[q], lwy[q], c, g);
+              } else {
+                if (q < np) pair2s<false>(words[i], c, g, lox, loy);
+                else if (q == np && (L & 1)) pair2s<true>(words[i] & 0xFFFFu, c, g, lox, loy);
+              }
+              if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s<kPF>(c, g, acc, e, s_sum, row);
             }
           }
         }

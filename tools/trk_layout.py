@@ -16,7 +16,7 @@ warmup = bench.TRACK_CPL   # one launch (bench.py's tracking lines: TRACK_CPL ca
 K = steps + warmup
 packed = layout.endswith("packed2")
 cs1 = layout.startswith("cs1")
-C = int(os.environ.get("TRK_C", "3072"))   # channels (TRK_C: other launch sizes)
+C = int(os.environ.get("TRK_C", str(bench.TRACK_C1)))   # channels (TRK_C: other launch sizes)
 n_streams = C if cs1 else C // 12
 stride = K * bench.TRACK_NS
 rng = np.random.default_rng(17)
