@@ -1590,12 +1590,23 @@ int g_init(gnsscorr_acq_ctx* c) {
   return GNSSCORR_OK;
 }
 
+int mx_dft_rows(gnsscorr_acq_ctx* c, const v2d* a, int src_rs, int rows, v2d* out, int rs);
+int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
+                 const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
+                 int dump_block);
+
+// DFT_N of natural rows: the mixed-radix plan where N has one, else Bluestein
+int gen_dft_rows(gnsscorr_acq_ctx* c, const v2d* a, int src_rs, int rows, v2d* out, int rs) {
+  return c->mix_nr ? mx_dft_rows(c, a, src_rs, rows, out, rs)
+                   : g_dft_rows(c, a, src_rs, rows, out, rs);
+}
+
 int g_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
   const long n = (long)n_codes * c->cfg.n_samples;
   hipLaunchKernelGGL(g_codes_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, d_codes, n,
                      (v2d*)c->d_in64);
   HIP_TRY(hipGetLastError());
-  return g_dft_rows(c, (const v2d*)c->d_in64, c->cfg.n_samples, n_codes, (v2d*)c->d_F64, c->rs64);
+  return gen_dft_rows(c, (const v2d*)c->d_in64, c->cfg.n_samples, n_codes, (v2d*)c->d_F64, c->rs64);
 }
 
 int g_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int n_freqs,
@@ -1617,12 +1628,15 @@ int g_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int
   int n_cls = 0;
   HIP_TRY(hipMemcpyAsync(&n_cls, c->d_nclass, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  return g_dft_rows(c, (const v2d*)c->d_in64, N, n_cls * n_blocks, (v2d*)c->d_X64, c->rs64);
+  return gen_dft_rows(c, (const v2d*)c->d_in64, N, n_cls * n_blocks, (v2d*)c->d_X64, c->rs64);
 }
 
 int g_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
                 const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
                 int dump_block) {
+  if (c->mix_nr)
+    return mx_correlate(c, n_blocks, mode, n_groups, n_bins, d_gcode, d_gfreq, spc, d_dump,
+                        dump_block);
   const int N = c->cfg.n_samples, M = c->gM;
   const bool nc = mode == GNSSCORR_ACQ_NONCOHERENT;
   const int n_units = n_groups * n_bins * (nc ? 1 : n_blocks);
@@ -1655,6 +1669,218 @@ int g_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n
   return GNSSCORR_OK;
 }
 
+// ---------------------------------------------------------------------------------
+// Mixed-radix Stockham FFT of length N (the generic path's default since round 5):
+// N = R_1 ... R_P, every R_i a radix the kernels are compiled for (mix_factor).
+// Pass i (Ns = R_1 ... R_{i-1}) reads elements j + r N/R_i (r < R_i) of a row,
+// multiplies element r by W_{Ns R}^{r k} (k = j mod Ns; = W_N^{r k N/(Ns R)}, the
+// table d_twN), runs a radix-R DFT in registers (dft<R>) and writes positions
+// (j / Ns) Ns R + k + r Ns: autosort, natural order out, no bit reversal.
+// Against Bluestein (two FFTs of length M = 2^q >= 2N - 1 per DFT plus the chirp
+// passes, ~60 N x 16 B of row traffic per correlation row at N = 38 192) a
+// correlation row moves ~5.5 N x 16 B: the product conj(X[k - m]) F[k] is formed
+// inside the first pass and |.|^2 / N^2 inside the last (added over the blocks of a
+// non-coherent search), so no pre / post passes run (acquisition.sci:107-132).
+// ---------------------------------------------------------------------------------
+constexpr int kMixThreads = 128;
+#ifndef MX_WAVES
+#define MX_WAVES 3
+#endif
+
+struct MixCorr {
+  const v2d* X;
+  const v2d* F;
+  int rs, n_blocks, nc_blk, n_bins, u0;
+  const int* group_code;
+  const int* group_freq;
+  const int2* fmap;
+};
+
+// MODE 0: rows in (stride in_rs) -> rows out (stride out_rs)
+// MODE 1: first pass of a correlation chunk: the input is y[n] = conj(X[n - m]) F[n] of
+//         unit u0 + row (its bin's class spectrum shifted by m, acquisition.sci:116)
+// MODE 2: last pass of a correlation chunk: |.|^2 / N^2 into pw (added when acc)
+// occupancy: a pass is latency bound (strided row loads, one butterfly per thread),
+// so the register allocator is held to 3 waves per SIMD up to radix 16 (the fused
+// first pass otherwise keeps all 2R complex loads in flight: 244 VGPRs, 2 waves;
+// at 4 waves radix 16 spills)
+template <int R>
+constexpr int mx_waves() { return R <= 16 ? MX_WAVES : 2; }
+template <int R, int MODE>
+__global__ __launch_bounds__(kMixThreads, mx_waves<R>()) void mx_pass(const v2d* __restrict__ in, int in_rs,
+                                                       v2d* __restrict__ out, int out_rs, int N,
+                                                       int Ns, const v2d* __restrict__ tw,
+                                                       MixCorr cp, double* __restrict__ pw,
+                                                       int acc) {
+  const int j = blockIdx.x * kMixThreads + threadIdx.x;   // < N / R
+  if (j >= N / R) return;
+  const long row = blockIdx.y;
+  const int NR = N / R;
+  v2d v[R];
+  if constexpr (MODE == 1) {
+    const int unit = cp.u0 + (int)row;
+    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
+    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
+    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
+    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
+    const v2d* Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
+    const v2d* Fr = cp.F + (long)cp.group_code[g] * cp.rs;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int n = j + r * NR;
+      int s = n - fm.y;
+      s += s < 0 ? N : 0;
+      const v2d x = Xr[s], f = Fr[n];
+      v[r] = (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))};
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; r++) v[r] = in[row * in_rs + j + r * NR];
+  }
+  const int k = j % Ns;
+  const int ts = k * (N / (Ns * R));   // r ts < N
+#pragma unroll
+  for (int r = 1; r < R; r++) v[r] = cmul(v[r], tw[r * ts]);
+  dft<R>(v);
+  const int d = (j / Ns) * Ns * R + k;
+  if constexpr (MODE == 2) {
+    const double sc = 1.0 / ((double)N * (double)N);
+    double* o = pw + row * N + d;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const double q = fma(v[r].x, v[r].x, v[r].y * v[r].y) * sc;
+      o[r * Ns] = acc ? o[r * Ns] + q : q;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; r++) out[row * out_rs + d + r * Ns] = v[r];
+  }
+}
+
+// the radices mx_pass is compiled for, largest first within a power of two
+#define MIX_RADICES(X) X(16) X(8) X(4) X(2) X(3) X(5) X(7) X(11) X(13) X(17) X(19) X(23) X(29) X(31)
+
+// N -> radices (powers of two as 16s, then one 8 / 4 / 2; odd primes); 0 when a
+// prime factor above 31 remains (Bluestein).  38192 -> 7, 16, 31, 11.
+int mix_factor(int N, int* r) {
+  int n = 0, m = N;
+  while (m % 16 == 0 && n < 24) { r[n++] = 16; m /= 16; }
+  if (m % 8 == 0) { r[n++] = 8; m /= 8; }
+  else if (m % 4 == 0) { r[n++] = 4; m /= 4; }
+  else if (m % 2 == 0) { r[n++] = 2; m /= 2; }
+  const int odd[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31};
+  for (int p : odd)
+    while (m % p == 0 && n < 24) { r[n++] = p; m /= p; }
+  if (m != 1 || n < 2) return 0;
+  // the fused passes take the smallest radices (fewest registers): the first (the
+  // correlation product, 2R loads) the smallest, the last (|.|^2) the next one
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++)
+      if (r[b] < r[a]) { const int t = r[a]; r[a] = r[b]; r[b] = t; }
+  const int second = r[1];
+  for (int a = 1; a + 1 < n; a++) r[a] = r[a + 1];
+  r[n - 1] = second;
+  return n;
+}
+
+template <int MODE>
+int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, int out_rs, int rows,
+              int Ns, const MixCorr& cp, double* pw, int acc) {
+  const int N = c->cfg.n_samples;
+  const dim3 grid((N / R + kMixThreads - 1) / kMixThreads, rows);
+  const v2d* tw = (const v2d*)c->d_twN;
+  switch (R) {
+#define MIX_CASE(RR)                                                                           \
+  case RR:                                                                                     \
+    hipLaunchKernelGGL((mx_pass<RR, MODE>), grid, dim3(kMixThreads), 0, c->stream, in, in_rs, \
+                       out, out_rs, N, Ns, tw, cp, pw, acc);                                   \
+    break;
+    MIX_RADICES(MIX_CASE)
+#undef MIX_CASE
+    default:
+      gnsscorr_set_error("acq64 mixed radix: no kernel for radix %d", R);
+      return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
+// DFT_N of `rows` natural rows a (stride src_rs) -> out (stride rs), chunked
+int mx_dft_rows(gnsscorr_acq_ctx* c, const v2d* a, int src_rs, int rows, v2d* out, int rs) {
+  const int N = c->cfg.n_samples, P = c->mix_nr;
+  const MixCorr none{};
+  for (int r0 = 0; r0 < rows; r0 += c->g_chunk) {
+    const int nr = rows - r0 < c->g_chunk ? rows - r0 : c->g_chunk;
+    v2d *A = (v2d*)c->d_gA, *B = (v2d*)c->d_gB;
+    const v2d* src = a + (long)r0 * src_rs;
+    int srs = src_rs, Ns = 1;
+    for (int i = 0; i < P; i++) {
+      const bool last = i + 1 == P;
+      v2d* dst = last ? out + (long)r0 * rs : (i % 2 == 0 ? A : B);
+      int rc = mx_launch<0>(c, c->mix_r[i], src, srs, dst, last ? rs : N, nr, Ns, none, nullptr, 0);
+      if (rc) return rc;
+      src = dst;
+      srs = N;
+      Ns *= c->mix_r[i];
+    }
+  }
+  return GNSSCORR_OK;
+}
+
+int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n_bins,
+                 const int32_t* d_gcode, const int32_t* d_gfreq, int spc, double* d_dump,
+                 int dump_block) {
+  const int N = c->cfg.n_samples, P = c->mix_nr;
+  const bool nc = mode == GNSSCORR_ACQ_NONCOHERENT;
+  const int n_units = n_groups * n_bins * (nc ? 1 : n_blocks);
+  for (int u0 = 0; u0 < n_units; u0 += c->g_chunk) {
+    const int nu = n_units - u0 < c->g_chunk ? n_units - u0 : c->g_chunk;
+    for (int b = 0; b < (nc ? n_blocks : 1); b++) {
+      MixCorr cp{(const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1,
+                 n_bins, u0, d_gcode, d_gfreq, (const int2*)c->d_fmap64};
+      v2d *A = (v2d*)c->d_gA, *B = (v2d*)c->d_gB;
+      const v2d* src = nullptr;
+      int Ns = 1;
+      for (int i = 0; i < P; i++) {
+        v2d* dst = i % 2 == 0 ? A : B;
+        int rc = i == 0 ? mx_launch<1>(c, c->mix_r[i], nullptr, 0, dst, N, nu, Ns, cp, nullptr, 0)
+                 : i + 1 == P ? mx_launch<2>(c, c->mix_r[i], src, N, nullptr, 0, nu, Ns, cp,
+                                             c->d_gpw, b > 0)
+                              : mx_launch<0>(c, c->mix_r[i], src, N, dst, N, nu, Ns, cp, nullptr, 0);
+        if (rc) return rc;
+        src = dst;
+        Ns *= c->mix_r[i];
+      }
+    }
+    hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
+                       (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats, d_dump,
+                       dump_block);
+    HIP_TRY(hipGetLastError());
+  }
+  return GNSSCORR_OK;
+}
+
+int mx_init(gnsscorr_acq_ctx* c) {
+  const long N = c->cfg.n_samples;
+  c->g_chunk = (int)((64L << 20) / (N * 16));   // ~64 MiB per work buffer
+  if (c->g_chunk < 1) c->g_chunk = 1;
+  if (c->g_chunk > 4096) c->g_chunk = 4096;
+  HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
+  HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)N * c->g_chunk));
+  HIP_TRY(hipMalloc(&c->d_gB, sizeof(double2) * (size_t)N * c->g_chunk));
+  HIP_TRY(hipMalloc(&c->d_gpw, sizeof(double) * (size_t)N * c->g_chunk));
+  double2* h = (double2*)malloc(sizeof(double2) * N);
+  if (!h) return GNSSCORR_ENOMEM;
+  for (long t = 0; t < N; t++) {   // W_N^t = exp(-2 pi i t / N)
+    const double a = -2.0 * M_PI * ((double)t / (double)N);
+    h[t] = make_double2(cos(a), sin(a));
+  }
+  hipError_t e = hipMemcpy(c->d_twN, h, sizeof(double2) * N, hipMemcpyHostToDevice);
+  free(h);
+  HIP_TRY(e);
+  return GNSSCORR_OK;
+}
+
 }  // namespace
 
 int acq64_plan_for(int n_samples) {
@@ -1666,6 +1892,11 @@ int acq64_plan_for(int n_samples) {
   if (n_samples >= 64 && n_samples <= (1 << 19)) return 3;
   return 0;
 }
+
+namespace {
+int mix_factor(int N, int* r);
+int mx_init(gnsscorr_acq_ctx* c);
+}  // namespace
 
 int acq64_init(gnsscorr_acq_ctx* c) {
   c->plan64 = acq64_plan_for(c->cfg.n_samples);
@@ -1680,7 +1911,13 @@ int acq64_init(gnsscorr_acq_ctx* c) {
   HIP_TRY(hipMemset(c->d_F64, 0, sizeof(double2) * (size_t)c->rs64 * c->cfg.max_codes));
   HIP_TRY(hipMalloc(&c->d_fmap64, sizeof(int2) * c->cfg.max_freqs));
   HIP_TRY(hipMalloc(&c->d_lead64, sizeof(int) * c->cfg.max_freqs));
-  if (c->plan64 == 3) return g_init(c);
+  if (c->plan64 == 3) {
+    // the mixed-radix plan unless N has a prime factor above 31 (or
+    // GNSSCORR_ACQ_BLUESTEIN=1: the chirp-z engine, for cross-checks)
+    const char* fb = getenv("GNSSCORR_ACQ_BLUESTEIN");
+    c->mix_nr = (fb && atoi(fb)) ? 0 : mix_factor(N, c->mix_r);
+    return c->mix_nr ? mx_init(c) : g_init(c);
+  }
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
   double2* tw = (double2*)malloc(sizeof(double2) * N);
   for (int j = 0; j < N; j++) {

@@ -37,6 +37,11 @@ struct gnsscorr_acq_ctx {
   double2 *d_gA = nullptr, *d_gB = nullptr;   // chunk x M work rows
   double* d_gpw = nullptr;              // chunk x N power rows
   int g_chunk = 0;                      // rows per chunk
+  // mixed-radix Stockham plan of the generic path (N a product of radices in
+  // {2..16, 17, 19, 23, 29, 31}; Bluestein otherwise or with GNSSCORR_ACQ_BLUESTEIN=1):
+  // mix_nr passes of radix mix_r[i] in global memory, twiddles d_twN (W_N^j)
+  int mix_nr = 0;
+  int mix_r[24] = {};
   // ---- shared
   int n_codes = 0;
   int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra

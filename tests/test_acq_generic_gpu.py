@@ -1,4 +1,4 @@
-"""GPU parity of the generic-N fp64 acquisition (Bluestein, csrc/acq64.hip): any
+"""GPU parity of the generic-N fp64 acquisition (csrc/acq64.hip): any
 samplesPerCode = round(fs / (codeFreqBasis / codeLength)) (acquisition.sci:47-48)
 without a compiled prime-factor plan, e.g. fs = 5 MHz (N = 5000) or the classic
 SoftGNSS front end at 38.192 MHz (N = 38192).
@@ -6,8 +6,11 @@ SoftGNSS front end at 38.192 MHz (N = 38192).
 Held to the same bar as the compiled plans (tests/test_acq_gpu.py check_rows,
 fp64 class): powers, peaks, second peaks and metrics within 1e-6 relative of the
 fp64 oracle (oracle/acq_oracle.py; observed ~1e-13), code phase and bin exact.
-The engine is also run at N = 16368 (GNSSCORR_ACQ_GENERIC=1) against the
-compiled 16 x 33 x 31 plan.
+Two engines: the mixed-radix Stockham plan (N a product of radices <= 31:
+5000 = 8 x 5^4, 38192 = 16 x 7 x 11 x 31; the default) and Bluestein's chirp-z
+(prime factors above 31, or GNSSCORR_ACQ_BLUESTEIN=1); both are held to the
+oracle and to each other.  The generic engine also runs at N = 16368
+(GNSSCORR_ACQ_GENERIC=1) against the compiled 16 x 33 x 31 plan.
 """
 import numpy as np
 import pytest
@@ -24,8 +27,11 @@ def _scene(gpu, fs, n_ms, seed):
     return gpu.ifgen(n_ms * int(round(fs / 1000.0)), sigs, fs=fs, seed=seed)
 
 
-@pytest.mark.parametrize("fs", [5.0e6, 38.192e6])
-def test_power_row_generic(gpu, fs):
+@pytest.mark.parametrize("engine", ["mixed", "bluestein"])
+@pytest.mark.parametrize("fs", [5.0e6, 38.192e6, 4.111e6])
+def test_power_row_generic(gpu, fs, engine, monkeypatch):
+    """4.111 MHz: N = 4111 is prime, Bluestein either way."""
+    monkeypatch.setenv("GNSSCORR_ACQ_BLUESTEIN", "1" if engine == "bluestein" else "0")
     n = int(round(fs / 1000.0))
     ctx = gpu.AcqCtx(fs, n, max_freqs=4, max_blocks=2, max_codes=2)
     codes = np.stack([A.make_ca_table_row(p, fs) for p in (19, 6)])
@@ -100,3 +106,52 @@ def test_generic_engine_at_16368_matches_compiled_plan(gpu, monkeypatch):
     print(f"[generic vs PFA at 16368] max peak rel diff {rel.max():.3e}")
     assert rel.max() < 1e-9
     assert np.allclose(r0["metric"], r1["metric"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
+def test_search_38192_mixed_radix(gpu, mode):
+    """The classic SoftGNSS front end (N = 38192 = 16 x 7 x 11 x 31, the mixed-radix
+    plan) against the oracle: 3 PRNs x 9 bins."""
+    fs, n = 38.192e6, 38192
+    nb = 2
+    ctx = gpu.AcqCtx(fs, n, max_freqs=16, max_blocks=nb, max_codes=3)
+    prns = [6, 11, 19]
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in prns])
+    ctx.set_codes(codes)
+    IF = _scene(gpu, fs, nb, 0x5EED0024)
+    freqs = 2.42e6 + 500.0 * np.arange(-4, 5)
+    gf = np.tile(np.arange(len(freqs)), (3, 1))
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    res, rows = ctx.search(IF, nb, freqs, np.arange(3), gf, spc=37, mode=m)
+    ref, ref_rows = A.acquire(IF, fs, codes, freqs, gf, spc=37, n_blocks=nb,
+                              noncoherent=mode == "noncoherent", return_rows=True)
+    if mode == "noncoherent":
+        for rr in ref_rows:
+            for r in rr:
+                r["block"] = -1
+    check_rows(res, rows, ref, ref_rows, True, label=f"mixed-38192-{mode}")
+    assert res[0]["metric"] > 2.5 and res[2]["metric"] > 2.5
+
+
+@pytest.mark.parametrize("fs", [5.0e6, 38.192e6])
+def test_mixed_radix_equals_bluestein(gpu, fs, monkeypatch):
+    """The two generic engines on one search: decisions identical, powers within
+    1e-9 relative of each other (both are fp64 DFTs of the same rows)."""
+    n = int(round(fs / 1000.0))
+    IF = _scene(gpu, fs, 2, 0x5EED0025)
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in (6, 19, 25)])
+    freqs = 2.42e6 + 500.0 * np.arange(-6, 7)
+    gf = np.tile(np.arange(len(freqs)), (3, 1))
+    out = []
+    for bl in ("0", "1"):
+        monkeypatch.setenv("GNSSCORR_ACQ_BLUESTEIN", bl)
+        ctx = gpu.AcqCtx(fs, n, max_freqs=16, max_blocks=2, max_codes=3)
+        ctx.set_codes(codes)
+        out.append(ctx.search(IF, 2, freqs, np.arange(3), gf, spc=int(round(fs / 1.023e6))))
+    (r0, w0), (r1, w1) = out
+    assert (r0["code_phase"] == r1["code_phase"]).all() and (r0["bin"] == r1["bin"]).all()
+    assert (w0["argmax"] == w1["argmax"]).all() and (w0["block"] == w1["block"]).all()
+    rel = np.abs(w0["peak"] - w1["peak"]) / w0["peak"]
+    rel2 = np.abs(w0["second"] - w1["second"]) / w0["second"]
+    print(f"[mixed vs bluestein N={n}] peak {rel.max():.3e} second {rel2.max():.3e}")
+    assert rel.max() < 1e-9 and rel2.max() < 1e-9
