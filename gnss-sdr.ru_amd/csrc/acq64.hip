@@ -1451,6 +1451,49 @@ __global__ __launch_bounds__(kGThreads) void g_stats_kernel(const double* __rest
   }
 }
 
+// One-pass row statistics (the generic path's default): 1024 threads, thread t
+// scans k = t, t + 1024, ...  Its elements lie 1024 samples apart, so the open
+// window (argmax - spc, argmax + spc) holds at most one of them when 2 spc - 1 <=
+// 1024: the thread's runner-up stands in for its maximum when that maximum is
+// inside the window (acq64_corr_kernel's per-thread top-2).  Same results as
+// g_stats_kernel's two passes; one read of the row.
+constexpr int kStatsThreads = 1024;
+__global__ __launch_bounds__(kStatsThreads) void g_stats1_kernel(
+    const double* __restrict__ pw, int N, int u0, int n_blocks, int nc, int spc,
+    gnsscorr_acq_row* __restrict__ stats, double* __restrict__ dump, int dump_block) {
+  __shared__ double s_v[kStatsThreads / 64], s_m[kStatsThreads / 64];
+  __shared__ int s_k[kStatsThreads / 64];
+  const int unit = u0 + blockIdx.x;
+  const double* row = pw + (long)blockIdx.x * N;
+  const int rowid = nc ? unit : unit / n_blocks;
+  const int blk0 = nc ? 0 : unit % n_blocks;
+  double a1 = -1.0, a2 = -1.0;
+  int ak = INT_MAX;
+  for (int k = threadIdx.x; k < N; k += kStatsThreads) {
+    const double v = row[k];
+    a2 = v > a1 ? a1 : fmax(a2, v);
+    ak = v > a1 ? k : ak;       // strict: the first index of the thread's maximum
+    a1 = fmax(a1, v);
+  }
+  double bv = a1;
+  int bk = ak;
+  block_argmax<kStatsThreads / 64>(bv, bk, s_v, s_k);
+  int d = ak == INT_MAX ? 0 : ak - bk;
+  d += d < 0 ? N : 0;
+  double sv = (ak != INT_MAX && d >= spc && d <= N - spc) ? a1 : a2;
+  sv = block_max0<kStatsThreads / 64>(sv, s_m);
+  if (dump && !nc && blk0 == dump_block)
+    for (int k = threadIdx.x; k < N; k += kStatsThreads) dump[(long)rowid * N + k] = row[k];
+  if (threadIdx.x == 0) {
+    gnsscorr_acq_row r;
+    r.peak = bv;
+    r.second = sv;
+    r.argmax = bk;
+    r.block = nc ? -1 : blk0;
+    stats[(long)rowid * n_blocks + blk0] = r;
+  }
+}
+
 // wipe-off rows in natural order (acq64_wipe_kernel with a runtime N)
 __global__ __launch_bounds__(256) void g_wipe_kernel(const int8_t* __restrict__ src, int iq,
                                                      int n_blocks, int coh,
@@ -1661,9 +1704,14 @@ int g_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n
                          dim3(kGThreads), 0, c->stream, D, N, M, b > 0, c->d_gpw);
       HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
-                       (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats, d_dump,
-                       dump_block);
+    if (2 * spc - 1 <= kStatsThreads)
+      hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, c->stream,
+                         (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
+                         d_dump, dump_block);
+    else
+      hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
+                         (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
+                         d_dump, dump_block);
     HIP_TRY(hipGetLastError());
   }
   return GNSSCORR_OK;
@@ -1852,9 +1900,14 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
         Ns *= c->mix_r[i];
       }
     }
-    hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
-                       (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats, d_dump,
-                       dump_block);
+    if (2 * spc - 1 <= kStatsThreads)
+      hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, c->stream,
+                         (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
+                         d_dump, dump_block);
+    else
+      hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
+                         (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
+                         d_dump, dump_block);
     HIP_TRY(hipGetLastError());
   }
   return GNSSCORR_OK;
