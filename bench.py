@@ -533,7 +533,9 @@ def run_fullsky(dist, dev, steps, warmup):
         found = sum(1 for p in gps if res[int(p) - 1][3]["metric"] > 2.5) + \
             sum(1 for k in glo if res[32 + int(k) + 7][3]["metric"] > 2.5)
     proj = None
-    if dist.world == 1:
+    # (BENCH_FULLSKY_PROJECTION=0: the per-section PMC pass, whose per-launch
+    # averages would otherwise mix the shard launches of every world size)
+    if dist.world == 1 and os.environ.get("BENCH_FULLSKY_PROJECTION", "1") != "0":
         del fsky
         proj = fullsky_shard_projection(dev, if_gps, if_glo, steps, dt / steps)
     return dict(dt=dt, steps=steps, found=found, n_planted=len(gps) + len(glo),
@@ -1538,7 +1540,9 @@ def main():
                              "frac": dp / k_s / 1e12 / PEAK_FP64_TFLOPS,
                              "hbm_algorithmic_GBs": C * sgt["steps"] * sgt["fs"] / 1000 * 2 / 14
                              / k_s / 1e9,
-                             **pmc_hbm("sgt", "sgt_track_kernel", k_s),
+                             # the wave-per-channel instance (>= 1024 channels); the
+                             # 14-channel latency run is the <2, true, 256> one
+                             **pmc_hbm("sgt", "sgt_track_kernel<2, true, 64>", k_s),
                              "kernel_ms_per_launch": sgt["kern_ms"]},
                 "epochs_sane": sgt["ok"],
             }

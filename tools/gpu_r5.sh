@@ -42,10 +42,10 @@ run_prof() {
 run_pmc() {
   echo "== pmc (per section; HBM bytes into a copy of profiles/pmc_traffic.json)"
   cp profiles/pmc_traffic.json $O/pmc_traffic.json
-  for S in acq track fullsky glo_coherent sgt sdr; do
+  for S in ${PMC_SECTIONS:-acq track fullsky glo_coherent sgt sdr}; do
     mkdir -p $O/pmc_$S
     for C in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
+      BENCH_FULLSKY_PROJECTION=0 timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
         python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1
     done
     R=""
@@ -53,7 +53,7 @@ run_pmc() {
     python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S $R > /dev/null
     echo "pmc section $S ok"
   done
-  for L in cs1_int8 cs1_packed2 rx12_int8 rx12_packed2; do
+  for L in ${PMC_LAYOUTS:-cs1_int8 cs1_packed2 rx12_int8 rx12_packed2}; do
     mkdir -p $O/pmc_trk_$L
     for C in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES"; do
       D=$(echo $C | cut -d' ' -f1)
