@@ -199,7 +199,9 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Wave mode asks for 3 waves per SIMD (<= 168 VGPRs): measured 3 % faster than
 // the 2 the chunked path otherwise compiles to.
 template <int FT, bool CLOSED, int MAXT>
-// (the prefix columns limit a CU to 7 wave-mode workgroups: 2 waves per SIMD)
+// (with the prefix columns a wave-mode workgroup takes 16 KiB + the code table:
+// 7 fit a CU for GLONASS (511 chips, 4112 B table), 6 for GPS (1023 chips, 8208 B);
+// that is under 2 waves per SIMD, so the bound asks for 2)
 __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) : 1) void sgt_track_kernel(
     SgtParams p, const int8_t* __restrict__ ifbuf, int64_t stride, int64_t n_samples,
     const uint32_t* __restrict__ codes, gnsscorr_sgt_chan* __restrict__ chans, int n_epochs,
