@@ -613,6 +613,50 @@ def run_glo_coherent(dist, dev, steps, warmup):
     return dict(dt=dt, steps=steps, nb=nb, found=found, n_planted=len(glo))
 
 
+GPS_SCI_FS, GPS_SCI_COH, GPS_SCI_BAND = 16.0e6, 4, 14.0   # SCI/GPS/L1/initSettings.sci:68-87
+
+
+def run_gps_scilab(dist, dev, steps, warmup):
+    """The Scilab GPS receiver's own default acquisition (initSettings.sci:68-87):
+    fs 16 MHz (samplesPerCode 16000: the 40 x 40 x 10 fp64 plan), 32 PRN x 113 bins
+    (14 kHz at 125 Hz) x 2 blocks of 4 ms coherent, resident IF, one search per step
+    (acquisition.sci:46-192; parity in tests/test_acq_16m_gpu.py)."""
+    fs, n = GPS_SCI_FS, int(round(GPS_SCI_FS / 1000.0))
+    rng = np.random.default_rng(0x5EED0040 + dist.rank)
+    planted = rng.choice(np.arange(1, 33), 6, replace=False)
+    sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
+                 doppler=float(rng.uniform(-5000, 5000)), cn0=44.0, data_bits=1) for p in planted]
+    IF = gc.ifgen(2 * GPS_SCI_COH * n, sigs, fs=fs, seed=0x5EED0041 + dist.rank)
+    nb = int(round(GPS_SCI_BAND * 2 * GPS_SCI_COH)) + 1         # acquisition.sci:101-104
+    freqs = 2.42e6 - (GPS_SCI_BAND / 2) * 1000 + (1000 / (2 * GPS_SCI_COH)) * np.arange(nb)
+    codes = np.stack([gc.sample_code(gc.ca_code(p), 1.023e6, fs, n) for p in range(1, 33)])
+    ctx = gc.AcqCtx(fs, n, device=dev, max_freqs=nb, max_blocks=2 * GPS_SCI_COH, max_codes=32)
+    ctx.set_codes(codes)
+    ctx.set_coherent(GPS_SCI_COH)
+    d_if = gc.DevBuf.from_array(IF, dev)
+    d_f = gc.DevBuf.from_array(freqs, dev)
+    d_gc = gc.DevBuf.from_array(np.arange(32, dtype=np.int32), dev)
+    d_gf = gc.DevBuf.from_array(np.tile(np.arange(nb, dtype=np.int32), 32), dev)
+    d_rows = gc.DevBuf(32 * nb * gc.ACQ_ROW.itemsize, dev)
+    d_res = gc.DevBuf(32 * gc.ACQ_RESULT.itemsize, dev)
+
+    def step():
+        ctx.search_dev(d_if.ptr, 2, nb, d_f.ptr, 32, nb, d_gc.ptr, d_gf.ptr, d_rows.ptr,
+                       d_res.ptr, spc=16)
+    for _ in range(warmup):
+        step()
+    ctx.sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.sync()
+    dt = dist.max(time.perf_counter() - t0)
+    res = d_res.download(np.uint8).view(gc.ACQ_RESULT)
+    found = int(sum(res[int(p) - 1]["metric"] > 2.5 for p in planted))
+    return dict(dt=dt, steps=steps, nb=nb, n=n, found=found, n_planted=len(planted))
+
+
 SDR_REC, SDR_SV, SDR_ROWS, SDR_N = 64, 32, 120, 2048
 SDR_CORR_CH = 4096
 # doAcqStrong int-op model per (sv, row): cmulsc 8/sample, 2048-pt int16 IFFT (11 ranks x
@@ -1228,7 +1272,8 @@ def launch_ranks(n: int, argv) -> int:
 # projection) come last.  The headline keys come first (the contract's keys).
 SECTION_ORDER = ("sdr_acquisition", "sdr_acquisition_medium", "sdr_acquisition_weak",
                  "sdr_tracking", "sdr_channel", "sdr_closed_loop", "sdr_frontend",
-                 "acquisition_f32", "acquisition_generic", "glonass_acquisition_5ms",
+                 "acquisition_f32", "acquisition_generic", "gps_acquisition_scilab",
+                 "glonass_acquisition_5ms",
                  "executed_fp64", "single_search", "ranks", "fullsky", "glonass_tracking",
                  "tracking")
 # descriptive strings moved out of the printed line into the detail file (DESIGN.md 6
@@ -1277,6 +1322,9 @@ def result_line(out):
     for k in SECTION_ORDER:
         if k in out:
             line[k] = compact(out[k])
+            if k not in ("tracking", "glonass_tracking", "fullsky") and \
+                    isinstance(line[k], dict) and isinstance(line[k].get("roofline"), dict):
+                line[k]["roofline"].pop("kernel", None)   # named in DESIGN.md 6
     if "ranks" in line:   # one runtime path is enough; every rank's device and PCI id stay
         line["ranks"] = [{k: v for k, v in r.items() if k != "hip_runtime" or r["rank"] == 0}
                          for r in line["ranks"]]
@@ -1357,6 +1405,7 @@ def main():
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
     gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps // 5, 5), 2)
     gen = None if a.skip_track else run_acq_generic(dist, dev, max(a.steps // 10, 3), 1)
+    gsc = None if a.skip_track else run_gps_scilab(dist, dev, max(a.steps // 5, 5), 2)
 
     if dist.rank == 0:
         W = dist.world
@@ -1577,6 +1626,23 @@ def main():
                                           pmc_run_bytes("fullsky") / W, sky_ms * 1e-3),
                              "traffic": pmc_traffic("acq64_corr_kernel<Plan<16368, 16, 33, 31, "
                                                     "512, true>, 1, false>", "fullsky")},
+            }
+        if gsc:
+            cells = 32 * gsc["nb"] * gsc["n"]
+            fl = cells * N_BLK * (5.0 * np.log2(gsc["n"]) + 10)
+            out["gps_acquisition_scilab"] = {
+                "metric": "acquisition cells/sec (the Scilab GPS receiver's default search)",
+                "value": cells * gsc["steps"] * W / gsc["dt"], "unit": "cells/s",
+                "ms_per_search": gsc["dt"] / gsc["steps"] * 1e3,
+                "config": f"SCI/GPS/L1/initSettings.sci defaults: 32 PRN x {gsc['nb']} bins (14 kHz "
+                          f"at 125 Hz) x 16000 code phases, 2 blocks of {GPS_SCI_COH} ms coherent, "
+                          "16 Msps, fp64 (40 x 40 x 10 plan), IF resident in HBM",
+                "planted_found": f"{gsc['found']}/{gsc['n_planted']}",
+                "dtype": "f64",
+                "roofline": {"bound": "valu", "kernel": "acq64 (whole search)",
+                             "achieved": fl / (gsc["dt"] / gsc["steps"]) / 1e12,
+                             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
+                             "frac": fl / (gsc["dt"] / gsc["steps"]) / 1e12 / PEAK_FP64_TFLOPS},
             }
         if gco:
             cells = 14 * gco["nb"] * N

@@ -59,6 +59,7 @@ def test_bench_main_assembles_the_json_line(monkeypatch):
         run_sdr=lambda *a, **k: _D(mw=_D(medium=_D(), weak=_D()), loop=_D(), long=_D(),
                                    bufs=None),
         run_glo_coherent=lambda *a, **k: _D(found=4, n_planted=4),
+        run_gps_scilab=lambda *a, **k: _D(found=6, n_planted=6, nb=113, n=16000),
         run_acq_generic=lambda *a, **k: _D(found=8, n_planted=8, fs=38.192e6, n=38192))
     for k, v in stubs.items():
         monkeypatch.setattr(bench, k, v)
