@@ -1667,7 +1667,13 @@ static int correlate_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_g
     return GNSSCORR_EINVAL;
   }
   const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;  // work units per row
-  const int nrec = c->prec == GNSSCORR_ACQ_F64 ? c->spec_recs : 1;
+  // records: every group on every record (virtual groups), or with a per-group
+  // record table each group on its own record only
+  const int nrec = c->prec == GNSSCORR_ACQ_F64 && !c->d_group_rec ? c->spec_recs : 1;
+  if (c->d_group_rec && (c->prec != GNSSCORR_ACQ_F64 || c->plan64 == 3 || d_dump)) {
+    gnsscorr_set_error("gnsscorr_acq_correlate: per-group records need a compiled fp64 plan");
+    return GNSSCORR_EINVAL;
+  }
   const int gall = n_groups * nrec;   // virtual groups rec * n_groups + g
   rc = ensure_order(c, gall, n_bins, upr);
   if (rc) return rc;
@@ -1842,12 +1848,13 @@ extern "C" int gnsscorr_acq_search(gnsscorr_acq_ctx* c, const int8_t* h_if, int 
   rc = search_launch(c, c->d_if, iq, n_blocks, mode, n_freqs, c->d_freqs, n_groups, n_bins,
                      c->d_gcode, c->d_gfreq, spc, c->d_rows, c->d_res, nullptr, -1);
   if (rc) return rc;
+  const int nro = c->d_group_rec ? 1 : c->recs;   // per-group records: one result per group
   if (h_rows)
     HIP_TRY(hipMemcpyAsync(h_rows, c->d_rows,
-                           sizeof(gnsscorr_acq_row) * c->recs * n_groups * n_bins,
+                           sizeof(gnsscorr_acq_row) * nro * n_groups * n_bins,
                            hipMemcpyDeviceToHost, c->stream));
   if (h_res)
-    HIP_TRY(hipMemcpyAsync(h_res, c->d_res, sizeof(gnsscorr_acq_result) * c->recs * n_groups,
+    HIP_TRY(hipMemcpyAsync(h_res, c->d_res, sizeof(gnsscorr_acq_result) * nro * n_groups,
                            hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return GNSSCORR_OK;
@@ -1889,6 +1896,17 @@ extern "C" int gnsscorr_acq_set_coherent(gnsscorr_acq_ctx* c, int coh_ms) {
   }
   c->coh = coh_ms;
   c->spec_blocks = 0;   // resident spectra were made with the previous setting
+  return GNSSCORR_OK;
+}
+
+extern "C" int gnsscorr_acq_set_group_records(gnsscorr_acq_ctx* c, const int32_t* d_group_rec) {
+  if (!c) return GNSSCORR_EINVAL;
+  if (d_group_rec && (c->prec != GNSSCORR_ACQ_F64 || c->plan64 == 3)) {
+    gnsscorr_set_error("gnsscorr_acq_set_group_records: needs the fp64 precision and a compiled "
+                       "plan (N = 16368 or 16000)");
+    return GNSSCORR_EINVAL;
+  }
+  c->d_group_rec = d_group_rec;   // the caller keeps it alive and in range [0, records)
   return GNSSCORR_OK;
 }
 

@@ -920,7 +920,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     const int* __restrict__ group_code, const int* __restrict__ group_freq, int n_bins, int spc,
     gnsscorr_acq_row* __restrict__ stats, double* __restrict__ dump, int dump_block,
     const int* __restrict__ order, const int2* __restrict__ fmap, const v2d* __restrict__ twN,
-    int gpr, int nbT) {
+    int gpr, int nbT, const int* __restrict__ group_rec) {
   constexpr int N = P::N, R1 = P::R1, R3 = P::R3, T = P::T, K3 = P::K3, L = P::L;
   constexpr bool kNC = MODE == GNSSCORR_ACQ_NONCOHERENT;
   // non-coherent: a thread's first kE running sums live in the LDS left over
@@ -948,8 +948,9 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   const int nblk = kNC ? n_blocks : 1;
   // records (gnsscorr_acq_set_records): virtual group gv = rec * gpr + g reads
   // blocks rec * n_blocks .. of the nbT resident blocks per class
+  // (gnsscorr_acq_set_group_records: group g searches record group_rec[g] only)
   const int gv = rowid / n_bins, bin = rowid % n_bins;
-  const int rec = gv / gpr, g = gv - rec * gpr;
+  const int rec = group_rec ? group_rec[gv] : gv / gpr, g = group_rec ? gv : gv - rec * gpr;
   const int code = group_code[g];
   const int2 fm = fmap[group_freq[g * n_bins + bin]];
   const int m = fm.y;
@@ -1294,7 +1295,7 @@ int corr_launch(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_units, int n_
   hipLaunchKernelGGL((acq64_corr_kernel<P, M, D>), dim3(n_units), dim3(P::TB), 0, c->stream, \
                      (const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, d_gcode,   \
                      d_gfreq, n_bins, spc, c->d_stats, d_dump, dump_block, c->d_order,         \
-                     c->d_fmap64, (const v2d*)c->d_twN, gpr, nbT)
+                     c->d_fmap64, (const v2d*)c->d_twN, gpr, nbT, c->d_group_rec)
   if (d_dump)
     ACQ64_LAUNCH(GNSSCORR_ACQ_BEST_OF_BLOCKS, true);
   else if (mode == GNSSCORR_ACQ_NONCOHERENT)
@@ -2059,7 +2060,7 @@ int acq64_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, i
   // n_groups per record; the units of every record of the resident spectra run
   // in one launch (virtual groups rec * n_groups + g)
   const int upr = mode == GNSSCORR_ACQ_NONCOHERENT ? 1 : n_blocks;
-  const int n_units = c->spec_recs * n_groups * n_bins * upr;
+  const int n_units = (c->d_group_rec ? 1 : c->spec_recs) * n_groups * n_bins * upr;
   if (c->plan64 == 3)
     return g_correlate(c, n_blocks, mode, n_groups, n_bins, d_gcode, d_gfreq, spc, d_dump,
                        dump_block);

@@ -54,6 +54,8 @@ struct gnsscorr_acq_ctx {
   int n_cu = 256;                       // persistent grid of the pipelined kernel
   int coh = 1;                          // code periods per coherent block (set_coherent)
   int recs = 1;                         // records per search (set_records, fp64 plans)
+  const int32_t* d_group_rec = nullptr; // per group: its IF record (set_group_records; NULL: every
+                                        // group on every record)
   int spec_recs = 1;                    // records of the resident IF spectra
   gnsscorr_acq_row* d_stats = nullptr;  // per (row, block) statistics
   size_t cap_stats = 0;

@@ -171,7 +171,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
     "gnsscorr_acq_spectra_dev", "gnsscorr_acq_correlate_dev", "gnsscorr_acq_select_dev",
     "gnsscorr_acq_sync", "gnsscorr_acq_stream", "gnsscorr_acq_set_coherent",
-    "gnsscorr_acq_set_records",
+    "gnsscorr_acq_set_records", "gnsscorr_acq_set_group_records",
     "gnsscorr_sgt_loop_coefs", "gnsscorr_sgt_init_chan", "gnsscorr_sgt_create",
     "gnsscorr_sgt_destroy", "gnsscorr_sgt_track_dev", "gnsscorr_sgt_track", "gnsscorr_sgt_sync",
     "gnsscorr_sgt_stream", "gnsscorr_sgt_replay", "gnsscorr_sgt_replay_dev",
@@ -248,6 +248,7 @@ def lib() -> C.CDLL:
         "gnsscorr_acq_sync": (I, [P]),
         "gnsscorr_acq_set_coherent": (I, [P, I]),
         "gnsscorr_acq_set_records": (I, [P, I]),
+        "gnsscorr_acq_set_group_records": (I, [P, P]),
         "gnsscorr_acq_stream": (P, [P]),
         "gnsscorr_sgt_loop_coefs": (None, [C.POINTER(SgtCfg)] + [C.POINTER(D)] * 5),
         "gnsscorr_sgt_init_chan": (I, [C.POINTER(SgtCfg), I, I, I64, I64, D, P]),
@@ -615,7 +616,7 @@ class AcqCtx:
         group_code = np.ascontiguousarray(group_code, np.int32)
         group_freq = np.ascontiguousarray(group_freq, np.int32).reshape(len(group_code), -1)
         G, B = group_freq.shape
-        R = self.records
+        R = 1 if getattr(self, "_group_rec", None) is not None else self.records
         rows = np.zeros(R * G * B, ACQ_ROW)
         res = np.zeros(R * G, ACQ_RESULT)
         _check(lib().gnsscorr_acq_search(self.h, _ptr(if_samples), int(iq), n_blocks, mode,
@@ -631,6 +632,14 @@ class AcqCtx:
         in one launch; search() then returns (R, G) results and (R, G, B) rows."""
         _check(lib().gnsscorr_acq_set_records(self.h, int(n_records)), "gnsscorr_acq_set_records")
         self.records = int(n_records)
+
+    def set_group_records(self, d_group_rec):
+        """Per-group IF records (gnsscorr_acq_set_group_records): a device int32 array
+        (DevBuf or pointer), group g searched on record d_group_rec[g] only; None: off."""
+        ptr = None if d_group_rec is None else getattr(d_group_rec, "ptr", d_group_rec)
+        _check(lib().gnsscorr_acq_set_group_records(self.h, ptr),
+               "gnsscorr_acq_set_group_records")
+        self._group_rec = d_group_rec   # keep the device array alive
 
     def set_coherent(self, coh_ms: int):
         """settings.acqCohIntegration: code periods per coherent block (default 1)."""

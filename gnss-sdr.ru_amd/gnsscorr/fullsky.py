@@ -11,7 +11,7 @@ i % world == r), each rank runs the same HIP kernels on its own GPU, and the
 only exchange is the final gather of the per-group results (a few hundred
 bytes) -- done by the caller over gloo, not RCCL.
 
-Plumbing over the C-ABI (libgnsscorr.so); the computation is in acq.hip.
+Plumbing over the C-ABI (libgnsscorr.so); the computation is in acq64.hip.
 """
 from __future__ import annotations
 
@@ -42,6 +42,13 @@ def merge(shards: list[list[tuple]]) -> list[tuple]:
 
 
 class FullSky:
+    """One rank's share of the full-sky search in ONE correlation launch (round 5):
+    the GPS and GLONASS IF records sit end to end as two records of one fp64
+    context, every group carries its record (gnsscorr_acq_set_group_records), and
+    the code table holds the rank's C/A codes plus the ST code.  At world 8 a rank's
+    205-246 rows then run as one round of the CUs instead of two launches side by
+    side."""
+
     def __init__(self, fs: float = 16.368e6, n_ms: int = 10, n_bins: int = 41,
                  bin_hz: float = 500.0, if_gps: float = 2.42e6, if_glo: float = 1.0e6,
                  glo_step: float = 0.5625e6, rank: int = 0, world: int = 1, device: int = 0,
@@ -50,34 +57,41 @@ class FullSky:
         self.fs, self.n_ms, self.n_bins, self.spc, self.device = fs, n_ms, n_bins, spc, device
         self.mine = shard(len(GROUPS), world, rank)
         rel = bin_hz * (np.arange(n_bins) - (n_bins - 1) / 2.0)
-        self.parts = []
         gps = [GROUPS[i][1] for i in self.mine if GROUPS[i][0] == 0]
         glo = [GROUPS[i][1] for i in self.mine if GROUPS[i][0] == 1]
-        if gps:
-            codes = np.stack([sample_code(ca_code(p), 1.023e6, fs, self.N) for p in gps])
-            freqs = if_gps + rel
-            gf = np.tile(np.arange(n_bins, dtype=np.int32), (len(gps), 1))
-            self.parts.append(self._part(0, gps, codes, freqs, np.arange(len(gps)), gf))
+        self.ids = [(0, p) for p in gps] + [(1, k) for k in glo]   # result order
+        self.two = bool(gps) and bool(glo)
+        codes, freqs, gcode, grec = [], [], [], []
+        for p in gps:
+            gcode.append(len(codes))
+            codes.append(sample_code(ca_code(p), 1.023e6, fs, self.N))
+            grec.append(0)
+            freqs.append(if_gps + rel)
         if glo:
-            codes = sample_code(st_code(), 0.511e6, fs, self.N)[None, :]
-            freqs = np.concatenate([if_glo + k * glo_step + rel for k in glo])
-            gf = np.arange(len(glo) * n_bins, dtype=np.int32).reshape(len(glo), n_bins)
-            self.parts.append(self._part(1, glo, codes, freqs, np.zeros(len(glo)), gf))
-
-    def _part(self, system, ids, codes, freqs, gcode, gf):
-        dev = self.device
-        ctx = AcqCtx(self.fs, self.N, device=dev, max_freqs=len(freqs), max_blocks=self.n_ms,
-                     max_codes=len(codes))
-        ctx.set_codes(codes)
-        G = len(ids)
-        return dict(system=system, ids=list(ids), ctx=ctx, n_freqs=len(freqs), freqs=freqs,
-                    gf=gf,
-                    d_if=DevBuf(2 * self.n_ms * self.N, dev),
-                    d_freqs=DevBuf.from_array(np.asarray(freqs, np.float64), dev),
-                    d_gcode=DevBuf.from_array(np.asarray(gcode, np.int32), dev),
-                    d_gfreq=DevBuf.from_array(np.ascontiguousarray(gf, np.int32), dev),
-                    d_rows=DevBuf(G * self.n_bins * ACQ_ROW.itemsize, dev),
-                    d_res=DevBuf(G * ACQ_RESULT.itemsize, dev))
+            st = len(codes)
+            codes.append(sample_code(st_code(), 0.511e6, fs, self.N))
+            for k in glo:
+                gcode.append(st)
+                grec.append(1 if self.two else 0)
+                freqs.append(if_glo + k * glo_step + rel)
+        G = len(self.ids)
+        self.freqs = np.concatenate(freqs)
+        gf = np.arange(G * n_bins, dtype=np.int32).reshape(G, n_bins)
+        dev = device
+        self.ctx = AcqCtx(fs, self.N, device=dev, max_freqs=len(self.freqs),
+                          max_blocks=n_ms * (2 if self.two else 1), max_codes=len(codes))
+        self.ctx.set_codes(np.stack(codes))
+        self.d_grec = DevBuf.from_array(np.asarray(grec, np.int32), dev)
+        if self.two:
+            self.ctx.set_records(2)
+            self.ctx.set_group_records(self.d_grec)
+        self.G = G
+        self.d_if = DevBuf(2 * n_ms * self.N * (2 if self.two else 1), dev)
+        self.d_freqs = DevBuf.from_array(self.freqs, dev)
+        self.d_gcode = DevBuf.from_array(np.asarray(gcode, np.int32), dev)
+        self.d_gfreq = DevBuf.from_array(gf, dev)
+        self.d_rows = DevBuf(G * n_bins * ACQ_ROW.itemsize, dev)
+        self.d_res = DevBuf(G * ACQ_RESULT.itemsize, dev)
 
     @property
     def cells(self) -> int:
@@ -87,34 +101,27 @@ class FullSky:
     def load(self, if_gps: np.ndarray, if_glo: np.ndarray):
         """Interleaved int8 I,Q records of at least n_ms ms (the GPS and GLONASS front ends)."""
         need = 2 * self.n_ms * self.N
-        for p in self.parts:
-            rec = if_gps if p["system"] == 0 else if_glo
-            p["d_if"].upload(np.ascontiguousarray(rec[:need], np.int8))
+        recs = []
+        if any(s_ == 0 for s_, _ in self.ids):
+            recs.append(np.ascontiguousarray(if_gps[:need], np.int8))
+        if any(s_ == 1 for s_, _ in self.ids):
+            recs.append(np.ascontiguousarray(if_glo[:need], np.int8))
+        self.d_if.upload(np.concatenate(recs))
 
     def run(self):
-        """Enqueue the search (asynchronous on each context's stream).  The two
-        parts (GPS and GLONASS) run on their own streams with no join: joining
-        them (both spectra first, then both correlation launches together) was
-        measured slower at world 4 and 8 -- 246 workgroups from two concurrent
-        launches do not all fit one round of the CUs."""
-        for p in self.parts:
-            G = len(p["ids"])
-            p["ctx"].spectra_dev(p["d_if"].ptr, self.n_ms, p["n_freqs"], p["d_freqs"].ptr)
-            p["ctx"].correlate_dev(self.n_ms, p["d_freqs"].ptr, G, self.n_bins,
-                                   p["d_gcode"].ptr, p["d_gfreq"].ptr, p["d_rows"].ptr,
-                                   p["d_res"].ptr, spc=self.spc, mode=ACQ_NONCOHERENT)
+        """Enqueue the search (asynchronous on the context's stream): the forward
+        spectra of both records, then one correlation launch for every group."""
+        self.ctx.spectra_dev(self.d_if.ptr, self.n_ms, len(self.freqs), self.d_freqs.ptr)
+        self.ctx.correlate_dev(self.n_ms, self.d_freqs.ptr, self.G, self.n_bins,
+                               self.d_gcode.ptr, self.d_gfreq.ptr, self.d_rows.ptr,
+                               self.d_res.ptr, spc=self.spc, mode=ACQ_NONCOHERENT)
 
     def sync(self):
-        for p in self.parts:
-            p["ctx"].sync()
+        self.ctx.sync()
 
     def results(self) -> list[tuple]:
         """[(group_index, system, prn_or_fch, ACQ_RESULT record)] for this rank's groups."""
         self.sync()
-        out = []
-        for p in self.parts:
-            res = p["d_res"].download(ACQ_RESULT, len(p["ids"]))
-            for j, gid in enumerate(p["ids"]):
-                gi = GROUPS.index((p["system"], gid))
-                out.append((gi, p["system"], gid, res[j]))
+        res = self.d_res.download(ACQ_RESULT, self.G)
+        out = [(GROUPS.index(sid), sid[0], sid[1], res[j]) for j, sid in enumerate(self.ids)]
         return sorted(out, key=lambda r: r[0])

@@ -357,6 +357,13 @@ int gnsscorr_acq_set_coherent(gnsscorr_acq_ctx *ctx, int coh_ms);
  * Default 1.  (acquisition.sci:46-192 per record; no reference counterpart
  * for the batching itself.) */
 int gnsscorr_acq_set_records(gnsscorr_acq_ctx *ctx, int n_records);
+/* Per-group records: with d_group_rec (device, one int32 per group, values in
+ * [0, records)) a correlate call searches group g on record d_group_rec[g] only,
+ * instead of every group on every record; results are per group.  Lets one launch
+ * hold groups of different IF streams (the GPS and GLONASS records of a full-sky
+ * search).  NULL turns it off.  fp64 compiled plans only; the array must stay
+ * valid while correlate calls use it.  (No reference counterpart: batching.) */
+int gnsscorr_acq_set_group_records(gnsscorr_acq_ctx *ctx, const int32_t *d_group_rec);
 /* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples doubles. */
 int gnsscorr_acq_power_row(gnsscorr_acq_ctx *ctx, const int8_t *h_if, int iq, int n_blocks,
                            int block, double freq, int code, double *h_power);

@@ -70,6 +70,35 @@ def test_fullsky_sharding_is_exact(gpu, scene):
     one = merge([_run(gpu, scene, 1, 0)])
     two = merge([_run(gpu, scene, 2, 0), _run(gpu, scene, 2, 1)])
     three = merge([_run(gpu, scene, 3, r) for r in range(3)])
-    for a, b, c in zip(one, two, three):
-        assert a[:3] == b[:3] == c[:3]
-        assert a[3].tobytes() == b[3].tobytes() == c[3].tobytes(), a[:3]
+    eight = merge([_run(gpu, scene, 8, r) for r in range(8)])
+    for a, b, c, d in zip(one, two, three, eight):
+        assert a[:3] == b[:3] == c[:3] == d[:3]
+        assert a[3].tobytes() == b[3].tobytes() == c[3].tobytes() == d[3].tobytes(), a[:3]
+
+
+def test_group_records_equal_separate_searches(gpu):
+    """gnsscorr_acq_set_group_records: groups of two IF records in one launch give
+    the same bytes as each record searched alone (two PRNs on record 0, one on 1)."""
+    fs, n = FS, N
+    s0 = [dict(system=0, prn=3, code_phase=210.0, doppler=1200.0, cn0=45.0)]
+    s1 = [dict(system=0, prn=17, code_phase=640.5, doppler=-2600.0, cn0=45.0)]
+    r0 = gpu.ifgen(4 * n, s0, fs=fs, seed=0x5EED0051)
+    r1 = gpu.ifgen(4 * n, s1, fs=fs, seed=0x5EED0052)
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in (3, 9, 17)])
+    freqs = 2.42e6 + 500.0 * np.arange(-8, 9)
+    nb = len(freqs)
+    gf = np.tile(np.arange(nb, dtype=np.int32), (3, 1))
+    for mode in (gpu.ACQ_BEST_OF_BLOCKS, gpu.ACQ_NONCOHERENT):
+        both = gpu.AcqCtx(fs, n, max_freqs=nb, max_blocks=8, max_codes=3)
+        both.set_codes(codes)
+        both.set_records(2)
+        d_rec = gpu.DevBuf.from_array(np.array([0, 0, 1], np.int32))
+        both.set_group_records(d_rec)
+        res, rows = both.search(np.concatenate([r0, r1]), 4, freqs, [0, 1, 2], gf, mode=mode)
+        for g, rec in ((0, r0), (1, r0), (2, r1)):
+            one = gpu.AcqCtx(fs, n, max_freqs=nb, max_blocks=4, max_codes=3)
+            one.set_codes(codes)
+            ra, wa = one.search(rec, 4, freqs, [g], gf[:1], mode=mode)
+            assert res[g].tobytes() == ra[0].tobytes(), (mode, g)
+            assert rows[g].tobytes() == wa[0].tobytes(), (mode, g)
+    assert res[0]["metric"] > 2.5 and res[2]["metric"] > 2.5
