@@ -1475,6 +1475,11 @@ def main():
                 "value": N_PRN * N_BINS * gen["n"] * gen["steps"] * W / gen["dt"],
                 "unit": "cells/s", "dtype": "f64",
                 "ms_per_search": gen["dt"] / gen["steps"] * 1e3,
+                # the passes stream rows through L2 / MALL: rocprof HBM bytes of one whole
+                # search (every per-search kernel, PMC pass of this section) over its time
+                "roofline": {"bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+                             "traffic_per_search": pmc_run_bytes("acq_generic"),
+                             **hbm_fields(pmc_run_bytes("acq_generic"), gen["dt"] / gen["steps"])},
                 "config": f"fs = {gen['fs'] / 1e6:.3f} Msps (N = {gen['n']}): 32 PRN x 41 bins x "
                           "2 blocks, every length-N DFT as mixed-radix Stockham passes "
                           "(16, 7, 11, 31) in global memory, product and |.|^2 fused",
@@ -1642,7 +1647,9 @@ def main():
                 "roofline": {"bound": "valu", "kernel": "acq64 (whole search)",
                              "achieved": fl / (gsc["dt"] / gsc["steps"]) / 1e12,
                              "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
-                             "frac": fl / (gsc["dt"] / gsc["steps"]) / 1e12 / PEAK_FP64_TFLOPS},
+                             "frac": fl / (gsc["dt"] / gsc["steps"]) / 1e12 / PEAK_FP64_TFLOPS,
+                             "traffic_per_search": pmc_run_bytes("gps_scilab"),
+                             **hbm_fields(pmc_run_bytes("gps_scilab"), gsc["dt"] / gsc["steps"])},
             }
         if gco:
             cells = 14 * gco["nb"] * N

@@ -42,14 +42,14 @@ run_prof() {
 run_pmc() {
   echo "== pmc (per section; HBM bytes into a copy of profiles/pmc_traffic.json)"
   cp profiles/pmc_traffic.json $O/pmc_traffic.json
-  for S in ${PMC_SECTIONS:-acq track fullsky glo_coherent sgt sdr}; do
+  for S in ${PMC_SECTIONS:-acq track fullsky glo_coherent gps_scilab acq_generic sgt sdr}; do
     mkdir -p $O/pmc_$S
     for C in FETCH_SIZE WRITE_SIZE; do
       BENCH_FULLSKY_PROJECTION=0 timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
         python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1
     done
     R=""
-    case $S in acq|fullsky|glo_coherent) R="--runs 13";; esac
+    case $S in acq|fullsky|glo_coherent|gps_scilab|acq_generic) R="--runs 13";; esac
     python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S $R > /dev/null
     echo "pmc section $S ok"
   done
