@@ -271,7 +271,7 @@ def run_track(dist, dev, steps, warmup):
     cmd1["prn"] = rng.integers(1, 33, C)
     cmd1["stream"] = np.repeat(np.arange(TRACK_RX), TRACK_CH)
     cmd1["carrier_incr"] = 635008600 + rng.integers(-262000, 262000, C) * 20   # +-5 kHz
-    cmd1["code_incr"] = 6710886 * 40 + rng.integers(-10, 10, C)
+    cmd1["code_incr"] = 6710886 * 40 + rng.integers(-800, 800, C)   # +-3 ppm code Doppler
     cmd1["epoch_load"] = -1
     cmds = np.tile(cmd1, K)
     d_cmds = gc.DevBuf.from_array(cmds, dev)
@@ -346,7 +346,7 @@ def _track_cmds(rng, C, streams):
     cmd1["prn"] = rng.integers(1, 33, C)
     cmd1["stream"] = streams
     cmd1["carrier_incr"] = 635008600 + rng.integers(-262000, 262000, C) * 20   # +-5 kHz
-    cmd1["code_incr"] = 6710886 * 40 + rng.integers(-10, 10, C)
+    cmd1["code_incr"] = 6710886 * 40 + rng.integers(-800, 800, C)   # +-3 ppm code Doppler
     cmd1["epoch_load"] = -1
     return cmd1
 

@@ -1127,6 +1127,13 @@ constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 #ifndef TRACK_PF
 #define TRACK_PF 1                // LO words and row bytes read ahead (pair2r, interval_end_s)
 #endif
+#ifndef TRACK_NODUMP_COPY
+#define TRACK_NODUMP_COPY 1       // pieces without a dump run a copy without the dump test
+#endif
+#ifndef TRACK_IV4
+#define TRACK_IV4 1               // 4-pair intervals when a half-chip lasts >= 8 samples
+#endif
+constexpr uint32_t kIv4Kinc2 = 0x20000000u;   // 8 kinc2 <= 2^32
 
 // Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
 // writes (plain stores and atomics) are visible to every lane's later LDS reads
@@ -1182,7 +1189,7 @@ struct StreamArgs {
 // interval end (see interval_end): flush the part before the carry, carry the
 // rest, step the half-chip; a dump adds the epoch's sums to the LDS and
 // starts the next epoch
-template <bool PF>
+template <bool PF, bool DUMPS = true>
 __device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, int& e,
                                                int32_t* s_sum, const uint8_t* __restrict__ row) {
   seg_flush(g.pi, g.pq, g.lb, g.pb, g.eb, acc);
@@ -1193,14 +1200,16 @@ __device__ __forceinline__ void interval_end_s(const Chan& c, Seg& g, Acc& acc, 
   g.hc += cy ? 1u : 0u;
   if constexpr (!PF) g.ld = cy ? g.hc : g.ld;
   g.carried = false;
-  const bool dump = cy && g.hc >= c.D;   // correlator.c:251-281
-  uint64_t any = __builtin_amdgcn_ballot_w64(dump);
-  asm volatile("" : "+s"(any));          // a uniform branch: the flush stays off the common path
-  if (any) {
-    if (dump) {
-      flush_epoch(acc, e, s_sum);
-      e++;
-      g.hc = 0;        // the bits of half-chip 0 come from the pre-reset index ld
+  if constexpr (DUMPS) {   // (!DUMPS: the caller showed that no lane dumps in this piece)
+    const bool dump = cy && g.hc >= c.D;   // correlator.c:251-281
+    uint64_t any = __builtin_amdgcn_ballot_w64(dump);
+    asm volatile("" : "+s"(any));          // a uniform branch: the flush stays off the common path
+    if (any) {
+      if (dump) {
+        flush_epoch(acc, e, s_sum);
+        e++;
+        g.hc = 0;        // the bits of half-chip 0 come from the pre-reset index ld
+      }
     }
   }
   if constexpr (PF) {
@@ -1537,7 +1546,19 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
         }
         g.ti = g.tq = g.pi = g.pq = 0;
         g.carried = false;
-        if (__all(L == kPieceLen)) {
+        // whether any lane's 32 samples hold a dump: its half-chip count at the
+        // window start plus the window's code carries reaches D (one dump per
+        // ~16 k samples, so 7 of 8 pieces have none and skip the dump test at
+        // every interval end)
+        const uint64_t Xe = (uint64_t)c.K0 + (uint64_t)(n0 + L) * c.kinc2;
+        const bool dump_here = g.hc + (uint32_t)((Xe >> 32) - r0) >= c.D;
+        // intervals of kIv pairs: 3 (6 samples) whenever a half-chip lasts >= 6
+        // samples; 4 (8 samples, 4 interval ends per piece instead of 6) when it
+        // lasts >= 8, i.e. 8 kinc2 <= 2^32 (at 16.368 Msps: code rates up to the
+        // nominal 2.046 MHz of half-chips), still at most one carry per interval
+        auto full_piece = [&](auto dumps_tag, auto iv_tag) {
+          constexpr bool kD = decltype(dumps_tag)::value;
+          constexpr int kIv = decltype(iv_tag)::value;
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             const uint32_t words[4] = {ch4[j].x, ch4[j].y, ch4[j].z, ch4[j].w};
@@ -1546,8 +1567,21 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
               const int q = 4 * j + i;
               if constexpr (kPF) pair2r<false>(words[i], lwx[q], lwy[q], c, g);
               else pair2s<false>(words[i], c, g, lox, loy);
-              if (q % 3 == 2 || q == kPieceLen / 2 - 1) interval_end_s<kPF>(c, g, acc, e, s_sum, row);
+              if (q % kIv == kIv - 1 || q == kPieceLen / 2 - 1)
+                interval_end_s<kPF, kD>(c, g, acc, e, s_sum, row);
             }
+          }
+        };
+        if (__all(L == kPieceLen)) {
+          uint64_t anyd = __builtin_amdgcn_ballot_w64(dump_here);
+          asm volatile("" : "+s"(anyd));
+          using I3 = std::integral_constant<int, 3>;
+          using I4 = std::integral_constant<int, 4>;
+          if (TRACK_NODUMP_COPY && !anyd) {
+            if (TRACK_IV4 && kPF && c.kinc2 <= kIv4Kinc2) full_piece(std::false_type{}, I4{});
+            else full_piece(std::false_type{}, I3{});
+          } else {
+            full_piece(std::true_type{}, I3{});
           }
         } else {
           const int np = L >> 1;
