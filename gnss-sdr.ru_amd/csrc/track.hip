@@ -1578,7 +1578,7 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
           using I3 = std::integral_constant<int, 3>;
           using I4 = std::integral_constant<int, 4>;
           if (TRACK_NODUMP_COPY && !anyd) {
-            if (TRACK_IV4 && kPF && c.kinc2 <= kIv4Kinc2) full_piece(std::false_type{}, I4{});
+            if (TRACK_IV4 && c.kinc2 <= kIv4Kinc2) full_piece(std::false_type{}, I4{});
             else full_piece(std::false_type{}, I3{});
           } else {
             full_piece(std::true_type{}, I3{});
