@@ -1133,6 +1133,9 @@ constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 #ifndef TRACK_IV4
 #define TRACK_IV4 1               // 4-pair intervals when a half-chip lasts >= 8 samples
 #endif
+#ifndef TRACK_ALIGNED
+#define TRACK_ALIGNED 1           // pieces whose code carries repeat every 8 samples: fixed masks
+#endif
 constexpr uint32_t kIv4Kinc2 = 0x20000000u;   // 8 kinc2 <= 2^32
 
 // Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
@@ -1572,12 +1575,81 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
             }
           }
         };
+        // a piece in which every lane's code carries fall at one offset j in each
+        // of its four 8-sample intervals (chunk t = samples 8t .. 8t + 7, carry
+        // between samples 8t + j - 1 and 8t + j): the part of a pair before the
+        // carry has a mask fixed for the piece, so a pair is one AND and four dot4
+        // (no NCO step or carry test per pair), and every interval ends on a carry
+        auto aligned_piece = [&](const uint32_t (&mq)[4]) {
+#pragma unroll
+          for (int t = 0; t < 4; t++) {
+            const uint32_t words[4] = {ch4[t].x, ch4[t].y, ch4[t].z, ch4[t].w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              uint32_t lo_x, lo_y;
+              if constexpr (kPF) {
+                lo_x = lwx[4 * t + i];
+                lo_y = lwy[4 * t + i];
+              } else {
+                const uint32_t p1 = g.p0 + c.cinc;
+                const uint32_t idx = (g.p0 >> 29) | ((p1 >> 26) & 0x38u);
+                lo_x = lox[idx];
+                lo_y = loy[idx];
+                g.p0 = p1 + c.cinc;
+              }
+              const uint32_t xm = words[i] & mq[i];
+              g.ti = dot4(words[i], lo_x, g.ti);
+              g.tq = dot4(words[i], lo_y, g.tq);
+              g.pi = dot4(xm, lo_x, g.pi);
+              g.pq = dot4(xm, lo_y, g.pq);
+            }
+            seg_flush(g.pi, g.pq, g.lb, g.pb, g.eb, acc);
+            const int ri = g.ti - g.pi, rq = g.tq - g.pq;
+            g.ti = g.pi = ri;
+            g.tq = g.pq = rq;
+            g.hc += 1u;   // no dump in the piece (the caller's ballot)
+            if constexpr (kPF) {
+              g.cb = g.nb;
+              unpack8(g.cb, g.lb, g.pb, g.eb);
+              g.nb = row[g.hc + 1];
+            } else {
+              g.ld = g.hc;
+              unpack8(row[g.ld], g.lb, g.pb, g.eb);
+            }
+          }
+        };
         if (__all(L == kPieceLen)) {
           uint64_t anyd = __builtin_amdgcn_ballot_w64(dump_here);
           asm volatile("" : "+s"(anyd));
           using I3 = std::integral_constant<int, 3>;
           using I4 = std::integral_constant<int, 4>;
-          if (TRACK_NODUMP_COPY && !anyd) {
+          bool aligned = false;
+          if (TRACK_ALIGNED && TRACK_NODUMP_COPY && !anyd) {
+            // j: samples before the lane's first carry (sample n has half-chip
+            // hc + h(n), h(n) = (kph + n kinc2) >> 32), estimated in fp32 and
+            // checked exactly.  h(j - 1) = 0, h(j) = 1, h(j + 23) = 3, h(j + 24) = 4
+            // put the carries at j, j + 8, j + 16, j + 24: three spacings summing to
+            // 24 from {floor P, ceil P} (P samples per half-chip) are all 8, and the
+            // next carry (>= j + 31) is past the piece
+            const float r = (4294967296.0f - (float)g.kph) * __builtin_amdgcn_rcpf((float)c.kinc2);
+            const int j = min(8, max(1, (int)__builtin_ceilf(r)));
+            auto h = [&](int n) {
+              return (uint32_t)(((uint64_t)g.kph + (uint64_t)(uint32_t)n * c.kinc2) >> 32);
+            };
+            const bool ok = h(j - 1) == 0u && h(j) == 1u && h(j + 23) == 3u && h(j + 24) == 4u;
+            uint64_t bad = __builtin_amdgcn_ballot_w64(!ok);
+            asm volatile("" : "+s"(bad));
+            if (!bad) {
+              uint32_t mq[4];
+#pragma unroll
+              for (int i = 0; i < 4; i++)
+                mq[i] = j >= 2 * i + 2 ? 0xFFFFFFFFu : (j == 2 * i + 1 ? 0xFFFFu : 0u);
+              aligned_piece(mq);
+              aligned = true;
+            }
+          }
+          if (aligned) {
+          } else if (TRACK_NODUMP_COPY && !anyd) {
             if (TRACK_IV4 && c.kinc2 <= kIv4Kinc2) full_piece(std::false_type{}, I4{});
             else full_piece(std::false_type{}, I3{});
           } else {

@@ -78,7 +78,7 @@ def _random_cmds(rng, n_calls, C, n_streams, slew=False):
     return cmds
 
 
-@pytest.mark.parametrize("nsamp", [16368, 8380, 5000])
+@pytest.mark.parametrize("nsamp", [16368, 8380, 5000, 8381, 2043])
 def test_batched_many_channels_vs_oracle(gpu, oracle, nsamp):
     rng = np.random.default_rng(7 + nsamp)
     C, n_streams, n_calls = 96, 3, 4
