@@ -64,9 +64,28 @@ constexpr int kMaxWaves = 16;
 #ifndef SGT_KSUB
 #define SGT_KSUB 16
 #endif
+// wave mode: chip-aligned chunks (run_chips) instead of the prefix columns,
+// which then stay out of the wave kernel's LDS
+#ifndef SGT_CHIPS
+#define SGT_CHIPS 1
+#endif
+#ifndef SGT_CHIP_GROUP
+#define SGT_CHIP_GROUP 4
+#endif
+#ifndef SGT_CHIP_FMA
+#define SGT_CHIP_FMA 1
+#endif
+#ifndef SGT_CHIP_PF
+#define SGT_CHIP_PF 1     // the next chunk's IF words loaded during this chunk
+#endif
+#ifndef SGT_CHIP_PARK
+#define SGT_CHIP_PARK 0   // the channel state parked in LDS during the chunk loop
+#endif
 constexpr int kSub = SGT_KSUB;
 constexpr int kPfWaveBytes = kSub * 64 * 16;
-__host__ __device__ constexpr bool sgt_prefix(int maxt) { return SGT_PREFIX && maxt <= 256; }
+__host__ __device__ constexpr bool sgt_prefix(int maxt) {
+  return SGT_PREFIX && maxt <= 256 && !(SGT_CHIPS && maxt == 64);
+}
 __host__ __device__ constexpr size_t sgt_tab_bytes(int code_length) {
   return ((size_t)(code_length + 3) * sizeof(double) + 15) & ~(size_t)15;   // s_sgn + guard
 }
@@ -211,7 +230,8 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
   // so a 511-chip GLONASS table takes 4.1 KB, not the 1023-chip maximum
   extern __shared__ double s_sgn[];
   __shared__ double s_part[2][kMaxWaves][6];
-  __shared__ double2 s_w[32];   // chunked path: exp(i*A*n/fs), n < kC
+  __shared__ double2 s_w[40];   // chunked paths: exp(i*A*n/fs), n < kC
+  __shared__ gnsscorr_sgt_chan s_park;
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
   constexpr bool WAVE = MAXT == 64;
   constexpr bool kPrefix = sgt_prefix(MAXT);
@@ -536,9 +556,277 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
       ie = accI[0]; ip = accI[1]; il = accI[2];
       qe = accQ[0]; qp = accQ[1]; ql = accQ[2];
     };
+    // ---- chip-aligned chunks (wave mode, round 5).  Lane chunk q holds the
+    // samples of ONE prompt chip j = jF + q, k in [kS(j), kS(j+1)), kS(j) the
+    // first sample whose prompt index ceil(remCode + k*step) reaches j.  Within
+    // it the prompt code is constant, the early arm (remCode - spc) is still on
+    // chip j-1 for its first bE samples and the late arm (remCode + spc) already
+    // on chip j+1 from sample bL on; bE, bL take one of two values each (floor
+    // of spc/step or one more), so with T the chunk's sum of W_n * raw,
+    // H = T after bE samples and G = T after bL samples (captured in two short
+    // windows of the sample loop):
+    //   U_P = c(j) T,  U_E = c(j) T + (c(j-1) - c(j)) H,
+    //   U_L = c(j) T + (c(j+1) - c(j)) (T - G)                 (tracking.sci:316-326)
+    // No per-sample code selects and no prefix columns in LDS (the wave kernel's
+    // LDS is the code table and the W_n table).  The chunk's IF bytes start
+    // anywhere: kNW dwords are loaded and realigned by v_alignbyte.  The carrier
+    // at a chunk's first sample comes from the lane's previous chunk (64 chips
+    // earlier: kS moves by m or m + 1 samples) times a uniform rotation.
+    // Lanes whose chunk falls outside the windows (exact crossings moved by
+    // rounding) take an exact per-sample loop for that chunk.
+    auto run_chips = [&](auto kc_tag) {
+      constexpr int kC = decltype(kc_tag)::value;   // 17 or 33: longest chunk
+      constexpr int kHW = 5, kTW = 9;               // capture windows: n < kHW, n >= kC - kTW
+      constexpr int kNR = (kC * kBps + 3) / 4;      // realigned dwords holding kC samples
+      constexpr int kNW = kNR + 1;                  // loaded dwords (any byte alignment)
+      const double inv_step = uni(1.0 / step), stp = uni(step);
+      const double aPu = uni(aP), aEu = uni(aE), aLu = uni(aL);
+      const int jF = (int)ceil(aPu);                                     // k = 0's prompt chip
+      const int nC = (int)ceil(aPu + (double)(blk - 1) * stp) - jF + 1;  // chips of the epoch
+      const int nIt = (nC + 63) >> 6;
+      const int m64 = (int)floor(64.0 * inv_step);                       // samples per 64 chips
+      {
+        double sw, cw;
+        sincos(A * ((double)tid / p.fs), &sw, &cw);
+        if (tid < kC) s_w[tid] = make_double2(cw, sw);
+      }
+      double sR, cR;   // exp(i A m64 / fs)
+      sincos(A * ((double)m64 / p.fs), &sR, &cR);
+      sR = uni(sR);
+      cR = uni(cR);
+      __syncthreads();
+      // first k with ceil(a + k*step) >= t: exact when the real-valued estimate
+      // has a 1e-6-sample margin from an integer; else one of est - 1, est, est + 1
+      auto first_k = [&](double a, int t, bool& risky) -> int {
+        const double d = ((double)(t - 1) - a) * inv_step;
+        const double fd = floor(d);
+        const double fr = d - fd;
+        risky |= !(fr > 1e-6 && fr < 1.0 - 1e-6);
+        return (int)fd + 1;
+      };
+      auto exact_k = [&](double a, int t, int est) -> int {
+        if ((int)ceil(a + (double)(est - 1) * stp) >= t) return est - 1;
+        if ((int)ceil(a + (double)est * stp) >= t) return est;
+        return est + 1;
+      };
+      struct Bd { int kS, kN, kE, kL; };
+      auto bounds = [&](int j) {
+        bool risky = false;
+        Bd b;
+        b.kS = first_k(aPu, j, risky);
+        b.kN = first_k(aPu, j + 1, risky);
+        b.kE = first_k(aEu, j, risky);
+        b.kL = first_k(aLu, j + 1, risky);
+        if (risky) {
+          b.kS = exact_k(aPu, j, b.kS);
+          b.kN = exact_k(aPu, j + 1, b.kN);
+          b.kE = exact_k(aEu, j, b.kE);
+          b.kL = exact_k(aLu, j + 1, b.kL);
+        }
+        return b;
+      };
+      typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+      auto fetch = [&](const Bd& b, uint32_t (&w)[kNW]) {
+        const uintptr_t a0 = (uintptr_t)(src + (int64_t)kBps * b.kS);
+        const uint32_t* p4 = reinterpret_cast<const uint32_t*>(a0 & ~(uintptr_t)3);
+        // a wave whose lanes all read inside the epoch loads without guards
+        const bool inside = b.kS >= 0 && b.kS + (4 * kNW + kBps - 1) / kBps <= blk;
+        if (__builtin_amdgcn_ballot_w64(!inside) == 0) {
+#pragma unroll
+          for (int u = 0; u + 4 <= kNW; u += 4) {
+            const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(p4 + u);
+            w[u] = v.x; w[u + 1] = v.y; w[u + 2] = v.z; w[u + 3] = v.w;
+          }
+#pragma unroll
+          for (int u = kNW & ~3; u < kNW; u++) w[u] = p4[u];
+        } else {
+          // only dwords holding a byte of the epoch [src, src + kBps blk)
+          const uintptr_t lo = (uintptr_t)src, hi = lo + (uintptr_t)((int64_t)kBps * blk);
+#pragma unroll
+          for (int u = 0; u < kNW; u++) {
+            const uintptr_t a = (uintptr_t)(p4 + u);
+            w[u] = (a + 4 > lo && a < hi) ? p4[u] : 0u;
+          }
+        }
+      };
+      double accI[3] = {0.0, 0.0, 0.0}, accQ[3] = {0.0, 0.0, 0.0};
+      const uint32_t* sg = reinterpret_cast<const uint32_t*>(s_sgn) + 1;   // hi words
+      auto code = [&](int i) {   // the code as +-1.0 (only the high word differs)
+        return __longlong_as_double((long long)sg[2 * clampu(i, L + 1)] << 32);
+      };
+      Bd b = bounds(jF + tid);
+      double sb, cb;   // carrier at the chunk's first sample
+      sincos(A * ((double)b.kS / p.fs) + c.rem_carr, &sb, &cb);
+      uint32_t nx[kNW];
+      if (SGT_CHIP_PF) fetch(b, nx);
+      for (int it = 0; it < nIt; it++) {
+        uint32_t w[kNW];
+        if (!SGT_CHIP_PF) fetch(b, nx);
+#pragma unroll
+        for (int u = 0; u < kNW; u++) w[u] = nx[u];
+        const int j = jF + it * 64 + tid;
+        Bd bn = b;
+        if (it + 1 < nIt) {
+          bn = bounds(j + 64);
+          if (SGT_CHIP_PF) fetch(bn, nx);
+        }
+        const int len = b.kN - b.kS, bE = b.kE - b.kS, bL = b.kL - b.kS;
+        const bool ok = len <= kC && len >= kC - 3 && bE >= 0 && bE <= kHW && bL - 1 >= kC - kTW &&
+                        bL <= len;
+        // the chunk's samples from byte a0 & 3 on, realigned to dword 0
+        const uint32_t sh = (uint32_t)((uintptr_t)(src + (int64_t)kBps * b.kS) & 3);
+        uint32_t r[kNR];
+#pragma unroll
+        for (int u = 0; u < kNR; u++) r[u] = __builtin_amdgcn_alignbyte(w[u + 1], w[u], sh);
+        // samples outside [0, blk) count as 0 (the epoch's first and last chunks)
+        const bool edge = b.kS < 0 || b.kS + kC > blk;
+        const bool any_edge = __builtin_amdgcn_ballot_w64(edge) != 0;
+        double Tr = 0.0, Ti = 0.0, Hr = 0.0, Hi = 0.0, Gr = 0.0, Gi = 0.0;
+        auto sample_loop = [&](auto edge_tag) {
+          constexpr bool kEdge = decltype(edge_tag)::value;
+          int wo = 0;   // opaque: the W_n reads stay inside the loop
+          asm volatile("" : "+v"(wo));
+#pragma unroll
+          for (int n = 0; n < kC; n++) {
+            if (n % SGT_CHIP_GROUP == 0 && n > 0) {
+              // groups of samples: the next group's W_n reads and IF words depend
+              // on the running sum so far, so the compiler cannot hoist every
+              // sample's table entry and conversion to the chunk's start
+              asm volatile("" : "+v"(wo) : "v"(Tr));
+#pragma unroll
+              for (int u = n * kBps / 4; u < kNR && u < (n + SGT_CHIP_GROUP) * kBps / 4 + 1; u++)
+                asm volatile("" : "+v"(r[u]) : "v"(Ti));
+            }
+            int re, im = 0;
+            if constexpr (FT == 2) {
+              re = (int)__builtin_amdgcn_sbfe(r[n >> 1], (n & 1) * 16 + sh_re, 8);
+              im = (int)__builtin_amdgcn_sbfe(r[n >> 1], (n & 1) * 16 + sh_im, 8);
+            } else {
+              re = (int)__builtin_amdgcn_sbfe(r[n >> 2], (n & 3) * 8, 8);
+            }
+            bool v = true;
+            if (n >= kC - 3) v = n < len;
+            if (kEdge) v = v && (unsigned)(b.kS + n) < (unsigned)blk;
+            if (kEdge || n >= kC - 3) {
+              re = v ? re : 0;
+              im = v ? im : 0;
+            }
+            const double2 W = s_w[n + wo];   // broadcast read
+            if constexpr (SGT_CHIP_FMA) {
+              // T += W_n * raw as fused steps (fp64 rounding only)
+              Tr = fma(W.x, (double)re, Tr);
+              Ti = fma(W.y, (double)re, Ti);
+              if constexpr (FT == 2) {
+                Tr = fma(-W.y, (double)im, Tr);
+                Ti = fma(W.x, (double)im, Ti);
+              }
+            } else {
+              double ur, ui;
+              if constexpr (FT == 2) {
+                ur = fma(W.x, (double)re, -(W.y * (double)im));   // W_n * raw
+                ui = fma(W.x, (double)im, W.y * (double)re);
+              } else {
+                ur = W.x * (double)re;
+                ui = W.y * (double)re;
+              }
+              Tr += ur;
+              Ti += ui;
+            }
+            if (n < kHW) {
+              const bool h = n == bE - 1;
+              Hr = h ? Tr : Hr;
+              Hi = h ? Ti : Hi;
+            }
+            if (n >= kC - kTW) {
+              const bool g = n == bL - 1;
+              Gr = g ? Tr : Gr;
+              Gi = g ? Ti : Gi;
+            }
+          }
+        };
+        if (any_edge) sample_loop(std::true_type{});
+        else sample_loop(std::false_type{});
+        if (ok) {
+          const double cP = code(j), dE = code(j - 1) - cP, dL = code(j + 1) - cP;   // dE, dL: 0, +-2
+          const double PTr = cP * Tr, PTi = cP * Ti;
+          const double Ur[3] = {fma(dE, Hr, PTr), PTr, fma(dL, Tr - Gr, PTr)};
+          const double Ui[3] = {fma(dE, Hi, PTi), PTi, fma(dL, Ti - Gi, PTi)};
+#pragma unroll
+          for (int x = 0; x < 3; x++) {
+            accQ[x] = fma(cb, Ur[x], fma(-sb, Ui[x], accQ[x]));
+            accI[x] = fma(sb, Ur[x], fma(cb, Ui[x], accI[x]));
+          }
+        } else {
+          // exact per-sample loop for this lane's chunk (rare)
+#pragma unroll 1
+          for (int k = max(b.kS, 0); k < min(b.kN, blk); k++) {
+            const double t = (double)k * stp;
+            const double gx[3] = {s_sgn[clampu((int)ceil(aEu + t), L + 1)],
+                                  s_sgn[clampu((int)ceil(aPu + t), L + 1)],
+                                  s_sgn[clampu((int)ceil(aLu + t), L + 1)]};
+            double re, im = 0.0;
+            if constexpr (FT == 2) {
+              const int wv = *reinterpret_cast<const uint16_t*>(src + 2 * (int64_t)k);
+              re = (double)(int)__builtin_amdgcn_sbfe(wv, sh_re, 8);
+              im = (double)(int)__builtin_amdgcn_sbfe(wv, sh_im, 8);
+            } else {
+              re = (double)src[k];
+            }
+            double se, ce;
+            sincos(A * ((double)k / p.fs) + c.rem_carr, &se, &ce);
+            const double qb = fma(ce, re, -(se * im)), ib = fma(ce, im, se * re);
+#pragma unroll
+            for (int x = 0; x < 3; x++) {
+              accQ[x] = fma(qb, gx[x], accQ[x]);
+              accI[x] = fma(ib, gx[x], accI[x]);
+            }
+          }
+        }
+        if (it + 1 < nIt) {
+          // carrier at the next chunk: kS moves by m64 or m64 + 1 samples
+          const int D = bn.kS - b.kS;
+          if (D == m64 || D == m64 + 1) {
+            double rc = cR, rs = sR;
+            if (D != m64) {
+              const double2 W1 = s_w[1];
+              rc = fma(cR, W1.x, -(sR * W1.y));
+              rs = fma(sR, W1.x, cR * W1.y);
+            }
+            const double cn = fma(cb, rc, -(sb * rs));
+            sb = fma(sb, rc, cb * rs);
+            cb = cn;
+          } else {
+            sincos(A * ((double)bn.kS / p.fs) + c.rem_carr, &sb, &cb);
+          }
+          b = bn;
+        }
+      }
+      ie = accI[0]; ip = accI[1]; il = accI[2];
+      qe = accQ[0]; qp = accQ[1]; ql = accQ[2];
+    };
     const bool chunked = p.chunked && in_table && 15.0 * step < 0.999 &&
                          ((uintptr_t)src & (kBps - 1)) == 0;
-    if (chunked && SGT_KC32 && 31.0 * step < 0.999)
+    const double invs = 1.0 / step, sps = floor(p.spc * invs);   // samples per chip, spc in samples
+    const bool chips33 = SGT_CHIPS && WAVE && chunked && sps <= 3.0 && invs >= 30.0 && invs < 33.0;
+    const bool chips17 = SGT_CHIPS && WAVE && chunked && sps <= 3.0 && invs >= 14.0 && invs < 17.0;
+    if (chips33 || chips17) {
+      // (SGT_CHIP_PARK: the channel state waits in LDS, so its 32 registers are
+      // free during the chunk loop)
+      if (SGT_CHIP_PARK && WAVE) {
+        if (tid == 0) s_park = c;
+        __syncthreads();
+      }
+      if (chips33) run_chips(std::integral_constant<int, 33>{});
+      else run_chips(std::integral_constant<int, 17>{});
+      if (SGT_CHIP_PARK && WAVE) {
+        __syncthreads();
+        const volatile uint32_t* pv = reinterpret_cast<const volatile uint32_t*>(&s_park);
+        uint32_t* pc = reinterpret_cast<uint32_t*>(&c);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof c / 4); i++) pc[i] = pv[i];
+      }
+    }
+    else if (chunked && SGT_KC32 && 31.0 * step < 0.999)
       run_chunks(std::integral_constant<int, 32>{});
     else if (chunked)
       run_chunks(std::integral_constant<int, 16>{});
