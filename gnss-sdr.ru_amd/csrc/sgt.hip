@@ -575,7 +575,7 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
     // Lanes whose chunk falls outside the windows (exact crossings moved by
     // rounding) take an exact per-sample loop for that chunk.
     auto run_chips = [&](auto kc_tag) {
-      constexpr int kC = decltype(kc_tag)::value;   // 17 or 33: longest chunk
+      constexpr int kC = decltype(kc_tag)::value;   // 16, 17, 32 or 33: longest chunk
       constexpr int kHW = 5, kTW = 9;               // capture windows: n < kHW, n >= kC - kTW
       constexpr int kNR = (kC * kBps + 3) / 4;      // realigned dwords holding kC samples
       constexpr int kNW = kNR + 1;                  // loaded dwords (any byte alignment)
@@ -807,17 +807,21 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
     const bool chunked = p.chunked && in_table && 15.0 * step < 0.999 &&
                          ((uintptr_t)src & (kBps - 1)) == 0;
     const double invs = 1.0 / step, sps = floor(p.spc * invs);   // samples per chip, spc in samples
-    const bool chips33 = SGT_CHIPS && WAVE && chunked && sps <= 3.0 && invs >= 30.0 && invs < 33.0;
-    const bool chips17 = SGT_CHIPS && WAVE && chunked && sps <= 3.0 && invs >= 14.0 && invs < 17.0;
-    if (chips33 || chips17) {
+    // the longest chunk is floor(samples per chip) + 1 samples: kC = 16 / 17 (GPS
+    // at 16 / 16.368 Msps), 32 / 33 (GLONASS); the loop masks its last 3 samples
+    const int ipc = (SGT_CHIPS && WAVE && chunked && sps <= 3.0 && invs < 33.0) ? (int)invs : 0;
+    const int kcs = ipc >= 29 ? (ipc >= 32 ? 33 : 32) : (ipc >= 13 && ipc <= 16 ? (ipc >= 16 ? 17 : 16) : 0);
+    if (kcs) {
       // (SGT_CHIP_PARK: the channel state waits in LDS, so its 32 registers are
       // free during the chunk loop)
       if (SGT_CHIP_PARK && WAVE) {
         if (tid == 0) s_park = c;
         __syncthreads();
       }
-      if (chips33) run_chips(std::integral_constant<int, 33>{});
-      else run_chips(std::integral_constant<int, 17>{});
+      if (kcs == 33) run_chips(std::integral_constant<int, 33>{});
+      else if (kcs == 32) run_chips(std::integral_constant<int, 32>{});
+      else if (kcs == 17) run_chips(std::integral_constant<int, 17>{});
+      else run_chips(std::integral_constant<int, 16>{});
       if (SGT_CHIP_PARK && WAVE) {
         __syncthreads();
         const volatile uint32_t* pv = reinterpret_cast<const volatile uint32_t*>(&s_park);
