@@ -1136,6 +1136,9 @@ constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 #ifndef TRACK_ALIGNED
 #define TRACK_ALIGNED 1           // pieces whose code carries repeat every 8 samples: fixed masks
 #endif
+#ifndef TRACK_X2LUT
+#define TRACK_X2LUT 1             // packed bytes expanded through a 256-word LDS table
+#endif
 constexpr uint32_t kIv4Kinc2 = 0x20000000u;   // 8 kinc2 <= 2^32
 
 // Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
@@ -1339,6 +1342,13 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
   // address is the byte index 4 (a | b << 3) itself (kPF); without the read-ahead
   // each wave keeps its own copy beside its sums (s_lo)
   __shared__ uint32_t s_lot[128];
+  // packed: byte b -> its four int8 levels (one LDS read instead of the spread
+  // and v_perm of if2_expand_byte per output word)
+  constexpr bool kX2 = PK && TRACK_X2LUT;
+  __shared__ uint32_t s_x2[kX2 ? 256 : 1];
+  if constexpr (kX2) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_x2[i] = if2_expand_byte((uint32_t)i);
+  }
   if (kPF && threadIdx.x < 64) {
     const int a = lane & 7, b = lane >> 3;
     const uint32_t ia = (uint32_t)__builtin_amdgcn_sbfe((int)kLutI, 4 * a, 4) & 0xFFu;
@@ -1348,7 +1358,7 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
     s_lot[lane] = ia | qa << 8 | ib << 16 | qb << 24;
     s_lot[64 + lane] = qa | ((0u - ia) & 0xFFu) << 8 | qb << 16 | ((0u - ib) & 0xFFu) << 24;
   }
-  if (kPF) __syncthreads();   // the only workgroup barrier: before any wave leaves
+  if (kPF || kX2) __syncthreads();   // the only workgroup barrier: before any wave leaves
   uint8_t* wb = reinterpret_cast<uint8_t*>(s_dyn) + wave * stream_wave_lds(PK, nsamp);
   uint4* slot = reinterpret_cast<uint4*>(wb);                      // int8 only
   uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes);
@@ -1493,10 +1503,21 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       // ---- this lane's 32 samples as 16 pair words (4 chunks of 4)
       uint4 ch4[4];
       if constexpr (PK) {
-        ch4[0] = if2_expand_word(pq0.x);
-        ch4[1] = if2_expand_word(pq0.y);
-        ch4[2] = if2_expand_word(pq1.x);
-        ch4[3] = if2_expand_word(pq1.y);
+        if constexpr (kX2) {
+          auto x2 = [&](uint32_t w) {
+            return make_uint4(s_x2[w & 0xFFu], s_x2[(w >> 8) & 0xFFu], s_x2[(w >> 16) & 0xFFu],
+                              s_x2[w >> 24]);
+          };
+          ch4[0] = x2(pq0.x);
+          ch4[1] = x2(pq0.y);
+          ch4[2] = x2(pq1.x);
+          ch4[3] = x2(pq1.y);
+        } else {
+          ch4[0] = if2_expand_word(pq0.x);
+          ch4[1] = if2_expand_word(pq0.y);
+          ch4[2] = if2_expand_word(pq1.x);
+          ch4[3] = if2_expand_word(pq1.y);
+        }
       } else {
         if (p * kPieceSpan + kPieceSpan > nsamp && (nsamp & 7)) {
           // the call's partial last chunk (nsamp not a multiple of 8; single
@@ -1935,7 +1956,8 @@ static int launch_stream(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stri
   if (n_calls > 1 && ((nsamp * 2) & (pk ? 31 : 15))) return GNSSCORR_TRACK_NOT_FUSED;
   const int C = c->cfg.n_channels;
   size_t dyn = (size_t)stream_wave_lds(pk, (int)nsamp) * kStreamCh;
-  if (dyn + 1024 > c->lds_max) return GNSSCORR_TRACK_NOT_FUSED;
+  constexpr size_t kStatic = 2048;   // s_lot, s_x2 (packed), with margin
+  if (dyn + kStatic > c->lds_max) return GNSSCORR_TRACK_NOT_FUSED;
   // A launch takes as long as its busiest CU.  The dispatcher fills a CU with
   // as many workgroups as its resources allow, so at 768 workgroups on 256 CUs
   // some CUs got 4-5 while others got 2 (wave stamps: pieces p10 16.6 / p90
@@ -1948,7 +1970,7 @@ static int launch_stream(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stri
   // streams' kernels out of those CUs' LDS (co-residency).
   if (c->balance && n_wg > c->n_cu) {
     const size_t cap = c->lds_max / (size_t)(per_cu + 1) + 16;   // per_cu + 1 no longer fit
-    if (cap > dyn && cap * per_cu + 1024 * per_cu <= c->lds_max) dyn = cap;
+    if (cap > dyn && (cap + kStatic) * per_cu <= c->lds_max) dyn = cap;
   }
   StreamArgs A;
   memset(&A, 0, sizeof A);
