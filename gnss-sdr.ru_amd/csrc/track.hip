@@ -1412,13 +1412,21 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       const int valid = min(kPieceSpan, nsamp - n_piece);
       const int full_chunks = valid / 8;
       const int8_t* g8 = A.ifbuf + e_call + 2 * (int64_t)n_piece;
+      if (full_chunks == kPieceSpan / 8) {   // a whole piece: no per-lane guards
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int i = r * 64 + lane;
-        if (i < full_chunks)
+        for (int r = 0; r < 4; r++)
           __builtin_amdgcn_global_load_lds(
-              (const void*)(g8 + 16 * i),
+              (const void*)(g8 + 16 * (r * 64 + lane)),
               (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int i = r * 64 + lane;
+          if (i < full_chunks)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(g8 + 16 * i),
+                (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
+        }
       }
     }
     inflight = k * n_pieces + p;

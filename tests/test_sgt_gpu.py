@@ -123,16 +123,21 @@ def test_open_loop_low_rate_unclamped_path(gpu, system, fs):
         assert _close(got, sums).all(), (i, got, sums)
 
 
+@pytest.mark.parametrize("threads", [None, "64"])
 @pytest.mark.parametrize("chunk", ["1", "0"])
 @pytest.mark.parametrize("system,file_type", [(1, 2), (0, 2), (1, 1)])
-def test_open_loop_crossings_on_exact_chips(gpu, system, file_type, chunk, monkeypatch):
+def test_open_loop_crossings_on_exact_chips(gpu, system, file_type, chunk, threads, monkeypatch):
     """codeFreq = fs/32 (GPS: fs/16) and remCode on the 1/32 grid: every code index
     crossing ceil(remCode -/+ spc + k*step) lands exactly on an integer chip.  There
-    the chunked path's real-valued crossing estimate has no margin, so the exact
-    per-sample scan decides (sgt.hip run_chunks); GNSSCORR_SGT_CHUNK=0 runs the
-    per-sample index path on the same inputs.  Indices and state bit-exact."""
+    the chunked paths' real-valued crossing estimates have no margin, so the exact
+    reference expression decides (sgt.hip run_chunks; in wave mode, threads "64",
+    run_chips' exact chunk boundaries and its per-sample loop for chunks outside the
+    capture windows); GNSSCORR_SGT_CHUNK=0 runs the per-sample index path on the same
+    inputs.  Indices and state bit-exact."""
     gc = gpu
     monkeypatch.setenv("GNSSCORR_SGT_CHUNK", chunk)
+    if threads:
+        monkeypatch.setenv("GNSSCORR_SGT_THREADS", threads)
     rng = np.random.default_rng(5 + system + 2 * file_type)
     n = 120000
     IF = gc.ifgen(n, [], fs=FS, iq=file_type == 2, seed=33)
