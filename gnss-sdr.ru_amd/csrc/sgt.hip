@@ -556,8 +556,8 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
       ie = accI[0]; ip = accI[1]; il = accI[2];
       qe = accQ[0]; qp = accQ[1]; ql = accQ[2];
     };
-    // ---- chip-aligned chunks (wave mode, round 5).  Lane chunk q holds the
-    // samples of ONE prompt chip j = jF + q, k in [kS(j), kS(j+1)), kS(j) the
+    // ---- chip-aligned chunks (round 5; every launch shape).  Thread chunk q holds
+    // the samples of ONE prompt chip j = jF + q, k in [kS(j), kS(j+1)), kS(j) the
     // first sample whose prompt index ceil(remCode + k*step) reaches j.  Within
     // it the prompt code is constant, the early arm (remCode - spc) is still on
     // chip j-1 for its first bE samples and the late arm (remCode + spc) already
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
     // No per-sample code selects and no prefix columns in LDS (the wave kernel's
     // LDS is the code table and the W_n table).  The chunk's IF bytes start
     // anywhere: kNW dwords are loaded and realigned by v_alignbyte.  The carrier
-    // at a chunk's first sample comes from the lane's previous chunk (64 chips
+    // at a chunk's first sample comes from the thread's previous chunk (T chips
     // earlier: kS moves by m or m + 1 samples) times a uniform rotation.
     // Lanes whose chunk falls outside the windows (exact crossings moved by
     // rounding) take an exact per-sample loop for that chunk.
@@ -583,14 +583,14 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
       const double aPu = uni(aP), aEu = uni(aE), aLu = uni(aL);
       const int jF = (int)ceil(aPu);                                     // k = 0's prompt chip
       const int nC = (int)ceil(aPu + (double)(blk - 1) * stp) - jF + 1;  // chips of the epoch
-      const int nIt = (nC + 63) >> 6;
-      const int m64 = (int)floor(64.0 * inv_step);                       // samples per 64 chips
+      const int nIt = (nC + T - 1) / T;
+      const int m64 = (int)floor((double)T * inv_step);                  // samples per T chips
       {
         double sw, cw;
         sincos(A * ((double)tid / p.fs), &sw, &cw);
         if (tid < kC) s_w[tid] = make_double2(cw, sw);
       }
-      double sR, cR;   // exp(i A m64 / fs)
+      double sR, cR;   // exp(i A m64 / fs): the carrier T chips on
       sincos(A * ((double)m64 / p.fs), &sR, &cR);
       sR = uni(sR);
       cR = uni(cR);
@@ -664,10 +664,10 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
         if (!SGT_CHIP_PF) fetch(b, nx);
 #pragma unroll
         for (int u = 0; u < kNW; u++) w[u] = nx[u];
-        const int j = jF + it * 64 + tid;
+        const int j = jF + it * T + tid;
         Bd bn = b;
         if (it + 1 < nIt) {
-          bn = bounds(j + 64);
+          bn = bounds(j + T);
           if (SGT_CHIP_PF) fetch(bn, nx);
         }
         const int len = b.kN - b.kS, bE = b.kE - b.kS, bL = b.kL - b.kS;
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
           }
         }
         if (it + 1 < nIt) {
-          // carrier at the next chunk: kS moves by m64 or m64 + 1 samples
+          // carrier at the next chunk (T chips on): kS moves by m64 or m64 + 1 samples
           const int D = bn.kS - b.kS;
           if (D == m64 || D == m64 + 1) {
             double rc = cR, rs = sR;
@@ -809,7 +809,7 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
     const double invs = 1.0 / step, sps = floor(p.spc * invs);   // samples per chip, spc in samples
     // the longest chunk is floor(samples per chip) + 1 samples: kC = 16 / 17 (GPS
     // at 16 / 16.368 Msps), 32 / 33 (GLONASS); the loop masks its last 3 samples
-    const int ipc = (SGT_CHIPS && WAVE && chunked && sps <= 3.0 && invs < 33.0) ? (int)invs : 0;
+    const int ipc = (SGT_CHIPS && MAXT <= 256 && chunked && sps <= 3.0 && invs < 33.0) ? (int)invs : 0;
     const int kcs = ipc >= 29 ? (ipc >= 32 ? 33 : 32) : (ipc >= 13 && ipc <= 16 ? (ipc >= 16 ? 17 : 16) : 0);
     if (kcs) {
       // (SGT_CHIP_PARK: the channel state waits in LDS, so its 32 registers are
