@@ -1139,6 +1139,12 @@ constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 #ifndef TRACK_X2LUT
 #define TRACK_X2LUT 1             // packed bytes expanded through a 256-word LDS table
 #endif
+#ifndef TRACK_SLOTS
+#define TRACK_SLOTS 1             // int8 pieces in flight per wave (LDS-DMA slots)
+#endif
+#ifndef TRACK_DMA_AUX
+#define TRACK_DMA_AUX 0           // cache policy of the piece LDS-DMA (2: nt, streaming)
+#endif
 constexpr uint32_t kIv4Kinc2 = 0x20000000u;   // 8 kinc2 <= 2^32
 
 // Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
@@ -1167,7 +1173,7 @@ __host__ __device__ constexpr int stream_sum_bytes(int nsamp) {
   return (((nsamp / GNSSCORR_OSG_ROW + 2) * 24 + 15) & ~15);
 }
 __host__ __device__ constexpr int stream_wave_lds(bool pk, int nsamp) {
-  return (pk ? 0 : kStage2Bytes) + kPk8Stage + stream_sum_bytes(nsamp) + 512;
+  return (pk ? 0 : kStage2Bytes * TRACK_SLOTS) + kPk8Stage + stream_sum_bytes(nsamp) + 512;
 }
 
 // Arguments of one osg_stream_kernel launch: n_calls consecutive calls of
@@ -1360,8 +1366,9 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
   }
   if (kPF || kX2) __syncthreads();   // the only workgroup barrier: before any wave leaves
   uint8_t* wb = reinterpret_cast<uint8_t*>(s_dyn) + wave * stream_wave_lds(PK, nsamp);
-  uint4* slot = reinterpret_cast<uint4*>(wb);                      // int8 only
-  uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes);
+  constexpr int kSlots = PK ? 1 : TRACK_SLOTS;
+  uint4* slot0 = reinterpret_cast<uint4*>(wb);                     // int8 only: kSlots slots
+  uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes * kSlots);
   int32_t* s_sum = reinterpret_cast<int32_t*>(s_row + kPk8Stage);
   uint2* s_lo = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(s_sum) + stream_sum_bytes(nsamp));
   STREAM_PSTAMP(0);
@@ -1389,9 +1396,12 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
   const int n_pieces = (nsamp + kPieceSpan - 1) / kPieceSpan;
   int row_base = -1, row_n32 = 0;   // the E/P/L row words staged in s_row (uniform)
 
-  // ---- the piece in flight: LDS-DMA into the wave's slot (int8), or the lane's
-  // 16 bytes in registers (packed).  inflight = k * n_pieces + p, -1 none.
-  int inflight = -1;
+  // ---- the pieces in flight: LDS-DMA into the wave's slots (int8: piece number
+  // n goes to slot n % kSlots), or the lane's 16 bytes in registers (packed,
+  // one piece).  iss / con: pieces issued / consumed; (q_k, q_p): the last issued.
+  int iss = 0, con = 0, q_k = -1, q_p = -1;
+  bool last_full4 = false;   // the last issued int8 piece took all four DMA instructions
+  auto slot_of = [&](int n) { return slot0 + (n % kSlots) * (kStage2Bytes / 16); };
   uint2 pq0 = make_uint2(0u, 0u), pq1 = make_uint2(0u, 0u);
   auto issue = [&](int k, int p, int64_t e_call) {   // e_call: element offset of call k's stream
     const int n_piece = p * kPieceSpan;
@@ -1412,12 +1422,14 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       const int valid = min(kPieceSpan, nsamp - n_piece);
       const int full_chunks = valid / 8;
       const int8_t* g8 = A.ifbuf + e_call + 2 * (int64_t)n_piece;
+      uint4* slot = slot_of(iss);
+      last_full4 = full_chunks > 192;
       if (full_chunks == kPieceSpan / 8) {   // a whole piece: no per-lane guards
 #pragma unroll
         for (int r = 0; r < 4; r++)
           __builtin_amdgcn_global_load_lds(
               (const void*)(g8 + 16 * (r * 64 + lane)),
-              (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
+              (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, TRACK_DMA_AUX);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -1425,11 +1437,13 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
           if (i < full_chunks)
             __builtin_amdgcn_global_load_lds(
                 (const void*)(g8 + 16 * i),
-                (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
+                (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, TRACK_DMA_AUX);
         }
       }
     }
-    inflight = k * n_pieces + p;
+    iss = __builtin_amdgcn_readfirstlane(iss + 1);   // (uniform: scalar registers)
+    q_k = __builtin_amdgcn_readfirstlane(k);
+    q_p = __builtin_amdgcn_readfirstlane(p);
   };
 
   for (int k = 0; k < A.n_calls; k++) {
@@ -1453,7 +1467,7 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
     wave_lds_sync();   // ... and every lane's flushes add to zeroed sums
     const uint32_t pk_hi = max(max(c.D, c.hc0), (c.hc0 + 1u) & 0xFFFFu);
     const bool pk_lds = active && c.j1 != kNever && pk_hi < 3072u;
-    if (active && inflight != k * n_pieces) issue(k, 0, e_call);
+    if (active && q_k != k) issue(k, 0, e_call);
     if (pk_lds) {
       // the staged row serves later calls of the same PRN (replay, closed loop)
       // as far as it reaches
@@ -1482,6 +1496,20 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
           e_next = (int64_t)nc.stream * A.stream_stride * 2 + (int64_t)(k + 1) * A.call_elems;
       }
     }
+    // keep kSlots pieces in flight: the rest of this call, then the next call's
+    auto top_up = [&]() {
+      while (iss - con < kSlots) {
+        int nk = q_k, np = q_p + 1;
+        if (np >= n_pieces) {
+          nk++;
+          np = 0;
+        }
+        if (nk == k) issue(k, np, e_call);
+        else if (nk == k + 1 && e_next >= 0) issue(k + 1, np, e_next);
+        else break;
+      }
+    };
+    if (active) top_up();
 
     Acc acc;
 #pragma unroll
@@ -1510,6 +1538,7 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       }
       // ---- this lane's 32 samples as 16 pair words (4 chunks of 4)
       uint4 ch4[4];
+      const int cslot = con;   // this piece's slot (int8)
       if constexpr (PK) {
         if constexpr (kX2) {
           auto x2 = [&](uint32_t w) {
@@ -1540,17 +1569,45 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
             uint32_t t[4] = {0u, 0u, 0u, 0u};
             for (int q = 0; q < rem / 2; q++) t[q] = g32[q];
             if (rem & 1) t[rem / 2] = (uint32_t)reinterpret_cast<const uint16_t*>(g32)[rem - 1];
-            slot[i] = make_uint4(t[0], t[1], t[2], t[3]);
+            slot_of(cslot)[i] = make_uint4(t[0], t[1], t[2], t[3]);
           }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (kSlots > 1 && iss - con >= 2 && last_full4) {
+          // the four DMA instructions of the next piece are the youngest vector
+          // memory operations that may still be outstanding
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // this piece has landed
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the piece has landed in the slot
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the piece has landed in the slot
         if (p == 0) STREAM_PSTAMP(2);
+        if constexpr (kSlots > 1) {
+          // the slot read as inline asm: the compiler, which cannot tell the
+          // slots apart, would otherwise wait for every LDS-DMA in flight
+          // (vmcnt(0)) before it; the counted wait above is the dependency
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(
+              slot_of(cslot) + 4 * lane);
+          u32x4 v0, v1, v2, v3;
+          asm volatile(
+              "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
+              "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48\n\t"
+              "s_waitcnt lgkmcnt(0)"
+              : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
+              : "v"(la)
+              : "memory");
+          ch4[0] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+          ch4[1] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+          ch4[2] = make_uint4(v2.x, v2.y, v2.z, v2.w);
+          ch4[3] = make_uint4(v3.x, v3.y, v3.z, v3.w);
+        } else {
+          const uint4* slot = slot_of(cslot);
 #pragma unroll
-        for (int j = 0; j < 4; j++) ch4[j] = slot[4 * lane + j];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers
+          for (int j = 0; j < 4; j++) ch4[j] = slot[4 * lane + j];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers
+        }
       }
-      if (p + 1 < n_pieces) issue(k, p + 1, e_call);
-      else if (e_next >= 0) issue(k + 1, 0, e_next);
+      con = __builtin_amdgcn_readfirstlane(con + 1);
+      top_up();   // the slot just read takes the piece kSlots ahead
       if (L == 0) continue;
       const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
       const uint64_t r0 = X >> 32;
@@ -1736,10 +1793,11 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       }
     }
     if (e >= 0) flush_epoch(acc, e, s_sum);
-    if (!active && inflight >= 0 && !PK) {
+    if (!active && iss != con) {
       // a prefetch for a call that turned out idle must land before the slot is reused
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      inflight = -1;
+      con = iss;
+      q_k = q_p = -1;
     }
     wave_lds_sync();   // every lane's flushes land before lane 0 reads the sums
     STREAM_PSTAMP(3);
