@@ -78,9 +78,6 @@ constexpr int kMaxWaves = 16;
 #ifndef SGT_CHIP_PF
 #define SGT_CHIP_PF 1     // the next chunk's IF words loaded during this chunk
 #endif
-#ifndef SGT_CHIP_PARK
-#define SGT_CHIP_PARK 0   // the channel state parked in LDS during the chunk loop
-#endif
 constexpr int kSub = SGT_KSUB;
 constexpr int kPfWaveBytes = kSub * 64 * 16;
 __host__ __device__ constexpr bool sgt_prefix(int maxt) {
@@ -231,7 +228,6 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
   extern __shared__ double s_sgn[];
   __shared__ double s_part[2][kMaxWaves][6];
   __shared__ double2 s_w[40];   // chunked paths: exp(i*A*n/fs), n < kC
-  __shared__ gnsscorr_sgt_chan s_park;
   const int ch = xcd_channel(blockIdx.x, gridDim.x);
   constexpr bool WAVE = MAXT == 64;
   constexpr bool kPrefix = sgt_prefix(MAXT);
@@ -812,23 +808,10 @@ __global__ __launch_bounds__(MAXT, MAXT == 64 ? (sgt_prefix(64) ? 2 : SGT_WPE) :
     const int ipc = (SGT_CHIPS && MAXT <= 256 && chunked && sps <= 3.0 && invs < 33.0) ? (int)invs : 0;
     const int kcs = ipc >= 29 ? (ipc >= 32 ? 33 : 32) : (ipc >= 13 && ipc <= 16 ? (ipc >= 16 ? 17 : 16) : 0);
     if (kcs) {
-      // (SGT_CHIP_PARK: the channel state waits in LDS, so its 32 registers are
-      // free during the chunk loop)
-      if (SGT_CHIP_PARK && WAVE) {
-        if (tid == 0) s_park = c;
-        __syncthreads();
-      }
       if (kcs == 33) run_chips(std::integral_constant<int, 33>{});
       else if (kcs == 32) run_chips(std::integral_constant<int, 32>{});
       else if (kcs == 17) run_chips(std::integral_constant<int, 17>{});
       else run_chips(std::integral_constant<int, 16>{});
-      if (SGT_CHIP_PARK && WAVE) {
-        __syncthreads();
-        const volatile uint32_t* pv = reinterpret_cast<const volatile uint32_t*>(&s_park);
-        uint32_t* pc = reinterpret_cast<uint32_t*>(&c);
-#pragma unroll
-        for (int i = 0; i < (int)(sizeof c / 4); i++) pc[i] = pv[i];
-      }
     }
     else if (chunked && SGT_KC32 && 31.0 * step < 0.999)
       run_chunks(std::integral_constant<int, 32>{});
