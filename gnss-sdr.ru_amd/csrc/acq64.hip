@@ -1854,12 +1854,203 @@ int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, in
   return GNSSCORR_OK;
 }
 
+// ---------------------------------------------------------------------------------
+// Four-step plan (round 5): N = N1 N2 with N1 = A B and N2 = C D, each a pair of
+// compiled radices.  X[k1 + N1 k2] = sum_n2 W_N2^(n2 k2) W_N^(n2 k1) sum_n1
+// W_N1^(n1 k1) x[N2 n1 + n2].  m4_cols runs the N1-point DFTs of a tile of kM4T2
+// columns n2 in LDS (A-point DFTs, twiddle W_N1^(q u), B-point DFTs: the standard
+// two-factor split), multiplies by W_N^(n2 k1) and writes Y[k1 N2 + n2]; m4_rows
+// runs the N2-point DFTs of kM4T1 rows k1 the same way and writes X[k1 + N1 k2].
+// Two passes over the rows instead of the four of the mixed-radix plan at
+// N = 38 192 = 112 x 341; the correlation product is formed in the first, |.|^2 /
+// N^2 in the second (acquisition.sci:107-132), as in mx_pass.
+// ---------------------------------------------------------------------------------
+#ifndef M4_CT
+#define M4_CT 128   // m4_cols threads
+#endif
+#ifndef M4_T2
+#define M4_T2 16    // m4_cols: columns n2 per workgroup
+#endif
+#ifndef M4_RT
+#define M4_RT 64    // m4_rows threads
+#endif
+#ifndef M4_T1
+#define M4_T1 4     // m4_rows: rows k1 per workgroup
+#endif
+constexpr int kM4ColThreads = M4_CT, kM4T2 = M4_T2, kM4RowThreads = M4_RT, kM4T1 = M4_T1;
+
+// MODE 0: rows in (stride in_rs); MODE 1: the correlation product of unit u0 + row
+template <int A, int B, int MODE>
+__global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__ in, int in_rs,
+                                                       v2d* __restrict__ out, int N,
+                                                       const v2d* __restrict__ tw, MixCorr cp) {
+  constexpr int N1 = A * B;
+  __shared__ v2d s[N1][kM4T2 + 1];
+  const int N2 = N / N1;
+  const int n2_0 = blockIdx.x * kM4T2;
+  const long row = blockIdx.y;
+  const v2d *Xr = nullptr, *Fr = nullptr;
+  int shift = 0;
+  if constexpr (MODE == 1) {
+    const int unit = cp.u0 + (int)row;
+    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
+    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
+    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
+    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
+    Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
+    Fr = cp.F + (long)cp.group_code[g] * cp.rs;
+    shift = fm.y;
+  }
+  for (int idx = threadIdx.x; idx < N1 * kM4T2; idx += kM4ColThreads) {
+    const int n1 = idx / kM4T2, t = idx % kM4T2, n2 = n2_0 + t;
+    v2d x = (v2d){0.0, 0.0};
+    if (n2 < N2) {
+      const int n = N2 * n1 + n2;
+      if constexpr (MODE == 1) {
+        int sx = n - shift;
+        sx += sx < 0 ? N : 0;
+        const v2d xv = Xr[sx], f = Fr[n];
+        x = (v2d){fma(xv.x, f.x, xv.y * f.y), fma(xv.x, f.y, -(xv.y * f.x))};   // conj(X) F
+      } else {
+        x = in[row * in_rs + n];
+      }
+    }
+    s[n1][t] = x;
+  }
+  __syncthreads();
+  // A-point DFTs over p of x[B p + q], times W_N1^(q u), back into the same slots
+  for (int task = threadIdx.x; task < B * kM4T2; task += kM4ColThreads) {
+    const int q = task / kM4T2, t = task % kM4T2;
+    v2d v[A];
+#pragma unroll
+    for (int p = 0; p < A; p++) v[p] = s[B * p + q][t];
+    dft<A>(v);
+#pragma unroll
+    for (int u = 1; u < A; u++) v[u] = cmul(v[u], tw[q * u * N2]);   // W_N1^(q u) = W_N^(q u N2)
+#pragma unroll
+    for (int u = 0; u < A; u++) s[B * u + q][t] = v[u];
+  }
+  __syncthreads();
+  // B-point DFTs over q: X[u + A v] into slot B u + v
+  for (int task = threadIdx.x; task < A * kM4T2; task += kM4ColThreads) {
+    const int u = task / kM4T2, t = task % kM4T2;
+    v2d v[B];
+#pragma unroll
+    for (int q = 0; q < B; q++) v[q] = s[B * u + q][t];
+    dft<B>(v);
+#pragma unroll
+    for (int w = 0; w < B; w++) s[B * u + w][t] = v[w];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < N1 * kM4T2; idx += kM4ColThreads) {
+    const int k1 = idx / kM4T2, t = idx % kM4T2, n2 = n2_0 + t;
+    if (n2 >= N2) continue;
+    const v2d x = s[B * (k1 % A) + k1 / A][t];
+    out[row * N + (long)k1 * N2 + n2] = cmul(x, tw[n2 * k1]);   // W_N^(n2 k1), n2 k1 < N
+  }
+}
+
+// MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added when acc)
+template <int C, int D, int MODE>
+__global__ __launch_bounds__(kM4RowThreads) void m4_rows(const v2d* __restrict__ Y,
+                                                       v2d* __restrict__ out, int out_rs, int N,
+                                                       const v2d* __restrict__ tw,
+                                                       double* __restrict__ pw, int acc) {
+  constexpr int N2 = C * D;
+  __shared__ v2d s[kM4T1][N2 + 1];
+  const int N1 = N / N2;
+  const int k1_0 = blockIdx.x * kM4T1;
+  const long row = blockIdx.y;
+  for (int idx = threadIdx.x; idx < kM4T1 * N2; idx += kM4RowThreads) {
+    const int r = idx / N2, n2 = idx % N2, k1 = k1_0 + r;
+    s[r][n2] = k1 < N1 ? Y[row * N + (long)k1 * N2 + n2] : (v2d){0.0, 0.0};
+  }
+  __syncthreads();
+  for (int task = threadIdx.x; task < D * kM4T1; task += kM4RowThreads) {
+    const int q = task / kM4T1, r = task % kM4T1;
+    v2d v[C];
+#pragma unroll
+    for (int p = 0; p < C; p++) v[p] = s[r][D * p + q];
+    dft<C>(v);
+#pragma unroll
+    for (int u = 1; u < C; u++) v[u] = cmul(v[u], tw[q * u * N1]);   // W_N2^(q u) = W_N^(q u N1)
+#pragma unroll
+    for (int u = 0; u < C; u++) s[r][D * u + q] = v[u];
+  }
+  __syncthreads();
+  for (int task = threadIdx.x; task < C * kM4T1; task += kM4RowThreads) {
+    const int u = task / kM4T1, r = task % kM4T1;
+    v2d v[D];
+#pragma unroll
+    for (int q = 0; q < D; q++) v[q] = s[r][D * u + q];
+    dft<D>(v);
+#pragma unroll
+    for (int w = 0; w < D; w++) s[r][D * u + w] = v[w];
+  }
+  __syncthreads();
+  const double sc = 1.0 / ((double)N * (double)N);
+  for (int idx = threadIdx.x; idx < kM4T1 * N2; idx += kM4RowThreads) {
+    const int k2 = idx / kM4T1, r = idx % kM4T1, k1 = k1_0 + r;
+    if (k1 >= N1) continue;
+    const v2d x = s[r][D * (k2 % C) + k2 / C];
+    const long d = (long)k1 + (long)N1 * k2;
+    if constexpr (MODE == 2) {
+      const double q = fma(x.x, x.x, x.y * x.y) * sc;
+      double* o = pw + row * N + d;
+      *o = acc ? *o + q : q;
+    } else {
+      out[row * out_rs + d] = x;
+    }
+  }
+}
+
+// the compiled four-step plans: {A, B, C, D}
+constexpr int kM4Plans[][4] = {{0, 0, 0, 0}, {7, 16, 11, 31}, {3, 16, 11, 31}};
+
+int m4_plan(int N) {
+  for (int i = 1; i < (int)(sizeof kM4Plans / sizeof kM4Plans[0]); i++)
+    if (N == kM4Plans[i][0] * kM4Plans[i][1] * kM4Plans[i][2] * kM4Plans[i][3]) return i;
+  return 0;
+}
+
+// rows [src] -> DFT rows or the correlation's power rows, one chunk of `rows`
+template <int MODE_IN, int MODE_OUT>
+int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_rs, int rows,
+              const MixCorr& cp, double* pw, int acc) {
+  const int N = c->cfg.n_samples;
+  const v2d* tw = (const v2d*)c->d_twN;
+  v2d* Y = (v2d*)c->d_gA;
+  switch (c->m4) {
+#define M4_CASE(I, A, B, C, D)                                                                 \
+  case I:                                                                                      \
+    hipLaunchKernelGGL((m4_cols<A, B, MODE_IN>), dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows), \
+                       dim3(kM4ColThreads), 0, c->stream, in, in_rs, Y, N, tw, cp);            \
+    hipLaunchKernelGGL((m4_rows<C, D, MODE_OUT>), dim3((A * B + kM4T1 - 1) / kM4T1, rows),     \
+                       dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tw, pw, acc);     \
+    break;
+    M4_CASE(1, 7, 16, 11, 31)
+    M4_CASE(2, 3, 16, 11, 31)
+#undef M4_CASE
+    default:
+      gnsscorr_set_error("acq64 four-step: no plan %d", c->m4);
+      return GNSSCORR_EINVAL;
+  }
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
 // DFT_N of `rows` natural rows a (stride src_rs) -> out (stride rs), chunked
 int mx_dft_rows(gnsscorr_acq_ctx* c, const v2d* a, int src_rs, int rows, v2d* out, int rs) {
   const int N = c->cfg.n_samples, P = c->mix_nr;
   const MixCorr none{};
   for (int r0 = 0; r0 < rows; r0 += c->g_chunk) {
     const int nr = rows - r0 < c->g_chunk ? rows - r0 : c->g_chunk;
+    if (c->m4) {
+      const int rc = m4_launch<0, 0>(c, a + (long)r0 * src_rs, src_rs, out + (long)r0 * rs, rs, nr,
+                                     none, nullptr, 0);
+      if (rc) return rc;
+      continue;
+    }
     v2d *A = (v2d*)c->d_gA, *B = (v2d*)c->d_gB;
     const v2d* src = a + (long)r0 * src_rs;
     int srs = src_rs, Ns = 1;
@@ -1887,6 +2078,11 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
     for (int b = 0; b < (nc ? n_blocks : 1); b++) {
       MixCorr cp{(const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1,
                  n_bins, u0, d_gcode, d_gfreq, (const int2*)c->d_fmap64};
+      if (c->m4) {
+        const int rc = m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0);
+        if (rc) return rc;
+        continue;
+      }
       v2d *A = (v2d*)c->d_gA, *B = (v2d*)c->d_gB;
       const v2d* src = nullptr;
       int Ns = 1;
@@ -1949,6 +2145,7 @@ int acq64_plan_for(int n_samples) {
 
 namespace {
 int mix_factor(int N, int* r);
+int m4_plan(int N);
 int mx_init(gnsscorr_acq_ctx* c);
 }  // namespace
 
@@ -1970,6 +2167,10 @@ int acq64_init(gnsscorr_acq_ctx* c) {
     // GNSSCORR_ACQ_BLUESTEIN=1: the chirp-z engine, for cross-checks)
     const char* fb = getenv("GNSSCORR_ACQ_BLUESTEIN");
     c->mix_nr = (fb && atoi(fb)) ? 0 : mix_factor(N, c->mix_r);
+    // the four-step plan where one is compiled for N (GNSSCORR_ACQ_MIX4=0: the
+    // mixed-radix passes, for cross-checks)
+    const char* f4 = getenv("GNSSCORR_ACQ_MIX4");
+    c->m4 = c->mix_nr && !(f4 && f4[0] == '0') ? m4_plan(N) : 0;
     return c->mix_nr ? mx_init(c) : g_init(c);
   }
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));

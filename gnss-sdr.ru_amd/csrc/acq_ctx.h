@@ -42,6 +42,9 @@ struct gnsscorr_acq_ctx {
   // mix_nr passes of radix mix_r[i] in global memory, twiddles d_twN (W_N^j)
   int mix_nr = 0;
   int mix_r[24] = {};
+  // four-step plan of the generic path (N = N1 N2, N1 = A B and N2 = C D two-radix
+  // sub-transforms in LDS, two passes over the rows): 0 none, else its plan index
+  int m4 = 0;
   // ---- shared
   int n_codes = 0;
   int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra

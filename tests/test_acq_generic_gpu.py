@@ -7,7 +7,9 @@ Held to the same bar as the compiled plans (tests/test_acq_gpu.py check_rows,
 fp64 class): powers, peaks, second peaks and metrics within 1e-6 relative of the
 fp64 oracle (oracle/acq_oracle.py; observed ~1e-13), code phase and bin exact.
 Two engines: the mixed-radix Stockham plan (N a product of radices <= 31:
-5000 = 8 x 5^4, 38192 = 16 x 7 x 11 x 31; the default) and Bluestein's chirp-z
+5000 = 8 x 5^4, 38192 = 16 x 7 x 11 x 31; the default; where a four-step plan is
+compiled, 38192 = 112 x 341 and 16368 = 48 x 341, its two LDS passes replace the
+four global ones, GNSSCORR_ACQ_MIX4=0 keeps the passes) and Bluestein's chirp-z
 (prime factors above 31, or GNSSCORR_ACQ_BLUESTEIN=1); both are held to the
 oracle and to each other.  The generic engine also runs at N = 16368
 (GNSSCORR_ACQ_GENERIC=1) against the compiled 16 x 33 x 31 plan.
@@ -154,4 +156,33 @@ def test_mixed_radix_equals_bluestein(gpu, fs, monkeypatch):
     rel = np.abs(w0["peak"] - w1["peak"]) / w0["peak"]
     rel2 = np.abs(w0["second"] - w1["second"]) / w0["second"]
     print(f"[mixed vs bluestein N={n}] peak {rel.max():.3e} second {rel2.max():.3e}")
+    assert rel.max() < 1e-9 and rel2.max() < 1e-9
+
+
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
+@pytest.mark.parametrize("fs,generic", [(38.192e6, "0"), (16.368e6, "1")])
+def test_four_step_equals_mixed_radix_passes(gpu, fs, generic, mode, monkeypatch):
+    """The four-step plan (m4_cols / m4_rows: 112 x 341 at 38.192 Msps, 48 x 341 at
+    16.368 Msps on the generic engine) against the four mixed-radix passes
+    (GNSSCORR_ACQ_MIX4=0) on one search: decisions identical, peaks and second
+    peaks within 1e-9 relative (both fp64 DFTs of the same rows)."""
+    monkeypatch.setenv("GNSSCORR_ACQ_GENERIC", generic)
+    n = int(round(fs / 1000.0))
+    IF = _scene(gpu, fs, 2, 0x5EED0026)
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in (6, 19, 25)])
+    freqs = 2.42e6 + 500.0 * np.arange(-6, 7)
+    gf = np.tile(np.arange(len(freqs)), (3, 1))
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    out = []
+    for m4 in ("1", "0"):
+        monkeypatch.setenv("GNSSCORR_ACQ_MIX4", m4)
+        ctx = gpu.AcqCtx(fs, n, max_freqs=16, max_blocks=2, max_codes=3)
+        ctx.set_codes(codes)
+        out.append(ctx.search(IF, 2, freqs, np.arange(3), gf, spc=int(round(fs / 1.023e6)), mode=m))
+    (r0, w0), (r1, w1) = out
+    assert (r0["code_phase"] == r1["code_phase"]).all() and (r0["bin"] == r1["bin"]).all()
+    assert (w0["argmax"] == w1["argmax"]).all() and (w0["block"] == w1["block"]).all()
+    rel = np.abs(w0["peak"] - w1["peak"]) / w0["peak"]
+    rel2 = np.abs(w0["second"] - w1["second"]) / w0["second"]
+    print(f"[four-step vs passes N={n} {mode}] peak {rel.max():.3e} second {rel2.max():.3e}")
     assert rel.max() < 1e-9 and rel2.max() < 1e-9
