@@ -1471,18 +1471,19 @@ def main():
         if gen:
             out["acquisition_generic"] = {
                 "metric": "acquisition cells/sec (config-2 search at a rate without a compiled "
-                          "plan: fp64 mixed-radix engine)",
+                          "plan: fp64 generic engine)",
                 "value": N_PRN * N_BINS * gen["n"] * gen["steps"] * W / gen["dt"],
                 "unit": "cells/s", "dtype": "f64",
                 "ms_per_search": gen["dt"] / gen["steps"] * 1e3,
-                # the passes stream rows through L2 / MALL: rocprof HBM bytes of one whole
-                # search (every per-search kernel, PMC pass of this section) over its time
+                # rocprof HBM bytes of one whole search (every per-search kernel, PMC pass of
+                # this section) over its time
                 "roofline": {"bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
                              "traffic_per_search": pmc_run_bytes("acq_generic"),
                              **hbm_fields(pmc_run_bytes("acq_generic"), gen["dt"] / gen["steps"])},
                 "config": f"fs = {gen['fs'] / 1e6:.3f} Msps (N = {gen['n']}): 32 PRN x 41 bins x "
-                          "2 blocks, every length-N DFT as mixed-radix Stockham passes "
-                          "(16, 7, 11, 31) in global memory, product and |.|^2 fused",
+                          "2 blocks, every length-N DFT as a four-step N1 x N2 = 112 x 341 "
+                          "plan (two LDS passes, product fused into the first, |.|^2 into "
+                          "the second)",
                 "planted_found": f"{gen['found']}/{gen['n_planted']}",
             }
         if trk:
