@@ -1482,8 +1482,8 @@ def main():
                              **hbm_fields(pmc_run_bytes("acq_generic"), gen["dt"] / gen["steps"])},
                 "config": f"fs = {gen['fs'] / 1e6:.3f} Msps (N = {gen['n']}): 32 PRN x 41 bins x "
                           "2 blocks, every length-N DFT as a four-step N1 x N2 = 112 x 341 "
-                          "plan (two LDS passes, product fused into the first, |.|^2 into "
-                          "the second)",
+                          "plan (two LDS passes, product fused into the first, |.|^2 and "
+                          "per-column top-2 row statistics into the second)",
                 "planted_found": f"{gen['found']}/{gen['n_planted']}",
             }
         if trk:

@@ -1950,12 +1950,32 @@ __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__
   }
 }
 
-// MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added when acc)
+// Per-column top-2 of a power row (MODE 3 of m4_rows): the column k1 holds the
+// samples k1 + N1 k2, N1 apart, so when 2 spc - 1 <= N1 the open window around the
+// row's argmax holds at most one of them and {a1, first index, runner-up} per column
+// give the second peak exactly (g_stats1_kernel's argument with columns for threads).
+struct M4Top {
+  double a1, a2;
+  int ak, pad;
+};
+// merge the top-2 of a disjoint set into (a1, ak, a2): ties keep the first index
+__device__ __forceinline__ void top2_merge(double& a1, int& ak, double& a2, double b1, int bk,
+                                           double b2) {
+  const bool take = better(b1, bk, a1, ak);
+  a2 = take ? fmax(a1, b2) : fmax(a2, b1);
+  ak = take ? bk : ak;
+  a1 = take ? b1 : a1;
+}
+
+// MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added when
+// acc); MODE 3: as 2 on a row's last block, per-column top-2 into top (pw written only
+// when store)
 template <int C, int D, int MODE>
 __global__ __launch_bounds__(kM4RowThreads) void m4_rows(const v2d* __restrict__ Y,
                                                        v2d* __restrict__ out, int out_rs, int N,
                                                        const v2d* __restrict__ tw,
-                                                       double* __restrict__ pw, int acc) {
+                                                       double* __restrict__ pw, int acc,
+                                                       M4Top* __restrict__ top, int store) {
   constexpr int N2 = C * D;
   __shared__ v2d s[kM4T1][N2 + 1];
   const int N1 = N / N2;
@@ -1989,18 +2009,69 @@ __global__ __launch_bounds__(kM4RowThreads) void m4_rows(const v2d* __restrict__
   }
   __syncthreads();
   const double sc = 1.0 / ((double)N * (double)N);
+  // MODE 3: a thread's elements all lie in column r = threadIdx.x % kM4T1, k2 ascending
+  static_assert(kM4RowThreads == 64 && 64 % kM4T1 == 0, "m4_rows: one wave, whole columns");
+  double a1 = -1.0, a2 = -1.0;
+  int ak = INT_MAX;
   for (int idx = threadIdx.x; idx < kM4T1 * N2; idx += kM4RowThreads) {
     const int k2 = idx / kM4T1, r = idx % kM4T1, k1 = k1_0 + r;
     if (k1 >= N1) continue;
     const v2d x = s[r][D * (k2 % C) + k2 / C];
     const long d = (long)k1 + (long)N1 * k2;
-    if constexpr (MODE == 2) {
+    if constexpr (MODE == 2 || MODE == 3) {
       const double q = fma(x.x, x.x, x.y * x.y) * sc;
       double* o = pw + row * N + d;
-      *o = acc ? *o + q : q;
+      const double v = acc ? *o + q : q;
+      if (MODE == 2 || store) *o = v;
+      if constexpr (MODE == 3) {
+        a2 = v > a1 ? a1 : fmax(a2, v);
+        ak = v > a1 ? (int)d : ak;   // strict: the first index of the thread's maximum
+        a1 = fmax(a1, v);
+      }
     } else {
       out[row * out_rs + d] = x;
     }
+  }
+  if constexpr (MODE == 3) {
+#pragma unroll
+    for (int o = kM4T1; o < 64; o <<= 1)
+      top2_merge(a1, ak, a2, __shfl_xor(a1, o, 64), __shfl_xor(ak, o, 64), __shfl_xor(a2, o, 64));
+    const int k1 = k1_0 + (int)threadIdx.x;
+    if (threadIdx.x < kM4T1 && k1 < N1) top[row * N1 + k1] = M4Top{a1, a2, ak, 0};
+  }
+}
+
+// Row statistics from the per-column top-2 (one wave per row): the argmax over the
+// columns, then the second peak as the maximum of each column's a1 when its argmax lies
+// outside the open circular window (argmax - spc, argmax + spc), else its runner-up.
+// Same results as g_stats1_kernel on the power rows.
+__global__ __launch_bounds__(64) void m4_stats_kernel(const M4Top* __restrict__ top, int N1,
+                                                      int N, int u0, int n_blocks, int nc,
+                                                      int spc,
+                                                      gnsscorr_acq_row* __restrict__ stats) {
+  const int unit = u0 + blockIdx.x;
+  const M4Top* t = top + (long)blockIdx.x * N1;
+  const int rowid = nc ? unit : unit / n_blocks;
+  const int blk0 = nc ? 0 : unit % n_blocks;
+  double bv = -1.0;
+  int bk = INT_MAX;
+  for (int c = threadIdx.x; c < N1; c += 64)
+    if (better(t[c].a1, t[c].ak, bv, bk)) { bv = t[c].a1; bk = t[c].ak; }
+  wave_argmax(bv, bk);
+  double sv = -1.0;
+  for (int c = threadIdx.x; c < N1; c += 64) {
+    int d = t[c].ak - bk;
+    d += d < 0 ? N : 0;
+    sv = fmax(sv, (d >= spc && d <= N - spc) ? t[c].a1 : t[c].a2);
+  }
+  sv = wave_max(sv);
+  if (threadIdx.x == 0) {
+    gnsscorr_acq_row r;
+    r.peak = bv;
+    r.second = sv;
+    r.argmax = bk;
+    r.block = nc ? -1 : blk0;
+    stats[(long)rowid * n_blocks + blk0] = r;
   }
 }
 
@@ -2016,7 +2087,7 @@ int m4_plan(int N) {
 // rows [src] -> DFT rows or the correlation's power rows, one chunk of `rows`
 template <int MODE_IN, int MODE_OUT>
 int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_rs, int rows,
-              const MixCorr& cp, double* pw, int acc) {
+              const MixCorr& cp, double* pw, int acc, int store = 1) {
   const int N = c->cfg.n_samples;
   const v2d* tw = (const v2d*)c->d_twN;
   v2d* Y = (v2d*)c->d_gA;
@@ -2026,7 +2097,8 @@ int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_r
     hipLaunchKernelGGL((m4_cols<A, B, MODE_IN>), dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows), \
                        dim3(kM4ColThreads), 0, c->stream, in, in_rs, Y, N, tw, cp);            \
     hipLaunchKernelGGL((m4_rows<C, D, MODE_OUT>), dim3((A * B + kM4T1 - 1) / kM4T1, rows),     \
-                       dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tw, pw, acc);     \
+                       dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tw, pw, acc,      \
+                       (M4Top*)c->d_m4top, store);                                              \
     break;
     M4_CASE(1, 7, 16, 11, 31)
     M4_CASE(2, 3, 16, 11, 31)
@@ -2073,13 +2145,21 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
   const int N = c->cfg.n_samples, P = c->mix_nr;
   const bool nc = mode == GNSSCORR_ACQ_NONCOHERENT;
   const int n_units = n_groups * n_bins * (nc ? 1 : n_blocks);
+  // four-step plans: the row statistics ride on the last block's m4_rows (per-column
+  // top-2; its power rows are then not stored) unless the window can hold two samples
+  // of a column or the power rows are dumped
+  const int N1 = c->m4 ? kM4Plans[c->m4][0] * kM4Plans[c->m4][1] : 0;
+  const bool fused = c->m4 && c->d_m4top && 2 * spc - 1 <= N1 && !d_dump;
   for (int u0 = 0; u0 < n_units; u0 += c->g_chunk) {
     const int nu = n_units - u0 < c->g_chunk ? n_units - u0 : c->g_chunk;
-    for (int b = 0; b < (nc ? n_blocks : 1); b++) {
+    const int nb = nc ? n_blocks : 1;
+    for (int b = 0; b < nb; b++) {
       MixCorr cp{(const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1,
                  n_bins, u0, d_gcode, d_gfreq, (const int2*)c->d_fmap64};
       if (c->m4) {
-        const int rc = m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0);
+        const int rc = fused && b == nb - 1
+                           ? m4_launch<1, 3>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, 0)
+                           : m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0);
         if (rc) return rc;
         continue;
       }
@@ -2097,7 +2177,11 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
         Ns *= c->mix_r[i];
       }
     }
-    if (2 * spc - 1 <= kStatsThreads)
+    if (fused) {
+      hipLaunchKernelGGL(m4_stats_kernel, dim3(nu), dim3(64), 0, c->stream,
+                         (const M4Top*)c->d_m4top, N1, N, u0, n_blocks, (int)nc, spc,
+                         c->d_stats);
+    } else if (2 * spc - 1 <= kStatsThreads)
       hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, c->stream,
                          (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
                          d_dump, dump_block);
@@ -2119,6 +2203,11 @@ int mx_init(gnsscorr_acq_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)N * c->g_chunk));
   HIP_TRY(hipMalloc(&c->d_gB, sizeof(double2) * (size_t)N * c->g_chunk));
   HIP_TRY(hipMalloc(&c->d_gpw, sizeof(double) * (size_t)N * c->g_chunk));
+  // GNSSCORR_ACQ_M4STATS=0: the four-step plan keeps the separate statistics pass
+  const char* fs = getenv("GNSSCORR_ACQ_M4STATS");
+  if (c->m4 && !(fs && fs[0] == '0'))
+    HIP_TRY(hipMalloc(&c->d_m4top, sizeof(M4Top) * (size_t)kM4Plans[c->m4][0] *
+                                       kM4Plans[c->m4][1] * c->g_chunk));
   double2* h = (double2*)malloc(sizeof(double2) * N);
   if (!h) return GNSSCORR_ENOMEM;
   for (long t = 0; t < N; t++) {   // W_N^t = exp(-2 pi i t / N)
@@ -2188,11 +2277,13 @@ int acq64_init(gnsscorr_acq_ctx* c) {
 
 void acq64_free(gnsscorr_acq_ctx* c) {
   void* bufs[] = {c->d_F64, c->d_X64,   c->d_in64, c->d_twN, c->d_fmap64, c->d_lead64,
-                  c->d_chirp, c->d_vf, c->d_twM, c->d_gA,  c->d_gB,     c->d_gpw};
+                  c->d_chirp, c->d_vf, c->d_twM, c->d_gA,  c->d_gB,     c->d_gpw,
+                  c->d_m4top};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   c->d_chirp = c->d_vf = c->d_twM = c->d_gA = c->d_gB = nullptr;
   c->d_gpw = nullptr;
+  c->d_m4top = nullptr;
   c->d_F64 = c->d_X64 = c->d_in64 = c->d_twN = nullptr;
   c->d_fmap64 = nullptr;
   c->d_lead64 = nullptr;

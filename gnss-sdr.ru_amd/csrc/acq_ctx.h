@@ -45,6 +45,9 @@ struct gnsscorr_acq_ctx {
   // four-step plan of the generic path (N = N1 N2, N1 = A B and N2 = C D two-radix
   // sub-transforms in LDS, two passes over the rows): 0 none, else its plan index
   int m4 = 0;
+  // the four-step plan's per-column top-2 of the power rows (row statistics fused into
+  // m4_rows): chunk x N1 entries, or null when the statistics run as their own pass
+  void* d_m4top = nullptr;
   // ---- shared
   int n_codes = 0;
   int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra

@@ -186,3 +186,32 @@ def test_four_step_equals_mixed_radix_passes(gpu, fs, generic, mode, monkeypatch
     rel2 = np.abs(w0["second"] - w1["second"]) / w0["second"]
     print(f"[four-step vs passes N={n} {mode}] peak {rel.max():.3e} second {rel2.max():.3e}")
     assert rel.max() < 1e-9 and rel2.max() < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fs,generic", [(38.192e6, "0"), (16.368e6, "1")])
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
+def test_four_step_fused_statistics_equal_stats_pass(gpu, fs, generic, mode, monkeypatch):
+    """The row statistics fused into the four-step plan's last m4_rows (per-column
+    top-2, then m4_stats_kernel over the N1 columns) against the separate one-pass
+    statistics kernel over the stored power rows (GNSSCORR_ACQ_M4STATS=0): the same
+    power values feed both, so every peak, second peak, argmax and block is equal
+    bit for bit."""
+    monkeypatch.setenv("GNSSCORR_ACQ_GENERIC", generic)
+    n = int(round(fs / 1000.0))
+    IF = _scene(gpu, fs, 2, 0x5EED0027)
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in (3, 11, 30)])
+    freqs = 2.42e6 + 500.0 * np.arange(-6, 7)
+    gf = np.tile(np.arange(len(freqs)), (3, 1))
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    out = []
+    for st in ("1", "0"):
+        monkeypatch.setenv("GNSSCORR_ACQ_M4STATS", st)
+        ctx = gpu.AcqCtx(fs, n, max_freqs=16, max_blocks=2, max_codes=3)
+        ctx.set_codes(codes)
+        out.append(ctx.search(IF, 2, freqs, np.arange(3), gf, spc=int(round(fs / 1.023e6)), mode=m))
+    (r0, w0), (r1, w1) = out
+    for k in ("code_phase", "bin"):
+        assert (r0[k] == r1[k]).all(), k
+    for k in ("peak", "second", "argmax", "block"):
+        assert (w0[k] == w1[k]).all(), k
