@@ -1901,21 +1901,38 @@ __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__
     Fr = cp.F + (long)cp.group_code[g] * cp.rs;
     shift = fm.y;
   }
-  for (int idx = threadIdx.x; idx < N1 * kM4T2; idx += kM4ColThreads) {
+  // the tile's loads all issued before the first use (a compile-time trip count): a
+  // run-time loop waits one full memory latency per element
+  constexpr int kIt = (N1 * kM4T2 + kM4ColThreads - 1) / kM4ColThreads;
+  v2d xa[kIt], xb[kIt];
+#pragma unroll
+  for (int i = 0; i < kIt; i++) {
+    const int idx = threadIdx.x + i * kM4ColThreads;
     const int n1 = idx / kM4T2, t = idx % kM4T2, n2 = n2_0 + t;
-    v2d x = (v2d){0.0, 0.0};
-    if (n2 < N2) {
+    xa[i] = xb[i] = (v2d){0.0, 0.0};
+    if (idx < N1 * kM4T2 && n2 < N2) {
       const int n = N2 * n1 + n2;
       if constexpr (MODE == 1) {
         int sx = n - shift;
         sx += sx < 0 ? N : 0;
-        const v2d xv = Xr[sx], f = Fr[n];
-        x = (v2d){fma(xv.x, f.x, xv.y * f.y), fma(xv.x, f.y, -(xv.y * f.x))};   // conj(X) F
+        xa[i] = Xr[sx];
+        xb[i] = Fr[n];
       } else {
-        x = in[row * in_rs + n];
+        xa[i] = in[row * in_rs + n];
       }
     }
-    s[n1][t] = x;
+  }
+#pragma unroll
+  for (int i = 0; i < kIt; i++) {
+    const int idx = threadIdx.x + i * kM4ColThreads;
+    if (idx < N1 * kM4T2) {
+      v2d x = xa[i];
+      if constexpr (MODE == 1) {
+        const v2d xv = xa[i], f = xb[i];
+        x = (v2d){fma(xv.x, f.x, xv.y * f.y), fma(xv.x, f.y, -(xv.y * f.x))};   // conj(X) F
+      }
+      s[idx / kM4T2][idx % kM4T2] = x;
+    }
   }
   __syncthreads();
   // A-point DFTs over p of x[B p + q], times W_N1^(q u), back into the same slots
@@ -1942,11 +1959,20 @@ __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__
     for (int w = 0; w < B; w++) s[B * u + w][t] = v[w];
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < N1 * kM4T2; idx += kM4ColThreads) {
+  v2d w[kIt];   // W_N^(n2 k1), n2 k1 < N: all loads in flight at once
+#pragma unroll
+  for (int i = 0; i < kIt; i++) {
+    const int idx = threadIdx.x + i * kM4ColThreads;
+    const int k1 = idx / kM4T2, n2 = n2_0 + idx % kM4T2;
+    w[i] = idx < N1 * kM4T2 && n2 < N2 ? tw[n2 * k1] : (v2d){0.0, 0.0};
+  }
+#pragma unroll
+  for (int i = 0; i < kIt; i++) {
+    const int idx = threadIdx.x + i * kM4ColThreads;
     const int k1 = idx / kM4T2, t = idx % kM4T2, n2 = n2_0 + t;
-    if (n2 >= N2) continue;
+    if (idx >= N1 * kM4T2 || n2 >= N2) continue;
     const v2d x = s[B * (k1 % A) + k1 / A][t];
-    out[row * N + (long)k1 * N2 + n2] = cmul(x, tw[n2 * k1]);   // W_N^(n2 k1), n2 k1 < N
+    out[row * N + (long)k1 * N2 + n2] = cmul(x, w[i]);
   }
 }
 
@@ -1981,9 +2007,20 @@ __global__ __launch_bounds__(kM4RowThreads) void m4_rows(const v2d* __restrict__
   const int N1 = N / N2;
   const int k1_0 = blockIdx.x * kM4T1;
   const long row = blockIdx.y;
-  for (int idx = threadIdx.x; idx < kM4T1 * N2; idx += kM4RowThreads) {
-    const int r = idx / N2, n2 = idx % N2, k1 = k1_0 + r;
-    s[r][n2] = k1 < N1 ? Y[row * N + (long)k1 * N2 + n2] : (v2d){0.0, 0.0};
+  {   // the tile's loads all in flight at once (see m4_cols)
+    constexpr int kIt = (kM4T1 * N2 + kM4RowThreads - 1) / kM4RowThreads;
+    v2d xa[kIt];
+#pragma unroll
+    for (int i = 0; i < kIt; i++) {
+      const int idx = threadIdx.x + i * kM4RowThreads;
+      const int r = idx / N2, n2 = idx % N2, k1 = k1_0 + r;
+      xa[i] = idx < kM4T1 * N2 && k1 < N1 ? Y[row * N + (long)k1 * N2 + n2] : (v2d){0.0, 0.0};
+    }
+#pragma unroll
+    for (int i = 0; i < kIt; i++) {
+      const int idx = threadIdx.x + i * kM4RowThreads;
+      if (idx < kM4T1 * N2) s[idx / N2][idx % N2] = xa[i];
+    }
   }
   __syncthreads();
   for (int task = threadIdx.x; task < D * kM4T1; task += kM4RowThreads) {
@@ -2013,15 +2050,27 @@ __global__ __launch_bounds__(kM4RowThreads) void m4_rows(const v2d* __restrict__
   static_assert(kM4RowThreads == 64 && 64 % kM4T1 == 0, "m4_rows: one wave, whole columns");
   double a1 = -1.0, a2 = -1.0;
   int ak = INT_MAX;
-  for (int idx = threadIdx.x; idx < kM4T1 * N2; idx += kM4RowThreads) {
+  constexpr int kOt = (kM4T1 * N2 + kM4RowThreads - 1) / kM4RowThreads;
+  double prev[(MODE == 2 || MODE == 3) ? kOt : 1];
+  if constexpr (MODE == 2 || MODE == 3) {   // the running power sums, all loads in flight
+#pragma unroll
+    for (int i = 0; i < kOt; i++) {
+      const int idx = threadIdx.x + i * kM4RowThreads;
+      const int k2 = idx / kM4T1, k1 = k1_0 + idx % kM4T1;
+      prev[i] = acc && idx < kM4T1 * N2 && k1 < N1 ? pw[row * N + k1 + (long)N1 * k2] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kOt; i++) {
+    const int idx = threadIdx.x + i * kM4RowThreads;
     const int k2 = idx / kM4T1, r = idx % kM4T1, k1 = k1_0 + r;
-    if (k1 >= N1) continue;
+    if (idx >= kM4T1 * N2 || k1 >= N1) continue;
     const v2d x = s[r][D * (k2 % C) + k2 / C];
     const long d = (long)k1 + (long)N1 * k2;
     if constexpr (MODE == 2 || MODE == 3) {
       const double q = fma(x.x, x.x, x.y * x.y) * sc;
       double* o = pw + row * N + d;
-      const double v = acc ? *o + q : q;
+      const double v = acc ? prev[i] + q : q;
       if (MODE == 2 || store) *o = v;
       if constexpr (MODE == 3) {
         a2 = v > a1 ? a1 : fmax(a2, v);
