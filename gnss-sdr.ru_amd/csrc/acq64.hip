@@ -1997,7 +1997,11 @@ __device__ __forceinline__ void top2_merge(double& a1, int& ak, double& a2, doub
 // acc); MODE 3: as 2 on a row's last block, per-column top-2 into top (pw written only
 // when store)
 template <int C, int D, int MODE>
-__global__ __launch_bounds__(kM4RowThreads) void m4_rows(const v2d* __restrict__ Y,
+#ifndef M4_ROWS_WPE
+#define M4_ROWS_WPE 2   // waves per SIMD the register budget of m4_rows allows
+#endif
+__global__ __launch_bounds__(kM4RowThreads) __attribute__((amdgpu_waves_per_eu(M4_ROWS_WPE)))
+void m4_rows(const v2d* __restrict__ Y,
                                                        v2d* __restrict__ out, int out_rs, int N,
                                                        const v2d* __restrict__ tw,
                                                        double* __restrict__ pw, int acc,
