@@ -2249,7 +2249,13 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
 
 int mx_init(gnsscorr_acq_ctx* c) {
   const long N = c->cfg.n_samples;
-  c->g_chunk = (int)((64L << 20) / (N * 16));   // ~64 MiB per work buffer
+  // ~256 MiB per work buffer: 439 rows per chunk at N = 38 192, so each pass launches
+  // ~10 k workgroups and a search takes 6 chunks (64 MiB: 25 chunks, 1.72 against 1.38
+  // ms per search, profiles/r5/acq_generic_chunk_ab_r5ao.log); GNSSCORR_ACQ_GCHUNK_MB:
+  // another size, for A/Bs
+  const char* gm = getenv("GNSSCORR_ACQ_GCHUNK_MB");
+  const long mb = gm && atol(gm) > 0 ? atol(gm) : 256;
+  c->g_chunk = (int)((mb << 20) / (N * 16));
   if (c->g_chunk < 1) c->g_chunk = 1;
   if (c->g_chunk > 4096) c->g_chunk = 4096;
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
