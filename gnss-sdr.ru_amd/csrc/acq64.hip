@@ -2260,7 +2260,8 @@ int mx_init(gnsscorr_acq_ctx* c) {
   if (c->g_chunk > 4096) c->g_chunk = 4096;
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
   HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)N * c->g_chunk));
-  HIP_TRY(hipMalloc(&c->d_gB, sizeof(double2) * (size_t)N * c->g_chunk));
+  if (!c->m4)   // the four-step plan's passes need one work buffer (Y), the Stockham passes two
+    HIP_TRY(hipMalloc(&c->d_gB, sizeof(double2) * (size_t)N * c->g_chunk));
   HIP_TRY(hipMalloc(&c->d_gpw, sizeof(double) * (size_t)N * c->g_chunk));
   // GNSSCORR_ACQ_M4STATS=0: the four-step plan keeps the separate statistics pass
   const char* fs = getenv("GNSSCORR_ACQ_M4STATS");
