@@ -1404,7 +1404,7 @@ def main():
     sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps // 5, 5), 2)
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
     gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps // 5, 5), 2)
-    gen = None if a.skip_track else run_acq_generic(dist, dev, max(a.steps // 10, 3), 1)
+    gen = None if a.skip_track else run_acq_generic(dist, dev, max(a.steps // 2, 5), 2)
     gsc = None if a.skip_track else run_gps_scilab(dist, dev, max(a.steps // 5, 5), 2)
 
     if dist.rank == 0:
