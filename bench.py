@@ -24,8 +24,8 @@ host code and not part of the hot path).
 Run: python bench.py [--gpus N --steps K --warmup W].  For N>1 under
 torch.distributed.run the launcher's RANK/WORLD_SIZE env is used; without it
 bench.py starts the N rank processes itself (launch_ranks).  Ranks synchronise
-over gloo (CPU) only for the barrier, the max-over-ranks time and a small
-result gather.
+over a host socket (gnsscorr/hostgroup.py, no torch.distributed) only for the
+barrier, the max-over-ranks time and a small result gather.
 
 Output: ONE JSON line on rank 0 -- the contract's keys first, then every
 secondary section without its descriptive strings (floats to 4 significant
@@ -78,44 +78,29 @@ METRIC = "1ms E/P/L correlations/sec + acquisition cells/sec @16.368Msps; 1/2/4/
 
 
 class Dist:
+    """The bench's ranks: barrier, max-over-ranks and gather over gnsscorr.hostgroup (a
+    Unix-domain socket on the node, no torch.distributed), so a rank maps no HIP
+    runtime but the one libgnsscorr.so was built against."""
+
     def __init__(self, load_lib=True):
+        from gnsscorr.hostgroup import HostGroup
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            # bind libgnsscorr.so (and the ROCm runtime it was built against)
-            # before torch.distributed pulls in torch's own libamdhip64
-            if load_lib:
-                gc.lib()
-            import torch.distributed as td
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            td.init_process_group("gloo", rank=self.rank, world_size=self.world)
-            self.td = td
+        self.group = HostGroup(self.rank, self.world)
 
     def barrier(self):
-        if self.world > 1:
-            self.td.barrier()
+        self.group.barrier()
 
     def max(self, x: float) -> float:
-        if self.world == 1:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
-        return float(t.item())
+        return self.group.max(x)
 
     def gather(self, obj):
         """All ranks' objects (list, rank order); small host data only."""
-        if self.world == 1:
-            return [obj]
-        out = [None] * self.world
-        self.td.all_gather_object(out, obj)
-        return out
+        return self.group.allgather(obj)
 
     def close(self):
-        if self.world > 1:
-            self.td.destroy_process_group()
+        self.group.close()
 
 
 def acq_setup(dev, rank, precision=gc.ACQ_F64, records=1):
@@ -1241,14 +1226,15 @@ def launch_ranks(n: int, argv) -> int:
     WORLD_SIZE / MASTER_* set, and wait for them.  The parent never loads
     libgnsscorr.so or touches a GPU (children are started, not exec'd).  Rank 0
     prints the JSON line (stdout is inherited).  If a rank fails, the others are
-    stopped (they would wait at the gloo barrier forever); the exit code is the
+    stopped (they would wait at the rank barrier forever); the exit code is the
     first non-zero one."""
     import subprocess
     port = int(os.environ.get("MASTER_PORT", "0")) or _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   GNSSCORR_GROUP_KEY=f"{port}-{os.getpid()}")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
                                       env=env))
     rc = 0
@@ -1358,12 +1344,13 @@ def write_detail(out):
 
 
 def stub_main(a):
-    """BENCH_STUB=1 (CPU test of the launcher): every rank joins the gloo group,
+    """BENCH_STUB=1 (CPU test of the launcher): every rank joins the host group,
     meets at the barrier and rank 0 prints n_gpus and the gathered ranks; no
     library, no GPU."""
     dist = Dist(load_lib=False)
     dist.barrier()
-    info = dist.gather(dict(rank=dist.rank, local_rank=dist.local, pid=os.getpid()))
+    info = dist.gather(dict(rank=dist.rank, local_rank=dist.local, pid=os.getpid(),
+                            torch_loaded="torch" in sys.modules))
     t = dist.max(float(dist.rank))
     if dist.rank == 0:
         print(json.dumps({"metric": METRIC, "n_gpus": dist.world, "steps": a.steps,
@@ -1616,7 +1603,7 @@ def main():
                 "ms_per_search": sky["dt"] / sky["steps"] * 1e3,
                 "config": "BASELINE config 5: (32 GPS PRN + 14 GLONASS FCH) x 41 bins x 16368 "
                           f"x 10 ms non-coherent = {sky['cells']} cell-ms per search; groups "
-                          f"sharded round-robin over {W} GPU(s), results gathered over gloo",
+                          f"sharded round-robin over {W} GPU(s), results gathered over the host group",
                 "planted_found": f"{sky['found']}/{sky['n_planted']}",
                 "dtype": "f64",
                 "shard_projection": sky["projection"],

@@ -1871,7 +1871,9 @@ extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, i
   HIP_TRY(hipSetDevice(c->cfg.device));
   const int32_t gc = code, gf = 0;
   const int recs = c->recs;   // one record, whatever set_records says
+  const int32_t* grec = c->d_group_rec;   // and no per-group records
   c->recs = 1;
+  c->d_group_rec = nullptr;
   int rc = stage_host(c, h_if, iq, n_blocks, 1, &freq, 1, 1, &gc, &gf);
   if (!rc && !c->d_dump && hipMalloc(&c->d_dump, sizeof(double) * c->cfg.n_samples) != hipSuccess) {
     gnsscorr_set_error("gnsscorr_acq_power_row: out of device memory");
@@ -1881,6 +1883,7 @@ extern "C" int gnsscorr_acq_power_row(gnsscorr_acq_ctx* c, const int8_t* h_if, i
     rc = search_launch(c, c->d_if, iq, n_blocks, GNSSCORR_ACQ_BEST_OF_BLOCKS, 1, c->d_freqs, 1,
                        1, c->d_gcode, c->d_gfreq, 16, c->d_rows, nullptr, c->d_dump, block);
   c->recs = recs;
+  c->d_group_rec = grec;
   c->spec_blocks = 0;   // its one-record spectra must not serve a later multi-record correlate
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(h_power, c->d_dump, sizeof(double) * c->cfg.n_samples,
@@ -1906,7 +1909,9 @@ extern "C" int gnsscorr_acq_set_group_records(gnsscorr_acq_ctx* c, const int32_t
                        "plan (N = 16368 or 16000)");
     return GNSSCORR_EINVAL;
   }
-  c->d_group_rec = d_group_rec;   // the caller keeps it alive and in range [0, records)
+  // the caller keeps it alive; values outside [0, records) are clamped into that range
+  // by the correlation kernel, and set_records drops the table
+  c->d_group_rec = d_group_rec;
   return GNSSCORR_OK;
 }
 
@@ -1920,6 +1925,8 @@ extern "C" int gnsscorr_acq_set_records(gnsscorr_acq_ctx* c, int n_records) {
                        "precision and a compiled plan (n_samples %d or %d)", 16368, 16000);
     return GNSSCORR_EINVAL;
   }
+  // a per-group record table was made for the previous record count: set it again
+  if (n_records != c->recs) c->d_group_rec = nullptr;
   c->recs = n_records;
   c->spec_blocks = 0;   // resident spectra were made with the previous setting
   return GNSSCORR_OK;

@@ -950,7 +950,9 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   // blocks rec * n_blocks .. of the nbT resident blocks per class
   // (gnsscorr_acq_set_group_records: group g searches record group_rec[g] only)
   const int gv = rowid / n_bins, bin = rowid % n_bins;
-  const int rec = group_rec ? group_rec[gv] : gv / gpr, g = group_rec ? gv : gv - rec * gpr;
+  // a per-group record outside [0, nbT / n_blocks) is clamped: never a read past the spectra
+  const int rec = group_rec ? min(max(group_rec[gv], 0), nbT / n_blocks - 1) : gv / gpr;
+  const int g = group_rec ? gv : gv - rec * gpr;
   const int code = group_code[g];
   const int2 fm = fmap[group_freq[g * n_bins + bin]];
   const int m = fm.y;
@@ -1453,12 +1455,22 @@ __global__ __launch_bounds__(kGThreads) void g_stats_kernel(const double* __rest
 }
 
 // One-pass row statistics (the generic path's default): 1024 threads, thread t
-// scans k = t, t + 1024, ...  Its elements lie 1024 samples apart, so the open
-// window (argmax - spc, argmax + spc) holds at most one of them when 2 spc - 1 <=
-// 1024: the thread's runner-up stands in for its maximum when that maximum is
+// scans k = t, t + 1024, ...  Its elements lie 1024 samples apart (fewer across the
+// wrap, stats1_exact), so the open window (argmax - spc, argmax + spc) holds at most
+// one of them when stats1_exact: the thread's runner-up stands in for its maximum when
+// that maximum is
 // inside the window (acq64_corr_kernel's per-thread top-2).  Same results as
 // g_stats_kernel's two passes; one read of the row.
 constexpr int kStatsThreads = 1024;
+// g_stats1_kernel is exact when no thread holds two samples inside one open window
+// of 2 spc - 1 positions.  A thread's samples are kStatsThreads apart, except across
+// the wrap: thread t's last sample t + kStatsThreads q and its first lie N - kStatsThreads q
+// apart, smallest (r = N - kStatsThreads floor((N - 1) / kStatsThreads)) for the
+// threads with the most samples (304 at N = 38192, 16 at N = 16400).
+static inline bool stats1_exact(int N, int spc) {
+  const int r = N <= kStatsThreads ? kStatsThreads : N - kStatsThreads * ((N - 1) / kStatsThreads);
+  return 2 * spc - 1 <= (r < kStatsThreads ? r : kStatsThreads);
+}
 __global__ __launch_bounds__(kStatsThreads) void g_stats1_kernel(
     const double* __restrict__ pw, int N, int u0, int n_blocks, int nc, int spc,
     gnsscorr_acq_row* __restrict__ stats, double* __restrict__ dump, int dump_block) {
@@ -1583,6 +1595,17 @@ int g_dft_rows(gnsscorr_acq_ctx* c, const v2d* a, int src_rs, int rows, v2d* out
   return GNSSCORR_OK;
 }
 
+// rows per chunk of the generic engine: at most what one call of this context
+// can run in one go (codes x frequencies x blocks covers the code spectra, the IF
+// class spectra and a search's units), so small contexts keep small work buffers
+// (ADVICE r5); 1 .. 4096
+int chunk_cap(const gnsscorr_acq_ctx* c, int rows) {
+  const long most = (long)c->cfg.max_codes * c->cfg.max_freqs * c->cfg.max_blocks;
+  if (rows > most) rows = (int)(most < 4096 ? most : 4096);
+  if (rows > 4096) rows = 4096;
+  return rows < 1 ? 1 : rows;
+}
+
 int g_init(gnsscorr_acq_ctx* c) {
   const long N = c->cfg.n_samples;
   int M = 16, P = 0;   // P: passes (radix 16, the last possibly 2 / 4 / 8)
@@ -1591,9 +1614,7 @@ int g_init(gnsscorr_acq_ctx* c) {
   c->gM = M;
   c->gP = P;
   // chunk: ~64 MiB per work buffer
-  c->g_chunk = (int)((64L << 20) / ((long)M * 16));
-  if (c->g_chunk < 1) c->g_chunk = 1;
-  if (c->g_chunk > 4096) c->g_chunk = 4096;
+  c->g_chunk = chunk_cap(c, (int)((64L << 20) / ((long)M * 16)));
   HIP_TRY(hipMalloc(&c->d_chirp, sizeof(double2) * N));
   HIP_TRY(hipMalloc(&c->d_vf, sizeof(double2) * M));
   HIP_TRY(hipMalloc(&c->d_twM, sizeof(double2) * M));
@@ -1705,7 +1726,7 @@ int g_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int n
                          dim3(kGThreads), 0, c->stream, D, N, M, b > 0, c->d_gpw);
       HIP_TRY(hipGetLastError());
     }
-    if (2 * spc - 1 <= kStatsThreads)
+    if (stats1_exact(N, spc))
       hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, c->stream,
                          (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
                          d_dump, dump_block);
@@ -2234,7 +2255,7 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
       hipLaunchKernelGGL(m4_stats_kernel, dim3(nu), dim3(64), 0, c->stream,
                          (const M4Top*)c->d_m4top, N1, N, u0, n_blocks, (int)nc, spc,
                          c->d_stats);
-    } else if (2 * spc - 1 <= kStatsThreads)
+    } else if (stats1_exact(N, spc))
       hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, c->stream,
                          (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
                          d_dump, dump_block);
@@ -2256,8 +2277,7 @@ int mx_init(gnsscorr_acq_ctx* c) {
   const char* gm = getenv("GNSSCORR_ACQ_GCHUNK_MB");
   const long mb = gm && atol(gm) > 0 ? atol(gm) : 256;
   c->g_chunk = (int)((mb << 20) / (N * 16));
-  if (c->g_chunk < 1) c->g_chunk = 1;
-  if (c->g_chunk > 4096) c->g_chunk = 4096;
+  c->g_chunk = chunk_cap(c, c->g_chunk);
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
   HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)N * c->g_chunk));
   if (!c->m4)   // the four-step plan's passes need one work buffer (Y), the Stockham passes two

@@ -199,13 +199,7 @@ __device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
 // lanes of a reused register that the branch had masked off -- the cause of
 // the wrong sums DESIGN.md recorded for reordered IF loads in round 2.
 __device__ __forceinline__ uint32_t mad24(int a, int b, uint32_t c) {
-#ifdef TRACK_ASM_MAD   // the round-2 form, kept only to reproduce the hazard (tools/gpu_mad.sh)
-  uint32_t d;
-  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-#else
   return c + (uint32_t)__mul24(a, b);
-#endif
 }
 __device__ __forceinline__ void seg_flush(int si, int sq, int lb, int pb, int eb, Acc& cur) {
   cur.a[0] = mad24(lb, si, cur.a[0]);
@@ -873,8 +867,7 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
   // cpw channels; channels of a workgroup on different streams (one stream
   // per channel, receivers split over workgroups) take the per-wave piece
   // path (run_pieces: coalesced 1 KiB wave loads, no workgroup barrier)
-  // (stage_ok 3: A/B, round-2 lane reads for mixed streams; 4: A/B, the piece
-  // path for every workgroup)
+  // (stage_ok 4: A/B, the piece path for every workgroup)
   const bool shared_stage = IQ && stage_ok && stage_ok != 4 && uni && sst >= 0;
   const bool pieces = IQ && (stage_ok == 1 || stage_ok == 4) && !shared_stage && !any_short;
   const bool stage = shared_stage;
@@ -991,19 +984,6 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
           // for two 1024-thread workgroups per CU.  The tail run (staged in
           // LDS) goes through the same loop with its missing pairs masked, so
           // it does not serialise behind the full runs of its wave.
-#ifdef TRACK_LOAD4   // round 2's "four loads at a time" variant (tools/gpu_mad.sh)
-          if (!stage) {
-            const uint4* run = reinterpret_cast<const uint4*>(src);
-#pragma unroll 1
-            for (int j = 0; j < kVec; j += 4) {
-              const uint4 u0 = run[j], u1 = run[j + 1], u2 = run[j + 2], u3 = run[j + 3];
-              chunk(u0, j);
-              chunk(u1, j + 1);
-              chunk(u2, j + 2);
-              chunk(u3, j + 3);
-            }
-          } else
-#endif
           {
           // one loop per source, typed by address space: a pointer selected
           // between the LDS stage and global memory is a generic pointer, and
@@ -1139,13 +1119,27 @@ constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
 #ifndef TRACK_X2LUT
 #define TRACK_X2LUT 1             // packed bytes expanded through a 256-word LDS table
 #endif
-#ifndef TRACK_SLOTS
-#define TRACK_SLOTS 1             // int8 pieces in flight per wave (LDS-DMA slots)
-#endif
-#ifndef TRACK_DMA_AUX
-#define TRACK_DMA_AUX 0           // cache policy of the piece LDS-DMA (2: nt, streaming)
-#endif
 constexpr uint32_t kIv4Kinc2 = 0x20000000u;   // 8 kinc2 <= 2^32
+
+// The int8 piece slot (4 KiB: 256 chunks of 16 B = 8 IQ samples; lane l's 32
+// samples are chunks 4 l .. 4 l + 3) is swizzled: chunk g sits at entry
+// slot_entry(g) = 4 (g / 4) + ((g % 4) XOR (g / 16 % 4)).  A lane's ds_read_b128
+// of its chunk j then hits 16-byte bank slot 4 (l % 4) + (j XOR (l / 4 % 4)), and
+// each of the instruction's four 16-lane groups ({0-3,12-15,20-27}, ...,
+// MI355X_MICROARCH.md LDS table) holds four lanes of every l % 4 with four
+// different l / 4 % 4: 16 distinct slots, conflict-free.  Unswizzled, the lanes'
+// 64-byte stride put four lanes on every slot (4-way, 12 extra LDS cycles per
+// read).  The map is its own inverse: DMA entry e is
+// filled from chunk slot_entry(e), which stays inside e's 4-chunk group, so a
+// DMA instruction still reads whole 128-byte lines.
+#ifndef TRACK_SLOT_SWZ
+#define TRACK_SLOT_SWZ 1
+#endif
+#ifndef TRACK_WAVE_FLUSH
+#define TRACK_WAVE_FLUSH 1
+#endif
+__device__ __forceinline__ int slot_entry(int g) { return TRACK_SLOT_SWZ ? g ^ ((g >> 4) & 3) : g; }
+__device__ __forceinline__ int slot_chunk(int e) { return slot_entry(e); }
 
 // Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
 // writes (plain stores and atomics) are visible to every lane's later LDS reads
@@ -1168,12 +1162,46 @@ __device__ __forceinline__ void flush_epoch(Acc& acc, int e, int32_t* s_sum) {
   }
 }
 
+// Adds the six sums of every lane in `fl` (its epoch: e) into the wave's per-epoch
+// LDS sums and, with CLEAR, zeroes them.  Per distinct epoch among those lanes
+// (almost always one) a DPP scan inside each 16-lane row, then one LDS atomic per
+// row from lanes 15/31/47/63.  Every lane of the wave must be active.  The piece
+// starts after a dump and the call's end flush most lanes at once: 64 lanes each
+// adding to the same six words serialise on one LDS address (63 extra LDS cycles
+// per atomic, the bulk of the kernel's SQ_LDS_BANK_CONFLICT).
+template <bool CLEAR>
+__device__ __forceinline__ void flush_lanes(bool fl, Acc& acc, int e, int32_t* s_sum, int lane) {
+  if (!TRACK_WAVE_FLUSH) {
+    if (fl) flush_epoch(acc, e, s_sum);
+    return;
+  }
+  uint64_t m = __builtin_amdgcn_ballot_w64(fl);
+  asm volatile("" : "+s"(m));
+  while (m) {
+    const int E = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(m));
+    const bool mine = fl && e == E;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      int v = mine ? (int)acc.a[k] : 0;
+      v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+      v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+      if ((lane & 15) == 15) atomicAdd(&s_sum[E * 6 + k], v);
+      if (CLEAR) acc.a[k] = mine ? 0u : acc.a[k];
+    }
+    uint64_t done = __builtin_amdgcn_ballot_w64(mine);
+    asm volatile("" : "+s"(done));
+    m &= ~done;
+  }
+}
+
 // LDS per wavefront: [IF slot (int8)] [E/P/L row] [epoch sums] [64 LO word pairs]
 __host__ __device__ constexpr int stream_sum_bytes(int nsamp) {
   return (((nsamp / GNSSCORR_OSG_ROW + 2) * 24 + 15) & ~15);
 }
 __host__ __device__ constexpr int stream_wave_lds(bool pk, int nsamp) {
-  return (pk ? 0 : kStage2Bytes * TRACK_SLOTS) + kPk8Stage + stream_sum_bytes(nsamp) + 512;
+  return (pk ? 0 : kStage2Bytes) + kPk8Stage + stream_sum_bytes(nsamp) + 512;
 }
 
 // Arguments of one osg_stream_kernel launch: n_calls consecutive calls of
@@ -1366,9 +1394,8 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
   }
   if (kPF || kX2) __syncthreads();   // the only workgroup barrier: before any wave leaves
   uint8_t* wb = reinterpret_cast<uint8_t*>(s_dyn) + wave * stream_wave_lds(PK, nsamp);
-  constexpr int kSlots = PK ? 1 : TRACK_SLOTS;
-  uint4* slot0 = reinterpret_cast<uint4*>(wb);                     // int8 only: kSlots slots
-  uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes * kSlots);
+  uint4* const slot = reinterpret_cast<uint4*>(wb);                // int8 only: the piece slot
+  uint8_t* s_row = wb + (PK ? 0 : kStage2Bytes);
   int32_t* s_sum = reinterpret_cast<int32_t*>(s_row + kPk8Stage);
   uint2* s_lo = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(s_sum) + stream_sum_bytes(nsamp));
   STREAM_PSTAMP(0);
@@ -1396,12 +1423,10 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
   const int n_pieces = (nsamp + kPieceSpan - 1) / kPieceSpan;
   int row_base = -1, row_n32 = 0;   // the E/P/L row words staged in s_row (uniform)
 
-  // ---- the pieces in flight: LDS-DMA into the wave's slots (int8: piece number
-  // n goes to slot n % kSlots), or the lane's 16 bytes in registers (packed,
-  // one piece).  iss / con: pieces issued / consumed; (q_k, q_p): the last issued.
+  // ---- the piece in flight: LDS-DMA into the wave's slot (int8), or the lane's
+  // 16 bytes in registers (packed).  iss / con: pieces issued / consumed; (q_k,
+  // q_p): the last issued.
   int iss = 0, con = 0, q_k = -1, q_p = -1;
-  bool last_full4 = false;   // the last issued int8 piece took all four DMA instructions
-  auto slot_of = [&](int n) { return slot0 + (n % kSlots) * (kStage2Bytes / 16); };
   uint2 pq0 = make_uint2(0u, 0u), pq1 = make_uint2(0u, 0u);
   auto issue = [&](int k, int p, int64_t e_call) {   // e_call: element offset of call k's stream
     const int n_piece = p * kPieceSpan;
@@ -1422,22 +1447,23 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       const int valid = min(kPieceSpan, nsamp - n_piece);
       const int full_chunks = valid / 8;
       const int8_t* g8 = A.ifbuf + e_call + 2 * (int64_t)n_piece;
-      uint4* slot = slot_of(iss);
-      last_full4 = full_chunks > 192;
+      // DMA instruction r writes slot entries 64 r + lane; it reads the chunk the
+      // entry holds in the swizzled slot layout (slot_chunk: the chunks of one
+      // 128-byte line stay within one 8-lane group, so the loads stay coalesced)
       if (full_chunks == kPieceSpan / 8) {   // a whole piece: no per-lane guards
 #pragma unroll
         for (int r = 0; r < 4; r++)
           __builtin_amdgcn_global_load_lds(
-              (const void*)(g8 + 16 * (r * 64 + lane)),
-              (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, TRACK_DMA_AUX);
+              (const void*)(g8 + 16 * slot_chunk(r * 64 + lane)),
+              (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-          const int i = r * 64 + lane;
+          const int i = slot_chunk(r * 64 + lane);
           if (i < full_chunks)
             __builtin_amdgcn_global_load_lds(
                 (const void*)(g8 + 16 * i),
-                (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, TRACK_DMA_AUX);
+                (__attribute__((address_space(3))) void*)(slot + r * 64), 16, 0, 0);
         }
       }
     }
@@ -1496,9 +1522,9 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
           e_next = (int64_t)nc.stream * A.stream_stride * 2 + (int64_t)(k + 1) * A.call_elems;
       }
     }
-    // keep kSlots pieces in flight: the rest of this call, then the next call's
+    // keep one piece in flight: the rest of this call, then the next call's
     auto top_up = [&]() {
-      while (iss - con < kSlots) {
+      while (iss == con) {
         int nk = q_k, np = q_p + 1;
         if (np >= n_pieces) {
           nk++;
@@ -1538,7 +1564,6 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       }
       // ---- this lane's 32 samples as 16 pair words (4 chunks of 4)
       uint4 ch4[4];
-      const int cslot = con;   // this piece's slot (int8)
       if constexpr (PK) {
         if constexpr (kX2) {
           auto x2 = [&](uint32_t w) {
@@ -1569,62 +1594,35 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
             uint32_t t[4] = {0u, 0u, 0u, 0u};
             for (int q = 0; q < rem / 2; q++) t[q] = g32[q];
             if (rem & 1) t[rem / 2] = (uint32_t)reinterpret_cast<const uint16_t*>(g32)[rem - 1];
-            slot_of(cslot)[i] = make_uint4(t[0], t[1], t[2], t[3]);
+            slot[slot_entry(i)] = make_uint4(t[0], t[1], t[2], t[3]);
           }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (kSlots > 1 && iss - con >= 2 && last_full4) {
-          // the four DMA instructions of the next piece are the youngest vector
-          // memory operations that may still be outstanding
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // this piece has landed
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the piece has landed in the slot
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the piece has landed in the slot
         if (p == 0) STREAM_PSTAMP(2);
-        if constexpr (kSlots > 1) {
-          // the slot read as inline asm: the compiler, which cannot tell the
-          // slots apart, would otherwise wait for every LDS-DMA in flight
-          // (vmcnt(0)) before it; the counted wait above is the dependency
-          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-          const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(
-              slot_of(cslot) + 4 * lane);
-          u32x4 v0, v1, v2, v3;
-          asm volatile(
-              "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
-              "ds_read_b128 %2, %4 offset:32\n\tds_read_b128 %3, %4 offset:48\n\t"
-              "s_waitcnt lgkmcnt(0)"
-              : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
-              : "v"(la)
-              : "memory");
-          ch4[0] = make_uint4(v0.x, v0.y, v0.z, v0.w);
-          ch4[1] = make_uint4(v1.x, v1.y, v1.z, v1.w);
-          ch4[2] = make_uint4(v2.x, v2.y, v2.z, v2.w);
-          ch4[3] = make_uint4(v3.x, v3.y, v3.z, v3.w);
-        } else {
-          const uint4* slot = slot_of(cslot);
 #pragma unroll
-          for (int j = 0; j < 4; j++) ch4[j] = slot[4 * lane + j];
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers
-        }
+        for (int j = 0; j < 4; j++) ch4[j] = slot[slot_entry(4 * lane + j)];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers
       }
       con = __builtin_amdgcn_readfirstlane(con + 1);
-      top_up();   // the slot just read takes the piece kSlots ahead
-      if (L == 0) continue;
+      top_up();   // the slot just read takes the next piece
       const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
       const uint64_t r0 = X >> 32;
       g.kph = (uint32_t)X;
-      uint32_t ep;
-      if (fast) hc_after_fast(c, r0, invD, g.hc, g.ld, ep);
-      else hc_after(c, r0, g.hc, g.ld, ep);
-      {   // a piece that starts in a later epoch than the lane's sums (rare)
+      uint32_t ep = (uint32_t)e;   // (lanes past the call's end keep their epoch)
+      if (L > 0) {
+        if (fast) hc_after_fast(c, r0, invD, g.hc, g.ld, ep);
+        else hc_after(c, r0, g.hc, g.ld, ep);
+      }
+      {   // a piece that starts in a later epoch than the lane's sums (rare; every
+          // lane still active: flush_lanes' DPP scans)
         uint64_t any = __builtin_amdgcn_ballot_w64((int)ep != e);
         asm volatile("" : "+s"(any));
         if (any) {
-          if ((int)ep != e) {
-            if (e >= 0) flush_epoch(acc, e, s_sum);
-            e = (int)ep;
-          }
+          flush_lanes<true>((int)ep != e && e >= 0, acc, e, s_sum, lane);
+          e = (int)ep;
         }
       }
+      if (L == 0) continue;
       if (fast) {
         if constexpr (kPF) {
           g.cb = row[g.ld];
@@ -1792,7 +1790,7 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
         else per_sample(std::false_type{});
       }
     }
-    if (e >= 0) flush_epoch(acc, e, s_sum);
+    flush_lanes<false>(e >= 0, acc, e, s_sum, lane);   // (the next call starts from zero)
     if (!active && iss != con) {
       // a prefetch for a call that turned out idle must land before the slot is reused
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1868,8 +1866,6 @@ struct gnsscorr_track_ctx {
   int balance = 1;         // GNSSCORR_TRACK_BALANCE=0: no LDS padding for an even spread (A/B)
   int xcall_prefetch = 1;  // GNSSCORR_TRACK_XPF=0: no cross-call piece prefetch (A/B)
   int n_cu = 256;
-  int v1 = 0;             // GNSSCORR_TRACK_V1=1: workgroups whose channels read different
-                          // streams use the round-2 per-lane global reads, not the piece path (A/B)
   size_t lds_max = 0;     // LDS bytes a workgroup may allocate (gnsscorr_device_lds_bytes)
 };
 
@@ -1913,7 +1909,6 @@ extern "C" int gnsscorr_track_create(gnsscorr_track_ctx** out, const gnsscorr_tr
   c->tic = c->tic_ref;
   if (const char* e = getenv("GNSSCORR_TRACK_STAGE_IF")) c->stage_if = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_CPW")) c->cpw_override = atoi(e);
-  if (const char* e = getenv("GNSSCORR_TRACK_V1")) c->v1 = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_PIECES")) c->pieces_all = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_STREAM")) c->stream_kernel = atoi(e) != 0;
   if (const char* e = getenv("GNSSCORR_TRACK_BALANCE")) c->balance = atoi(e) != 0;
@@ -2096,7 +2091,6 @@ static int launch(gnsscorr_track_ctx* c, const int8_t* d_if, int64_t stride, int
   threads = (threads + 63) & ~63;
   const size_t stage_bytes = (size_t)((nsamp + kRun - 1) / kRun) * kPitch * 16;
   int stage = iq && c->stage_if && stage_bytes <= (size_t)kStageMaxBytes;
-  if (stage && c->v1) stage = 3;
   if (stage && c->pieces_all) stage = 4;
   // dynamic LDS: epoch sums, E/P/L row bytes, then one region that holds either
   // the workgroup's shared IF stage or the waves' 4 KiB piece slots

@@ -631,6 +631,8 @@ class AcqCtx:
         """Records per search (fp64): n_records IF records end to end, searched
         in one launch; search() then returns (R, G) results and (R, G, B) rows."""
         _check(lib().gnsscorr_acq_set_records(self.h, int(n_records)), "gnsscorr_acq_set_records")
+        if int(n_records) != getattr(self, "records", 1):
+            self._group_rec = None   # the library drops a per-group table on a count change
         self.records = int(n_records)
 
     def set_group_records(self, d_group_rec):

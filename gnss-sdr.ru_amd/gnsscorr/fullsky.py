@@ -9,7 +9,7 @@ winning row.  A group therefore never needs data from another rank: the
 shards are disjoint group sets (round-robin, rank r takes groups i with
 i % world == r), each rank runs the same HIP kernels on its own GPU, and the
 only exchange is the final gather of the per-group results (a few hundred
-bytes) -- done by the caller over gloo, not RCCL.
+bytes) -- done by the caller over gnsscorr.hostgroup, not RCCL.
 
 Plumbing over the C-ABI (libgnsscorr.so); the computation is in acq64.hip.
 """

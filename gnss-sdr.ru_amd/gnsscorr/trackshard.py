@@ -9,9 +9,9 @@ channels read -- with channels spread round-robin that is every stream: the IF
 is broadcast by each rank's own host-to-device copy, never over RCCL -- and
 runs gnsscorr_track on its GPU with the channels' stream indices remapped to
 its local copies.  The only exchange is the gather of the per-channel results
-(64 B each) by the caller, over gloo.
+(64 B each) by the caller, over gnsscorr.hostgroup.
 
-`plan()` is pure host logic (tested with gloo on the CPU); `TrackShard` drives
+`plan()` is pure host logic (tested with the host group on the CPU); `TrackShard` drives
 the C-ABI (libgnsscorr.so).
 """
 from __future__ import annotations

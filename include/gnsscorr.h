@@ -362,7 +362,9 @@ int gnsscorr_acq_set_records(gnsscorr_acq_ctx *ctx, int n_records);
  * instead of every group on every record; results are per group.  Lets one launch
  * hold groups of different IF streams (the GPS and GLONASS records of a full-sky
  * search).  NULL turns it off.  fp64 compiled plans only; the array must stay
- * valid while correlate calls use it.  (No reference counterpart: batching.) */
+ * valid while correlate calls use it.  A value outside [0, records) is clamped
+ * into that range; gnsscorr_acq_set_records with another count turns the table
+ * off (set it again after).  (No reference counterpart: batching.) */
 int gnsscorr_acq_set_group_records(gnsscorr_acq_ctx *ctx, const int32_t *d_group_rec);
 /* Debug/parity: full |ifft|^2 power row for (code, freq, block): n_samples doubles. */
 int gnsscorr_acq_power_row(gnsscorr_acq_ctx *ctx, const int8_t *h_if, int iq, int n_blocks,

@@ -215,3 +215,63 @@ def test_four_step_fused_statistics_equal_stats_pass(gpu, fs, generic, mode, mon
         assert (r0[k] == r1[k]).all(), k
     for k in ("peak", "second", "argmax", "block"):
         assert (w0[k] == w1[k]).all(), k
+
+
+@pytest.mark.parametrize("m4stats", ["1", "0"])
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
+def test_generic_multi_chunk_38192(gpu, mode, m4stats, monkeypatch):
+    """The generic engine's chunk loop: GNSSCORR_ACQ_GCHUNK_MB=2 gives
+    3 rows per chunk at N = 38192, so the 4-code spectra take 2 chunks, the 4 class rows
+    2, and the 4 x 9 (x 2 blocks) units 12-24 chunks: every chunk after the first runs
+    with u0 > 0 in MixCorr, m4_launch and m4_stats_kernel (fused statistics on) or
+    g_stats1_kernel (off).  Against the fp64 oracle (SCI/GPS/L1/acquisition.sci:98-169)."""
+    monkeypatch.setenv("GNSSCORR_ACQ_GCHUNK_MB", "2")
+    monkeypatch.setenv("GNSSCORR_ACQ_M4STATS", m4stats)
+    fs, n, nb = 38.192e6, 38192, 2
+    ctx = gpu.AcqCtx(fs, n, max_freqs=16, max_blocks=nb, max_codes=4)
+    prns = [6, 11, 19, 25]
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in prns])
+    ctx.set_codes(codes)
+    IF = _scene(gpu, fs, nb, 0x5EED0028)
+    freqs = 2.42e6 + 500.0 * np.arange(-4, 5)
+    gf = np.tile(np.arange(len(freqs)), (4, 1))
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    res, rows = ctx.search(IF, nb, freqs, np.arange(4), gf, spc=37, mode=m)
+    ref, ref_rows = A.acquire(IF, fs, codes, freqs, gf, spc=37, n_blocks=nb,
+                              noncoherent=mode == "noncoherent", return_rows=True)
+    if mode == "noncoherent":
+        for rr in ref_rows:
+            for r in rr:
+                r["block"] = -1
+    check_rows(res, rows, ref, ref_rows, True, label=f"chunked-38192-{mode}-m4stats{m4stats}")
+    assert res[0]["metric"] > 2.5 and res[2]["metric"] > 2.5
+
+
+@pytest.mark.parametrize("engine", ["four_step", "passes", "bluestein"])
+def test_second_peak_window_across_the_wrap(gpu, engine, monkeypatch):
+    """the one-pass statistics' thread t holds samples t and
+    t + 1024 q, only N - 1024 q = 304 apart across the wrap at N = 38192.  Two copies of
+    PRN 6 put the correlation peak at sample 101 and a weaker one at 37989 (thread 101's
+    last sample, 304 before it circularly).  With spc = 400 the weaker peak lies inside
+    the open window (argmax - spc, argmax + spc), so the second peak must come from
+    outside it (acquisition.sci:150-165); a one-pass thread runner-up would report the
+    weaker copy.  Scene checked on the host: oracle second 5.5e6, weaker peak 8.7e7."""
+    monkeypatch.setenv("GNSSCORR_ACQ_BLUESTEIN", "1" if engine == "bluestein" else "0")
+    monkeypatch.setenv("GNSSCORR_ACQ_MIX4", "0" if engine == "passes" else "1")
+    fs, n, nb, spc = 38.192e6, 38192, 2, 400
+    spc_n = n / 1023.0
+    p1, p2 = 100, 100 + 37888
+    IF = gpu.ifgen(nb * n, [dict(system=0, prn=6, code_phase=(n - p1) / spc_n, doppler=500.0,
+                                 cn0=60.0),
+                            dict(system=0, prn=6, code_phase=(n - p2) / spc_n, doppler=500.0,
+                                 cn0=56.0)], fs=fs, seed=7)
+    codes = np.stack([A.make_ca_table_row(6, fs)])
+    freqs = 2.42e6 + 500.0 * np.arange(-1, 2)
+    gf = np.arange(3)[None, :]
+    ctx = gpu.AcqCtx(fs, n, max_freqs=4, max_blocks=nb, max_codes=1)
+    ctx.set_codes(codes)
+    res, rows = ctx.search(IF, nb, freqs, np.arange(1), gf, spc=spc)
+    ref, ref_rows = A.acquire(IF, fs, codes, freqs, gf, spc=spc, n_blocks=nb, return_rows=True)
+    r = ref_rows[0][2]
+    assert r["argmax"] == p1 + 1 and r["second"] < 0.1 * r["peak"]   # the trap is set
+    check_rows(res, rows, ref, ref_rows, True, label=f"wrap-window-{engine}")

@@ -91,7 +91,7 @@ def test_bench_main_assembles_the_json_line(monkeypatch):
 
 def test_bench_launches_n_ranks_itself():
     """`bench.py --gpus 2` without torch.distributed.run starts two rank processes
-    that meet at the gloo barrier (BENCH_STUB: no library, no GPU)."""
+    that meet at the host-group barrier (BENCH_STUB: no library, no GPU)."""
     import subprocess
     env = dict(os.environ, BENCH_STUB="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
@@ -108,3 +108,4 @@ def test_bench_launches_n_ranks_itself():
     assert [r["local_rank"] for r in d["ranks"]] == [0, 1]
     assert len({r["pid"] for r in d["ranks"]}) == 2
     assert d["max_rank"] == 1.0
+    assert not any(r["torch_loaded"] for r in d["ranks"])   # no second HIP runtime

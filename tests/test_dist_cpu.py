@@ -1,8 +1,10 @@
-"""CPU, multi-process: the N>1 control path with gloo (world_size 2).
+"""CPU, multi-process: the N>1 control path over the host group
+(gnsscorr/hostgroup.py: a Unix-domain socket on the node, no torch.distributed),
+world sizes 2, 3 and 8.
 
 * bench.Dist: barrier + max-over-ranks timing (the bench contract);
 * full-sky sharding (gnsscorr/fullsky.py): every rank takes a disjoint group
-  set, the per-group results are gathered (all_gather_object over gloo) and
+  set, the per-group results are gathered (HostGroup.allgather) and
   merged on rank 0 in group order -- the only exchange config 5 needs;
 * tracking sharding (gnsscorr/trackshard.py): channels round-robin over
   ranks, each rank's NCO commands remapped onto its local IF copies, results
@@ -13,7 +15,7 @@ import os
 import socket
 
 import pytest
-import torch.multiprocessing as mp
+import multiprocessing as mp
 
 
 def _free_port():
@@ -32,6 +34,7 @@ def _worker(rank, world, port, q):
     sys.path[:0] = [root, os.path.join(root, "gnss-sdr.ru_amd")]
     import bench
     from gnsscorr.fullsky import GROUPS, merge, shard
+    assert "torch" not in sys.modules
     d = bench.Dist()
     d.barrier()
     m = d.max(float(rank + 1) * 1.5)
@@ -44,8 +47,8 @@ def _worker(rank, world, port, q):
     d.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_barrier_max_and_fullsky_gather(world):
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_hostgroup_barrier_max_and_fullsky_gather(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -107,7 +110,7 @@ def _track_worker(rank, world, port, q):
 
 
 @pytest.mark.parametrize("world", [2])
-def test_gloo_track_sharding(world):
+def test_hostgroup_track_sharding(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -162,3 +165,39 @@ def test_track_shard_more_ranks_than_channels():
     assert ids == [] and len(res) == 0
     full = [(p[0], np.zeros(len(p[0]), gc.TRACK_RESULT)) for p in parts]
     assert len(merge(full, 3)) == 3
+
+
+def _group_worker(rank, world, key, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "gnss-sdr.ru_amd")]
+    from gnsscorr.hostgroup import HostGroup
+    g = HostGroup(rank, world, key=key, timeout_s=60)
+    out = []
+    for k in range(20):          # back-to-back collectives keep their order
+        out.append(g.allgather((rank, k)))
+        assert g.max(rank * k) == (world - 1) * k
+    g.close()
+    q.put((rank, out))
+
+
+def test_hostgroup_repeated_collectives_and_stale_socket(tmp_path):
+    """20 gathers in a row arrive in order on every rank; a socket file left by a
+    crashed run under the same key is replaced, not connected to."""
+    import tempfile
+    key = f"test-{os.getpid()}"
+    stale = os.path.join(tempfile.gettempdir(), f"gnsscorr-{key}.sock")
+    open(stale, "w").close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 4
+    procs = [ctx.Process(target=_group_worker, args=(r, world, key, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for r in range(world):
+        assert got[r] == [[(i, k) for i in range(world)] for k in range(20)]
+    assert not os.path.exists(stale)

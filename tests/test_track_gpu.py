@@ -382,6 +382,62 @@ def test_replay_many_streams_equals_single_calls(gpu, oracle, packed):
             np.testing.assert_array_equal(st[key][j], ref_state[j][key][0], err_msg=f"{key} {j}")
 
 
+def test_replay_bench_receiver_shape(gpu, oracle):
+    """The bench's main tracking shape: 1024 receivers x 12 channels
+    = 12288 channel-waves on 1024 interleaved int8 IQ streams, the bench's NCO schedule
+    (+-5 kHz carrier, +-3 ppm code Doppler, bench.py _track_cmds), 10 calls in ONE
+    replay_dev launch.  At this size the XCD mapping and the LDS balance padding depend
+    on the workgroup count, so it gets its own check: byte-identical to 10 single-call
+    launches, and 64 channels against the scalar oracle (oracle/osg_corr.c, reference
+    OSG/correlator/correlator.c:149-316)."""
+    rng = np.random.default_rng(12288)
+    RX, CH, K, nsamp = 1024, 12, 10, 16368
+    C = RX * CH
+    stride = K * nsamp
+    rep = gpu.TrackCtx(C, max_nsamp=nsamp, samp_rate=16.368e6)
+    seq = gpu.TrackCtx(C, max_nsamp=nsamp, samp_rate=16.368e6)
+    sb = rep.if_bytes(stride)
+    d_if = gpu.DevBuf(RX * sb)
+    d_if.fill_if2(0x5EED0003)
+    cmd1 = np.zeros(C, gpu.NCO_CMD)
+    cmd1["prn"] = rng.integers(1, 33, C)
+    cmd1["stream"] = np.repeat(np.arange(RX), CH)
+    cmd1["carrier_incr"] = 635008600 + rng.integers(-262000, 262000, C) * 20
+    cmd1["code_incr"] = 6710886 * 40 + rng.integers(-800, 800, C)
+    cmd1["epoch_load"] = -1
+    cmds = np.tile(cmd1, K).reshape(K, C)
+    d_cmds = gpu.DevBuf.from_array(cmds)
+    d_res = gpu.DevBuf(K * C * gpu.TRACK_RESULT.itemsize)
+    rep.replay_dev(d_if.ptr, stride, nsamp, K, d_cmds.ptr, d_res.ptr)
+    rep.sync()
+    got = d_res.download(gpu.TRACK_RESULT).reshape(K, C)
+    d_r1 = gpu.DevBuf(C * gpu.TRACK_RESULT.itemsize)
+    for k in range(K):
+        seq.track_dev(d_if.ptr + seq.if_bytes(k * nsamp), stride, nsamp,
+                      d_cmds.ptr + k * C * gpu.NCO_CMD.itemsize, d_r1.ptr, 0, seq.next_tic(nsamp))
+        seq.sync()
+        r = d_r1.download(gpu.TRACK_RESULT)
+        assert got[k].tobytes() == r.tobytes(), \
+            (k, np.flatnonzero((got[k]["dump"] != r["dump"]).any(axis=1))[:8])
+    sr, ss = rep.get_state(), seq.get_state()
+    for f in sr.dtype.names:
+        np.testing.assert_array_equal(sr[f], ss[f], err_msg=f)
+    assert (got["n_dumps"] >= 1).sum() >= C * K // 2   # 1-ms calls: most calls dump
+    sel = np.sort(rng.choice(C, 64, replace=False))
+    host = {int(s): d_if.download(np.int8, sb, int(s) * sb)
+            for s in np.unique(cmds[:, sel]["stream"])}
+    want, nd, ref_state = _oracle_channels(oracle, host, nsamp, cmds[:, sel].copy())
+    for k in range(K):
+        g = got[k][sel]
+        np.testing.assert_array_equal((g["n_dumps"] > 0).astype(np.int32), nd[k])
+        m = nd[k] == 1
+        np.testing.assert_array_equal(g["dump"][m], want[k][m])
+    st = rep.get_state()[sel]
+    for j in range(len(sel)):
+        for key in ("carrier_phase", "carrier_cycle", "code_phase", "half_chip", "acc"):
+            np.testing.assert_array_equal(st[key][j], ref_state[j][key][0], err_msg=f"{key} {j}")
+
+
 def test_track_rejects_bad_prn(gpu):
     ctx = gpu.TrackCtx(4, max_nsamp=1024)
     cm = _random_cmds(np.random.default_rng(0), 1, 4, 1)[0]
