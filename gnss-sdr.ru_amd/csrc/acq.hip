@@ -1474,7 +1474,7 @@ extern "C" int gnsscorr_acq_destroy(gnsscorr_acq_ctx* c) {
   acq64_free(c);
   void* bufs[] = {c->d_sigma, c->d_F, c->d_X, c->d_if, c->d_freqs, c->d_gcode, c->d_gfreq,
                   c->d_rows, c->d_res, c->d_dump, c->d_order, c->d_stage, c->d_stats,
-                  c->d_fmap, c->d_cfreq, c->d_resid, c->d_nclass};
+                  c->d_fmap, c->d_cfreq, c->d_resid, c->d_nclass, c->d_codes8, c->d_chips};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1501,6 +1501,17 @@ __global__ __launch_bounds__(256) void acq_symmetrize_kernel(float2* __restrict_
     Fc[(sn / M16) * kPlane + sn % M16] = make_float2(v.x, -v.y);
 }
 
+// spectra of the n_codes int8 replicas at d (device), kept resident
+static int codes_spectra(gnsscorr_acq_ctx* c, const int8_t* d, int n_codes) {
+  if (c->prec == GNSSCORR_ACQ_F64) return acq64_set_codes(c, d, n_codes);
+  int rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F, nullptr, nullptr);
+  if (rc) return rc;
+  hipLaunchKernelGGL(acq_symmetrize_kernel, dim3((n_codes * N + 255) / 256), dim3(256), 0,
+                     c->stream, c->d_F, n_codes);
+  HIP_TRY(hipGetLastError());
+  return GNSSCORR_OK;
+}
+
 extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const int8_t* h_codes) {
   if (!c || !h_codes || n_codes < 1 || n_codes > c->cfg.max_codes) {
     gnsscorr_set_error("gnsscorr_acq_set_codes: bad arguments (n_codes %d, max %d)", n_codes,
@@ -1509,30 +1520,78 @@ extern "C" int gnsscorr_acq_set_codes(gnsscorr_acq_ctx* c, int n_codes, const in
   }
   HIP_TRY(hipSetDevice(c->cfg.device));
   const size_t bytes = (size_t)n_codes * c->cfg.n_samples;
-  int8_t* d = nullptr;
-  HIP_TRY(hipMalloc(&d, bytes));
-  int rc = GNSSCORR_OK;
-  if (hipMemcpyAsync(d, h_codes, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
-    gnsscorr_set_error("gnsscorr_acq_set_codes: H2D copy failed");
-    rc = GNSSCORR_EDEVICE;
-  } else if (c->prec == GNSSCORR_ACQ_F64) {
-    rc = acq64_set_codes(c, d, n_codes);
-  } else {
-    rc = forward_launch(c, d, 0, 1, nullptr, 1, n_codes, c->d_F, nullptr, nullptr);
-    if (!rc) {
-      hipLaunchKernelGGL(acq_symmetrize_kernel, dim3((n_codes * N + 255) / 256), dim3(256), 0,
-                         c->stream, c->d_F, n_codes);
-      if (hipGetLastError() != hipSuccess) {
-        gnsscorr_set_error("gnsscorr_acq_set_codes: symmetrize launch failed");
-        rc = GNSSCORR_EDEVICE;
-      }
-    }
-  }
-  // the staging buffer is freed on every path, after the stream has used it
-  const hipError_t es = hipStreamSynchronize(c->stream);
-  (void)hipFree(d);
+  int rc = acq_grow((void**)&c->d_codes8, &c->cap_codes8, bytes, 1);
   if (rc) return rc;
-  HIP_TRY(es);
+  HIP_TRY(hipMemcpyAsync(c->d_codes8, h_codes, bytes, hipMemcpyHostToDevice, c->stream));
+  rc = codes_spectra(c, c->d_codes8, n_codes);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->n_codes = n_codes;
+  return GNSSCORR_OK;
+}
+
+// makeCaTable.sci:64-72 / makeStTable.sci:60-67 on the device: replica sample k
+// (1-based) takes chip ceil((ts k) / tc) (1-based; the last sample chip
+// codeLength), ts = 1/fs, tc = 1/code_rate, in fp64 exactly as gnsscorr_sample_code
+// evaluates it.  One id per replica, passed by value.
+constexpr int kIdBatch = 64;
+struct CodeIds {
+  int id[kIdBatch];
+};
+__global__ __launch_bounds__(256) void prn_codes_kernel(const int8_t* __restrict__ chips, CodeIds ids,
+                                                        int n_ids, int N, double fs,
+                                                        int8_t* __restrict__ out) {
+  const long total = (long)n_ids * N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / N), k = (int)(i % N) + 1;
+    const int id = ids.id[r];
+    const bool st = id == GNSSCORR_CODE_GLO_ST;
+    const int len = st ? 511 : 1023;
+    const double ts = 1.0 / fs, tc = 1.0 / (st ? 0.511e6 : 1.023e6);
+    long idx = (long)ceil((ts * (double)k) / tc);
+    if (k == N) idx = len;
+    const long j = ((idx - 1) % len + len) % len;
+    out[i] = chips[(st ? 32 : id - 1) * 1023 + j];
+  }
+}
+
+extern "C" int gnsscorr_acq_set_prn_codes(gnsscorr_acq_ctx* c, int n_codes,
+                                          const int32_t* h_code_ids) {
+  if (!c || !h_code_ids || n_codes < 1 || n_codes > c->cfg.max_codes) {
+    gnsscorr_set_error("gnsscorr_acq_set_prn_codes: bad arguments (n_codes %d, max %d)", n_codes,
+                       c ? c->cfg.max_codes : 0);
+    return GNSSCORR_EINVAL;
+  }
+  for (int i = 0; i < n_codes; i++)
+    if (h_code_ids[i] < 0 || h_code_ids[i] > 32) {
+      gnsscorr_set_error("gnsscorr_acq_set_prn_codes: code id %d (entry %d) is neither a GPS "
+                         "PRN 1..32 nor GNSSCORR_CODE_GLO_ST", h_code_ids[i], i);
+      return GNSSCORR_EINVAL;
+    }
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  if (!c->d_chips) {   // once per context: 32 C/A codes and the ST code
+    int8_t h[33 * 1023] = {};
+    for (int p = 1; p <= 32; p++) gnsscorr_ca_code(p, h + (p - 1) * 1023);
+    gnsscorr_st_code(h + 32 * 1023);
+    HIP_TRY(hipMalloc(&c->d_chips, sizeof h));
+    HIP_TRY(hipMemcpy(c->d_chips, h, sizeof h, hipMemcpyHostToDevice));
+  }
+  const int n = c->cfg.n_samples;
+  int rc = acq_grow((void**)&c->d_codes8, &c->cap_codes8, (size_t)n_codes * n, 1);
+  if (rc) return rc;
+  for (int b = 0; b < n_codes; b += kIdBatch) {
+    CodeIds ids;
+    const int nb = n_codes - b < kIdBatch ? n_codes - b : kIdBatch;
+    for (int i = 0; i < kIdBatch; i++) ids.id[i] = i < nb ? h_code_ids[b + i] : 1;
+    const long total = (long)nb * n;
+    const int grid = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+    hipLaunchKernelGGL(prn_codes_kernel, dim3(grid), dim3(256), 0, c->stream, c->d_chips, ids, nb,
+                       n, c->cfg.samp_rate, c->d_codes8 + (size_t)b * n);
+    HIP_TRY(hipGetLastError());
+  }
+  rc = codes_spectra(c, c->d_codes8, n_codes);
+  if (rc) return rc;
   c->n_codes = n_codes;
   return GNSSCORR_OK;
 }

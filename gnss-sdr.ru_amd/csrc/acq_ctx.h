@@ -67,6 +67,10 @@ struct gnsscorr_acq_ctx {
   size_t cap_stats = 0;
   int stat_groups = 0, stat_bins = 0, stat_blocks = 0, stat_mode = 0, stat_recs = 1;
   // host-API staging
+  int8_t* d_codes8 = nullptr;           // sampled code replicas, int8 [n_codes][N] (grown)
+  size_t cap_codes8 = 0;
+  int8_t* d_chips = nullptr;            // chip table: rows 0..31 GPS C/A PRN 1..32, row 32 the
+                                        // GLONASS ST code (511 chips), 1023 B each (set_prn_codes)
   int8_t* d_if = nullptr;
   double* d_freqs = nullptr;
   int* d_gcode = nullptr;

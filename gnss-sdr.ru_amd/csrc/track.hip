@@ -1132,13 +1132,7 @@ constexpr uint32_t kIv4Kinc2 = 0x20000000u;   // 8 kinc2 <= 2^32
 // read).  The map is its own inverse: DMA entry e is
 // filled from chunk slot_entry(e), which stays inside e's 4-chunk group, so a
 // DMA instruction still reads whole 128-byte lines.
-#ifndef TRACK_SLOT_SWZ
-#define TRACK_SLOT_SWZ 1
-#endif
-#ifndef TRACK_WAVE_FLUSH
-#define TRACK_WAVE_FLUSH 1
-#endif
-__device__ __forceinline__ int slot_entry(int g) { return TRACK_SLOT_SWZ ? g ^ ((g >> 4) & 3) : g; }
+__device__ __forceinline__ int slot_entry(int g) { return g ^ ((g >> 4) & 3); }
 __device__ __forceinline__ int slot_chunk(int e) { return slot_entry(e); }
 
 // Orders LDS accesses between the lanes of ONE wave: every lane's earlier LDS
@@ -1171,10 +1165,6 @@ __device__ __forceinline__ void flush_epoch(Acc& acc, int e, int32_t* s_sum) {
 // per atomic, the bulk of the kernel's SQ_LDS_BANK_CONFLICT).
 template <bool CLEAR>
 __device__ __forceinline__ void flush_lanes(bool fl, Acc& acc, int e, int32_t* s_sum, int lane) {
-  if (!TRACK_WAVE_FLUSH) {
-    if (fl) flush_epoch(acc, e, s_sum);
-    return;
-  }
   uint64_t m = __builtin_amdgcn_ballot_w64(fl);
   asm volatile("" : "+s"(m));
   while (m) {

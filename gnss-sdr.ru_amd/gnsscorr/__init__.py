@@ -125,6 +125,7 @@ ACQ_BEST_OF_BLOCKS = 0
 ACQ_NONCOHERENT = 1
 ACQ_F64 = 0      # reference precision (acquisition.sci evaluates in doubles)
 ACQ_F32 = 1      # single-precision fast path (n_samples 16368 only)
+CODE_GLO_ST = 0  # GNSSCORR_CODE_GLO_ST: the GLONASS ST code id of set_prn_codes
 
 
 class TrackCfg(C.Structure):
@@ -171,7 +172,7 @@ EXPORTED_FUNCTIONS = [
     "gnsscorr_acq_search", "gnsscorr_acq_search_dev", "gnsscorr_acq_power_row",
     "gnsscorr_acq_spectra_dev", "gnsscorr_acq_correlate_dev", "gnsscorr_acq_select_dev",
     "gnsscorr_acq_sync", "gnsscorr_acq_stream", "gnsscorr_acq_set_coherent",
-    "gnsscorr_acq_set_records", "gnsscorr_acq_set_group_records",
+    "gnsscorr_acq_set_records", "gnsscorr_acq_set_group_records", "gnsscorr_acq_set_prn_codes",
     "gnsscorr_sgt_loop_coefs", "gnsscorr_sgt_init_chan", "gnsscorr_sgt_create",
     "gnsscorr_sgt_destroy", "gnsscorr_sgt_track_dev", "gnsscorr_sgt_track", "gnsscorr_sgt_sync",
     "gnsscorr_sgt_stream", "gnsscorr_sgt_replay", "gnsscorr_sgt_replay_dev",
@@ -249,6 +250,7 @@ def lib() -> C.CDLL:
         "gnsscorr_acq_set_coherent": (I, [P, I]),
         "gnsscorr_acq_set_records": (I, [P, I]),
         "gnsscorr_acq_set_group_records": (I, [P, P]),
+        "gnsscorr_acq_set_prn_codes": (I, [P, I, P]),
         "gnsscorr_acq_stream": (P, [P]),
         "gnsscorr_sgt_loop_coefs": (None, [C.POINTER(SgtCfg)] + [C.POINTER(D)] * 5),
         "gnsscorr_sgt_init_chan": (I, [C.POINTER(SgtCfg), I, I, I64, I64, D, P]),
@@ -608,6 +610,14 @@ class AcqCtx:
         codes = np.ascontiguousarray(codes, np.int8).reshape(-1, self.n)
         _check(lib().gnsscorr_acq_set_codes(self.h, codes.shape[0], _ptr(codes)),
                "gnsscorr_acq_set_codes")
+
+    def set_prn_codes(self, code_ids):
+        """gnsscorr_acq_set_prn_codes: replicas generated on the device from code ids
+        (1..32: GPS C/A PRN; CODE_GLO_ST: the GLONASS ST code), then their spectra
+        (acquisition.sci:91-95).  Asynchronous on the context stream."""
+        ids = np.ascontiguousarray(code_ids, np.int32)
+        _check(lib().gnsscorr_acq_set_prn_codes(self.h, len(ids), _ptr(ids)),
+               "gnsscorr_acq_set_prn_codes")
 
     def search(self, if_samples, n_blocks, freqs, group_code, group_freq, spc=16, iq=True,
                mode=ACQ_BEST_OF_BLOCKS):

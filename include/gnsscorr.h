@@ -298,6 +298,17 @@ int gnsscorr_acq_destroy(gnsscorr_acq_ctx *ctx);
  * e.g. makeCaTable.sci / makeStTable.sci rows); their spectra are computed on
  * the device and kept resident. */
 int gnsscorr_acq_set_codes(gnsscorr_acq_ctx *ctx, int n_codes, const int8_t *h_codes);
+/* The code replicas generated on the device from code ids, then their spectra:
+ * what acquisition.sci:91-95 does at the start of every search
+ * (caCodesTable = makeCaTable(settings); conj(fft(caCodesTable(PRN,:)))).  Id p
+ * in 1..32 is GPS C/A PRN p (generateCAcode.sci, sampled at 1.023 MHz chips by
+ * makeCaTable.sci:64-72); GNSSCORR_CODE_GLO_ST is the GLONASS ST code
+ * (generateSTcode.sci, 0.511 MHz chips, makeStTable.sci:60-67).  Same replicas,
+ * bit for bit, as gnsscorr_ca_code / gnsscorr_st_code + gnsscorr_sample_code
+ * uploaded with gnsscorr_acq_set_codes.  Asynchronous on the context stream, no
+ * allocation after the first call (the chip table, 33 x 1023 B, is built then). */
+#define GNSSCORR_CODE_GLO_ST 0
+int gnsscorr_acq_set_prn_codes(gnsscorr_acq_ctx *ctx, int n_codes, const int32_t *h_code_ids);
 
 /* Search.  IF: n_blocks consecutive blocks of n_samples samples, format
  * `iq` (GNSSCORR_IF_* flags: interleaved I,Q or real, int8 or 2-bit packed).  freqs: n_freqs carrier
