@@ -1,7 +1,7 @@
 /*
  * oracle/e2e_receiver.c -- end-to-end drop-in harness (BASELINE config 1/3).
  *
- * The main loop of osgnss_next_step/src/osgnss_next_step.c:404-478 without
+ * The main loop of osgnss_next_step/src/osgnss_next_step.c:168-184 without
  * the Windows console (display.c) and the hard-coded e:\ debug path:
  *   init_tracking_loops_parameter -> correlator_init(tic_period) ->
  *   channel allocation -> while(fread 512 us of IQ) { Sim_GP2021_int; gpsisr; }
@@ -79,7 +79,7 @@ int main(int argc, char **argv)
   const long n_calls = atol(argv[3]);
   corr_out = fopen("/dev/null", "w");     /* osgpsisr.c DEBUG_TRACKING sink */
 
-  /* osgnss_next_step.c:391-399 */
+  /* osgnss_next_step.c:99-107 (init_tracking_loops_parameter) */
   calc_FLL_assisted_PLL_filter_loop_coefs(Bnp, Bnf, FLL_a_PLL_integ_time, &FLL_a_PLL_k1,
                                           &FLL_a_PLL_k2, &FLL_a_PLL_k3);
   convert_FLL_assisted_PLL_loop_filter_coefs_to_integer(FLL_a_PLL_k1, FLL_a_PLL_k2, FLL_a_PLL_k3,

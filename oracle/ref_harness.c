@@ -104,7 +104,7 @@ void ref_isr_get_chan(int ch, flat_loop *f)
   f->carrier_cold_corr = c->carrier_cold_corr; f->ms_sign = c->ms_sign;
 }
 
-/* loop constants exactly as osgnss_next_step.c:391-399 computes them, plus
+/* loop constants exactly as osgnss_next_step.c:99-107 (init_tracking_loops_parameter) computes them, plus
  * the correlator_init words; out = {i1, i2, i3, dll1, dll2, carrier_ref,
  * code_ref, d_freq} */
 void gpsisr(void);

@@ -1,6 +1,6 @@
 """CPU: the OSG loop constants and start state of the GPU channel loops.
 
-Reference: osgnss_next_step.c:391-399 (calc_* / convert_* in osgpsisr.c:253-330),
+Reference: osgnss_next_step.c:99-107 (init_tracking_loops_parameter) (calc_* / convert_* in osgpsisr.c:253-330),
 correlator.c:110-121 (reference words), osgnss_next_step.c:73-84 (reset).
 """
 import ctypes as C

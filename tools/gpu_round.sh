@@ -76,10 +76,10 @@ for L in cs1_int8 cs1_packed2 rx12_int8 rx12_packed2; do
   for V in new lo0 wg; do
     case $V in
       new) unset GNSSCORR_LIB; S=1;;
-      lo0) export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/gnsscorr/libgnsscorr_lo0.so; S=1;;
+      lo0) export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_lo0.so; S=1;;
       wg) unset GNSSCORR_LIB; S=0;;
     esac
-    [ $V = lo0 ] && [ ! -f gnss-sdr.ru_amd/gnsscorr/libgnsscorr_lo0.so ] && continue
+    [ $V = lo0 ] && [ ! -f gnss-sdr.ru_amd/ab/libgnsscorr_lo0.so ] && continue
     echo "$L $V: $(GNSSCORR_TRACK_STREAM=$S timeout -k 10 120 python3 tools/trk_layout.py $L 40)" | tee -a $O/trk_ab.log
   done
 done

@@ -1,5 +1,5 @@
 # Same-box A/B of tracking builds: bash tools/gpu_trk_libab.sh "<lib names>" [layouts] [reps] [tests]
-# lib name "base" = gnss-sdr.ru_amd/gnsscorr/libgnsscorr.so, else libgnsscorr_<name>.so
+# lib name "base" = gnss-sdr.ru_amd/gnsscorr/libgnsscorr.so, else ab/libgnsscorr_<name>.so
 # (tools/build_ab.sh); prints kernel ms per call (10-call launches, tools/trk_layout.py).
 # tests=1 first runs the tracking parity tests on the in-tree library.
 set -eu
@@ -15,7 +15,7 @@ fi
 for L in $LAYOUTS; do
   for i in $(seq $REPS); do
     for V in $LIBS; do
-      if [ $V = base ]; then unset GNSSCORR_LIB; else export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/gnsscorr/libgnsscorr_$V.so; fi
+      if [ $V = base ]; then unset GNSSCORR_LIB; else export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_$V.so; fi
       echo "$L $V: $(timeout -k 10 120 python3 tools/trk_layout.py $L 40)"
     done
   done

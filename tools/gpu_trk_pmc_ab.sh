@@ -1,7 +1,7 @@
 # PMC passes of osg_stream_kernel per tracking build and layout (12288 channels,
 # 10-call launches, tools/trk_layout.py):
 #   bash tools/gpu_trk_pmc_ab.sh <tag> "<lib names>" [layouts]
-# lib name "base" = the in-tree libgnsscorr.so, else libgnsscorr_<name>.so
+# lib name "base" = the in-tree libgnsscorr.so, else ab/libgnsscorr_<name>.so
 # (tools/build_ab.sh).  Writes gpurun_out/<tag>/pmc_<layout>_<lib>.json and prints
 # VALU / LDS instructions, bank-conflict cycles and wait share per launch.
 set -eu
@@ -14,7 +14,7 @@ mkdir -p $O
 export TMPDIR=/tmp TRK_C=${TRK_C:-12288}
 for L in $LAYOUTS; do
   for V in $LIBS; do
-    if [ $V = base ]; then unset GNSSCORR_LIB; else export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/gnsscorr/libgnsscorr_$V.so; fi
+    if [ $V = base ]; then unset GNSSCORR_LIB; else export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_$V.so; fi
     D=$O/${L}_$V; mkdir -p $D
     i=0
     for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
