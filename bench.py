@@ -6,7 +6,7 @@ Primary line (`value`): acquisition cells/s on BASELINE config 2 -- a full
 coherent, two consecutive 1-ms blocks, keep the better), 16368 samples per
 code period, computed in fp64 like the reference (Scilab doubles; parity
 ~1e-12 relative, tests/test_acq_gpu.py).  A step = complete searches of
-ACQ_RECORDS (8) consecutive 2-ms IF records already resident in HBM, each exactly
+ACQ_RECORDS (16) consecutive 2-ms IF records already resident in HBM, each exactly
 one acquisition.sci search (classes, wipe-off + FFT of the class rows, 2624
 correlation IFFTs, peak/second-peak/metric for 32 PRNs), run as one launch per
 stage (gnsscorr_acq_set_records): one record fills the GPU for 10.25 rounds of
@@ -47,7 +47,7 @@ import gnsscorr as gc  # noqa: E402
 FS = 16.368e6
 N = 16368
 N_PRN, N_BINS, N_BLK = 32, 41, 2
-ACQ_RECORDS = int(os.environ.get("BENCH_ACQ_RECORDS", "8"))   # config-2 searches per launch (gnsscorr_acq_set_records, fp64)
+ACQ_RECORDS = int(os.environ.get("BENCH_ACQ_RECORDS", "16"))   # config-2 searches per launch (gnsscorr_acq_set_records, fp64)
 CELLS_PER_SEARCH = N_PRN * N_BINS * N          # 21,474,816
 # algorithmic FLOPs of one correlation cell per 1-ms block: radix-2-equivalent
 # IFFT 5*log2(N) + complex multiply 6 + |.|^2 3 + max 1  

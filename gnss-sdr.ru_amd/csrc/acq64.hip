@@ -340,6 +340,25 @@ struct Plan {
   static constexpr int K1 = (G1 + T - 1) / T, K2 = (G2 + T - 1) / T;
   static constexpr int K3 = G3 / T, L = G3 - K3 * T;   // leftover stage-3 groups
   static constexpr int LS = L * R3 > 0 ? L * R3 : 1;
+  // LDS exchange layouts.  PFA plans (PlanA) keep the natural positions.  Cooley-Tukey
+  // plans pad them so that every exchange read and write is free of bank conflicts
+  // (PlanB at natural positions: 46 % of its LDS cycles were conflicts, PMC
+  // profiles/r6/pmc_gps_scilab_r6d.json):
+  //  exchange 1: stage-1 output (k1, g) at k1 LG1 + g.  Stage-2 group g2 = t reads
+  //    (t / R3) LG1 + t % R3 + n2 R3: with LG1 = R3 (mod 32) a 32-lane ds_read_b64 group
+  //    hits the double banks t + c (mod 32), all distinct; the writes are runs of g.
+  //  exchange 2: (k1, k2, n3) at k1 LB2 + k2 + n3 S3 (S3 = R2 + 1: injective).  The
+  //    writes (fixed k2, lanes (t / R3, t % R3)) hit S3 t (mod 16) with S3 odd; the
+  //    stage-3 reads (fixed n3, lanes k1 = t / R3, k2 = t % R3 + R3 j) hit LB2 (t / R3)
+  //    + t % R3 = t (mod 32) with LB2 = R3 (mod 32).
+  //  (MI355X_MICROARCH.md LDS table: ds_read_b64 2 x 32 lanes, bank (a/4) mod 64;
+  //  ds_write_b64 4 x 16 lanes, bank (a/4) mod 32.)
+  static constexpr int pad_to(int v, int m, int r) { return v + (((r - v) % m) + m) % m; }
+  static constexpr int LG1 = PFA_ ? N / R1 : pad_to(N / R1, 32, R3);
+  static constexpr int S2 = PFA_ ? R3 : 1;
+  static constexpr int S3 = PFA_ ? 1 : pad_to(R2 + 1, 8, 1) | 1;
+  static constexpr int LB2 = PFA_ ? R2 * R3 : pad_to(R2 * S2 + (R3 - 1) * S3 + 1, 32, R3);
+  static constexpr int LX = PFA_ ? N : (R1 * LG1 > R1 * LB2 ? R1 * LG1 : R1 * LB2);
   static constexpr int Q1 = N / R1, Q2 = N / R2, Q3 = N / R3;
   static constexpr int INV1 = PFA ? cinv(Q1 % R1, R1) : 0;
   static constexpr int INV2 = PFA ? cinv(Q2 % R2, R2) : 0;
@@ -522,7 +541,7 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       const int g = P::group1(t, j);
       if (g >= 0) {
 #pragma unroll
-        for (int k1 = 0; k1 < R1; k1++) lds[k1 * G1 + g] = part(v1[j][k1], p);
+        for (int k1 = 0; k1 < R1; k1++) lds[k1 * P::LG1 + g] = part(v1[j][k1], p);
       }
     }
     __syncthreads();
@@ -531,7 +550,7 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
     for (int j = 0; j < P::K2; j++) {
       const int g2 = t + j * T;
       if (act && g2 < G2) {
-        const int base = (g2 / R3) * G1 + g2 % R3;
+        const int base = (g2 / R3) * P::LG1 + g2 % R3;
 #pragma unroll
         for (int n2 = 0; n2 < R2; n2++) {
           set_part(v2[j][n2], p, lds[base + n2 * R3]);
@@ -560,7 +579,7 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       if (act && g2 < G2) {
         const int k1 = g2 / R3, n3 = g2 % R3;
 #pragma unroll
-        for (int k2 = 0; k2 < R2; k2++) lds[(k1 * R2 + k2) * R3 + n3] = part(v2[j][k2], p);
+        for (int k2 = 0; k2 < R2; k2++) lds[k1 * P::LB2 + k2 * P::S2 + n3 * P::S3] = part(v2[j][k2], p);
       }
     }
     __syncthreads();
@@ -568,9 +587,10 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
 #pragma unroll
     for (int j = 0; j < P::K3; j++) {
       const int g3 = act ? P::group3(t, j) : 0;
+      const int b3 = (g3 / R2) * P::LB2 + (g3 % R2) * P::S2;
 #pragma unroll
       for (int n3 = 0; n3 < R3; n3++) {
-        set_part(v3[j][n3], p, lds[g3 * R3 + n3]);
+        set_part(v3[j][n3], p, lds[b3 + n3 * P::S3]);
         lds_read_fence();
       }
     }
@@ -790,7 +810,7 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
                                                           int per_cls, int n_rows,
                                                           v2d* __restrict__ out, int rs,
                                                           const v2d* __restrict__ twN) {
-  __shared__ double lds[P::N];
+  __shared__ double lds[P::LX];
   __shared__ v2d side[P::LS];
   __shared__ v2d tw3[P::R3];
   const int t = threadIdx.x;
@@ -926,18 +946,18 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   // non-coherent: a thread's first kE running sums live in the LDS left over
   // beside the exchange plane for the whole row (the others are parked in the
   // plane between blocks, see start_sums)
-  constexpr int kLdsOther = N * 8 + P::LS * 16 + R3 * 16 + P::NW * 20 + 256;
+  constexpr int kLdsOther = P::LX * 8 + P::LS * 16 + R3 * 16 + P::NW * 20 + 256;
   constexpr int kE0 = kNC ? (kLdsBudget - kLdsOther) / (8 * T) : 0;
   constexpr int kE = kE0 < K3 * R3 ? kE0 : K3 * R3;
-  __shared__ double lds[N + kE * T];   // the exchange plane, then s_extra
+  __shared__ double lds[P::LX + kE * T];   // the exchange plane, then s_extra
   __shared__ v2d side[P::LS];
   __shared__ v2d tw3[R3];
   __shared__ double s_v[P::NW], s_m[P::NW];
   __shared__ int s_k[P::NW];
-  static_assert(sizeof(double) * (N + kE * T) + sizeof(v2d) * (P::LS + R3) +
+  static_assert(sizeof(double) * (P::LX + kE * T) + sizeof(v2d) * (P::LS + R3) +
                         (2 * sizeof(double) + sizeof(int)) * P::NW <= (size_t)kLdsBudget,
                 "acq64_corr_kernel: static LDS over the gfx950 budget");
-  double* const s_extra = lds + N;
+  double* const s_extra = lds + P::LX;
   const int t = threadIdx.x;
   const bool act = t < T;
   init_tw3<P>(tw3);
