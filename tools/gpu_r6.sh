@@ -1,18 +1,16 @@
 set -eu
 export TMPDIR=/tmp
-O=gpurun_out/r6e; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_acq_16m_gpu.py tests/test_acq_gpu.py tests/test_fullsky_gpu.py tests/test_acq_coh_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
+O=gpurun_out/r6g; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_track_gpu.py -k "two_slot" > $O/tests_s2.log 2>&1 || { tail -40 $O/tests_s2.log; exit 1; }
+tail -1 $O/tests_s2.log
+GNSSCORR_TRACK_2SLOT=1 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_track_gpu.py tests/test_packed_gpu.py tests/test_e2e_gpu.py tests/test_trackshard_gpu.py > $O/tests_forced.log 2>&1 || { tail -40 $O/tests_forced.log; exit 1; }
+tail -1 $O/tests_forced.log
+export TRK_C=12288
 for i in 1 2 3; do
-  for V in base r5acq; do
-    if [ $V = base ]; then unset GNSSCORR_LIB; else export GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_$V.so; fi
-    timeout -k 10 200 python3 tools/bench_part.py gps_scilab 10 > $O/scilab_${V}_${i}.log 2>&1
-    python3 -c "
-import json
-d = json.loads(open('$O/scilab_${V}_${i}.log').read().strip().split('\n')[-1])
-print('$V run $i', 'ms per search', round(d['dt'] / d['steps'] * 1e3, 4), 'found', d['found'], '/', d['n_planted'])"
+  for V in 0 1; do
+    echo "cs1_int8 2slot=$V: $(GNSSCORR_TRACK_2SLOT=$V timeout -k 10 120 python3 tools/trk_layout.py cs1_int8 40)"
   done
-done
-unset GNSSCORR_LIB
-bash tools/pmc_kernel.sh r6e/scilab gps_scilab 5 > $O/scilab_pmc.log 2>&1
-grep -A3 "acq64_corr_kernel<Plan<16000" $O/scilab/summary.txt | head -8 || true
+done | tee $O/ab.log
+for V in 0 1; do
+  echo "rx12_int8 2slot=$V: $(GNSSCORR_TRACK_2SLOT=$V timeout -k 10 120 python3 tools/trk_layout.py rx12_int8 40)"
+done | tee -a $O/ab.log
