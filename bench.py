@@ -1337,15 +1337,27 @@ def result_line(out):
         head["cpu_baseline"] = {k: v for k, v in head["cpu_baseline"].items()
                                 if k in ("value", "unit", "cores", "kind", "sample")}
     line = {k: (_round_all(v, 5) if isinstance(v, dict) else v) for k, v in head.items()}
+    # the workload string names the shape; its numbers, and the roofline's algorithmic
+    # bytes, stay in the detail file (the driver keeps only the tail of stdout)
+    if isinstance(line.get("config"), dict):
+        line["config"] = {k: v for k, v in line["config"].items()
+                          if k not in ("prns", "bins", "blocks", "samples_per_code", "cells_per_search")}
+    if isinstance(line.get("roofline"), dict):
+        line["roofline"].pop("hbm_algorithmic_bytes_per_launch", None)
     for k in SECTION_ORDER:
         if k in out:
             line[k] = compact(out[k])
             if k not in ("tracking", "glonass_tracking", "fullsky") and \
                     isinstance(line[k], dict) and isinstance(line[k].get("roofline"), dict):
                 line[k]["roofline"].pop("kernel", None)   # named in DESIGN.md 6
-    if "ranks" in line:   # one runtime path is enough; every rank's device and PCI id stay
-        line["ranks"] = [{k: v for k, v in r.items() if k != "hip_runtime" or r["rank"] == 0}
-                         for r in line["ranks"]]
+    if "ranks" in line:   # every rank's device and PCI id; rank 0's runtime path, and the
+        rk = out["ranks"]  # most HIP runtimes any rank maps (1: only libgnsscorr's)
+        hr = [r["hip_runtime"] if isinstance(r["hip_runtime"], dict)
+              else {"bound": r["hip_runtime"], "mapped": [r["hip_runtime"]]} for r in rk]
+        line["ranks"] = {"device": [r["device"] for r in rk],
+                         "pci": [r["pci_bus_id"] for r in rk],
+                         "hip_runtime": hr[0]["bound"],
+                         "runtimes_mapped_max": max(len(h["mapped"]) for h in hr)}
     g = line.get("glonass_tracking", {}).get("at_16368ksps")
     if g:   # the same line at the other rate: its rate, latency and kernel time
         line["glonass_tracking"]["at_16368ksps"] = {
@@ -1354,8 +1366,8 @@ def result_line(out):
             "kernel_ms_per_launch": g.get("roofline", {}).get("kernel_ms_per_launch")}
     t = line.get("tracking", {})
     for sub in list(t.get("layouts", {}).values()) + [t.get("closed_loop", {})]:
-        for k in ("unit", "calls_per_launch", "realtime_channels_per_gpu"):
-            sub.pop(k, None)   # = the tracking line's unit and TRACK_CPL
+        for k in ("unit", "calls_per_launch", "realtime_channels_per_gpu", "kernel_ms_per_launch"):
+            sub.pop(k, None)   # = the tracking line's unit, TRACK_CPL and TRACK_CPL x per call
     for sub in t.get("layouts", {}).values():
         sub.get("roofline", {}).pop("kernel", None)   # packed layouts: <true, false>
     for sub in t.get("pcie_inclusive", {}).values():
