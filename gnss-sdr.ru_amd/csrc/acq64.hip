@@ -220,12 +220,12 @@ __device__ __forceinline__ void dft_prime(v2d (&x)[P]) {
   }
   x[0] = X0;
 }
-// symmetric prime DFT fused with |.|^2 * scale: pw[k] = |X_k|^2 scale (ACC:
-// added to pw).  Outputs are folded into the powers as each (m, P-m) pair is
+// symmetric prime DFT fused with |.|^2 * scale: put(k, |X_k|^2 scale) for every
+// output k.  Outputs are folded into the powers as each (m, P-m) pair is
 // formed, so the complex outputs are never all live (register pressure of the
 // non-coherent kernel, whose running sums stay live across the transform).
-template <int P, bool ACC>
-__device__ __forceinline__ void dft_prime_power(v2d (&x)[P], double (&pw)[P], double scale) {
+template <int P, class Put>
+__device__ __forceinline__ void dft_prime_power(v2d (&x)[P], const Put& put_power, double scale) {
   constexpr int H = (P - 1) / 2;
 #pragma unroll
   for (int j = 1; j <= H; j++) {
@@ -236,10 +236,7 @@ __device__ __forceinline__ void dft_prime_power(v2d (&x)[P], double (&pw)[P], do
   v2d X0 = x[0];
 #pragma unroll
   for (int j = 1; j <= H; j++) X0 += x[j];
-  auto put = [&](int k, v2d v) {
-    const double p = fma(v.x, v.x, v.y * v.y) * scale;
-    pw[k] = ACC ? pw[k] + p : p;
-  };
+  auto put = [&](int k, v2d v) { put_power(k, fma(v.x, v.x, v.y * v.y) * scale); };
 #pragma unroll
   for (int m = 1; m <= H; m++) {
     v2d A = x[0], B = (v2d){0.0, 0.0};
@@ -496,18 +493,29 @@ __device__ __forceinline__ void set_part(v2d& v, int p, double d) {
 
 // The transform from stage-1 inputs v1 (loaded by the caller) to stage-3
 // outputs v3 (main groups g3 = t + j*T) and vl[j] (leftover outputs where
-// P::lvalid(t, j): slot P::lslot(t, j) of group K3*T + t % L).  lds: N doubles; side: LS complex;
-// tw3: W_R3^q, q < R3 (LDS); twN: W_N^j (global, CT plans only).
+// P::lvalid(t, j): slot P::lslot(t, j) of group K3*T + t % L).  lds: N doubles; side: the
+// LS real parts of the leftover groups' stage-3 inputs (their imaginary parts stay in
+// the plane after exchange 2: the leftover tasks read lds[K3*T*R3 ..] after fft_core's
+// last barrier, so a caller that writes the plane next must pass a barrier first);
+// twN: W_N^j (global, CT plans only).
 // Keeps the exchange reads as single ds_read_b64 (256 B/clk per CU): the
 // load/store optimizer otherwise pairs them into ds_read2_b64, which the LDS
 // serves at 128 B/clk (MI355X_MICROARCH.md, LDS table).
 __device__ __forceinline__ void lds_read_fence() { __builtin_amdgcn_sched_barrier(0); }
 
+// the lane id by mbcnt, opaque to the compiler (recomputed where it is used,
+// never hoisted or kept live across a loop)
+__device__ __forceinline__ int lane_id_opaque() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 struct NoHook {
   __device__ void operator()() const {}
 };
 template <class P, class Hook = NoHook, bool kStage3 = true, bool kPinStage1 = false>
-__device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
+__device__ __forceinline__ void fft_core(double* lds, double* side,
                                          const v2d* __restrict__ twN, int t,
                                          v2d (&v1)[P::K1][P::R1], v2d (&v3)[P::K3][P::R3],
                                          v2d (&vl)[2], const Hook& before_exchange = Hook()) {
@@ -595,8 +603,9 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       }
     }
     if constexpr (P::L > 0) {
-      if (t < P::L * R3) set_part(vl[0], p, lds[P::K3 * T * R3 + t]);
-      if (p == 1 && t < P::L * R3) side[t] = vl[0];
+      // PFA layout: leftover group K3*T + lg, input n3 at (K3*T + lg)*R3 + n3
+      static_assert(P::PFA, "leftover groups assume the PFA exchange layout");
+      if (p == 0 && t < P::L * R3) side[t] = lds[P::K3 * T * R3 + t];
     }
     __syncthreads();
     ACQ64_STAMP(6 + 2 * p);
@@ -608,16 +617,20 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
   }
   if constexpr (P::L > 0) {
     // leftover groups: the symmetric prime DFT (dft_prime) split by output
-    // pair, inputs from the side copy, W^(jm) from the tw3 table (cos, -sin)
+    // pair, real parts from the side copy, imaginary parts from the plane
+    // (exchange 2's last phase), W^(jm) from the constant table kTw (cos, -sin;
+    // an LDS copy took the 400 B that the non-coherent kernel's sums need)
     if (t < P::LT) {
       constexpr int H = (R3 - 1) / 2;
       const int lg = t % P::L, m = t / P::L;
-      const v2d* x = side + lg * R3;
-      v2d A = x[0], B = (v2d){0.0, 0.0};
+      const double* xr = side + lg * R3;
+      const double* xi = lds + P::K3 * T * R3 + lg * R3;
+      v2d A = (v2d){xr[0], xi[0]}, B = (v2d){0.0, 0.0};
       int q = m;
 #pragma unroll
       for (int j = 1; j <= H; j++) {
-        const v2d a = x[j], b = x[R3 - j], w = tw3[q];
+        const v2d a = (v2d){xr[j], xi[j]}, b = (v2d){xr[R3 - j], xi[R3 - j]};
+        const v2d w = (v2d){kTw<R3>.c[q], -kTw<R3>.s[q]};
         const v2d sj = a + b, dj = a - b;
         A = (v2d){fma(w.x, sj.x, A.x), fma(w.x, sj.y, A.y)};
         B = (v2d){fma(-w.y, dj.x, B.x), fma(-w.y, dj.y, B.y)};
@@ -628,12 +641,6 @@ __device__ __forceinline__ void fft_core(double* lds, v2d* side, const v2d* tw3,
       vl[1] = (v2d){A.x - B.y, A.y + B.x};   // A + iB (slot R3 - m)
     }
   }
-}
-
-template <class P>
-__device__ __forceinline__ void init_tw3(v2d* tw3) {
-  if (threadIdx.x < P::R3)
-    tw3[threadIdx.x] = (v2d){kTw<P::R3>.c[threadIdx.x], -kTw<P::R3>.s[threadIdx.x]};
 }
 
 // ---- workgroup reductions --------------------------------------------------------
@@ -688,10 +695,12 @@ __device__ __forceinline__ double wave_max(double v) {   // values >= -1
   return fmax(fmax(readlane_f64(v, 15), readlane_f64(v, 31)),
               fmax(readlane_f64(v, 47), readlane_f64(v, 63)));
 }
+// tid: the caller's thread index (default threadIdx.x)
 template <int NW>
-__device__ __forceinline__ void block_argmax(double& v, int& k, double* sv, int* sk) {
+__device__ __forceinline__ void block_argmax(double& v, int& k, double* sv, int* sk,
+                                             int tid = threadIdx.x) {
   wave_argmax(v, k);
-  if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; sk[threadIdx.x >> 6] = k; }
+  if ((tid & 63) == 0) { sv[tid >> 6] = v; sk[tid >> 6] = k; }
   __syncthreads();
   v = sv[0];
   k = sk[0];
@@ -700,11 +709,11 @@ __device__ __forceinline__ void block_argmax(double& v, int& k, double* sv, int*
     if (better(sv[i], sk[i], v, k)) { v = sv[i]; k = sk[i]; }
 }
 template <int NW>
-__device__ __forceinline__ double block_max0(double v, double* sm) {
+__device__ __forceinline__ double block_max0(double v, double* sm, int tid = threadIdx.x) {
   v = wave_max(v);
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  if ((tid & 63) == 0) sm[tid >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
 #pragma unroll
     for (int i = 1; i < NW; i++) v = fmax(v, sm[i]);
   }
@@ -811,13 +820,12 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
                                                           v2d* __restrict__ out, int rs,
                                                           const v2d* __restrict__ twN) {
   __shared__ double lds[P::LX];
-  __shared__ v2d side[P::LS];
-  __shared__ v2d tw3[P::R3];
+  __shared__ double side[P::LS];
   const int t = threadIdx.x;
-  init_tw3<P>(tw3);
   // rows grid-strided over a capped grid (n_rows is an upper bound of the
   // rows when the class count is on the device); fft_core ends on a barrier
-  // after its last LDS read, so the next row may start writing at once
+  // after its last exchange read, but the leftover tasks (P::L > 0) read the
+  // plane after it: the next row's exchange-1 writes wait for a barrier
   const int rows = n_cls_dev ? *n_cls_dev * per_cls : n_rows;
   for (int w = blockIdx.x; w < rows; w += gridDim.x) {
     const v2d* src = in + (long)w * P::N;
@@ -829,7 +837,7 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
       for (int n1 = 0; n1 < P::R1; n1++) v1[j][n1] = src[n1 * P::G1 + g];
     }
     v2d v3[P::K3][P::R3], vl[2] = {(v2d){0.0, 0.0}, (v2d){0.0, 0.0}};
-    fft_core<P>(lds, side, tw3, twN, t, v1, v3, vl);
+    fft_core<P>(lds, side, twN, t, v1, v3, vl);
     v2d* o = out + (long)w * rs;
     if (t < P::T) {
 #pragma unroll
@@ -847,6 +855,7 @@ __global__ __launch_bounds__(P::TB) void acq64_fwd_kernel(const v2d* __restrict_
           P::out_base(P::K3 * P::T + t % P::L, base, step);
           o[P::store_index((base + P::lslot(t, j) * step) % P::N)] = vl[j];
         }
+      __syncthreads();   // leftover tasks' plane reads before the next row's writes
     }
   }
 }
@@ -946,21 +955,26 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
   // non-coherent: a thread's first kE running sums live in the LDS left over
   // beside the exchange plane for the whole row (the others are parked in the
   // plane between blocks, see start_sums)
-  constexpr int kLdsOther = P::LX * 8 + P::LS * 16 + R3 * 16 + P::NW * 20 + 256;
+  constexpr int kLdsOther = P::LX * 8 + P::LS * 8 + P::NW * 20;
   constexpr int kE0 = kNC ? (kLdsBudget - kLdsOther) / (8 * T) : 0;
-  constexpr int kE = kE0 < K3 * R3 ? kE0 : K3 * R3;
-  __shared__ double lds[P::LX + kE * T];   // the exchange plane, then s_extra
-  __shared__ v2d side[P::LS];
-  __shared__ v2d tw3[R3];
+  // one s_extra row holds the leftover outputs' sums (pwl) when there are any
+  constexpr int kPwlRow = (kNC && L > 0 && kE0 > 0) ? 1 : 0;
+  static_assert(!kPwlRow || 2 * P::LT <= T, "leftover sums fit one s_extra row");
+  constexpr int kE = kE0 - kPwlRow < K3 * R3 ? kE0 - kPwlRow : K3 * R3;
+  __shared__ double lds[P::LX + (kE + kPwlRow) * T];   // the exchange plane, then s_extra
+  __shared__ double side[P::LS];
   __shared__ double s_v[P::NW], s_m[P::NW];
   __shared__ int s_k[P::NW];
-  static_assert(sizeof(double) * (P::LX + kE * T) + sizeof(v2d) * (P::LS + R3) +
+  static_assert(sizeof(double) * (P::LX + (kE + kPwlRow) * T + P::LS) +
                         (2 * sizeof(double) + sizeof(int)) * P::NW <= (size_t)kLdsBudget,
                 "acq64_corr_kernel: static LDS over the gfx950 budget");
   double* const s_extra = lds + P::LX;
-  const int t = threadIdx.x;
+  // non-coherent: threadIdx.x is rebuilt inside and after the block loop from the
+  // wave's base (uniform: an SGPR) and the lane id, so no per-lane copy of it stays
+  // live across the loop (that copy was the kernel's last spill to scratch)
+  const int wave_base = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
+  int t = threadIdx.x;
   const bool act = t < T;
-  init_tw3<P>(tw3);
   ACQ64_STAMP(0);
   const int unit = order[blockIdx.x];
   const int rowid = kNC ? unit : unit / n_blocks;
@@ -995,8 +1009,13 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     const v2d* Fc = F + fofs;
     // likewise every thread-dependent address: t is opaque per block, so the
     // index arithmetic is redone per block instead of held across it
-    int t = threadIdx.x;
-    asm volatile("" : "+v"(t));
+    int t;
+    if constexpr (kNC) {
+      t = wave_base + lane_id_opaque();
+    } else {
+      t = threadIdx.x;
+      asm volatile("" : "+v"(t));
+    }
     // stage-1 inputs: conj(X[k - m]) * F[k]  (= conj(X * conj(F)), acquisition.sci:116).
     // Slots of groups a thread does not own are left as garbage: fft_core never
     // stores them.
@@ -1077,34 +1096,39 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
             const double v = lds[(j * R3 + k) * T + tt];
             pw[j][k] = first ? 0.0 : v;
           }
-        pwl[0] = first ? (P::lvalid(t, 0) ? 0.0 : -1.0) : pwl[0];
-        pwl[1] = first ? (P::lvalid(t, 1) ? 0.0 : -1.0) : pwl[1];
+        if constexpr (!kPwlRow) {
+          pwl[0] = first ? (P::lvalid(t, 0) ? 0.0 : -1.0) : pwl[0];
+          pwl[1] = first ? (P::lvalid(t, 1) ? 0.0 : -1.0) : pwl[1];
+        }
         __syncthreads();   // exchange 1 overwrites the parked sums
       }
     };
     // |.|^2 / N^2 (|ifft(Y)|^2 = |fft(conj Y)|^2 / N^2); a prime radix-R3
     // stage is fused with the powers
     constexpr bool kFuse = is_prime(R3);
-    fft_core<P, decltype(start_sums), !kFuse, kNC>(lds, side, tw3, twN, t, v1, v3, vl,
+    fft_core<P, decltype(start_sums), !kFuse, kNC>(lds, side, twN, t, v1, v3, vl,
                                                    start_sums);
-    if constexpr (kE > 0) {
-      const int tt = min(t, T - 1);
-#pragma unroll
-      for (int f = 0; f < kE; f++) {
-        const double v = s_extra[f * T + tt];
-        pw[f / R3][f % R3] = i == 0 ? 0.0 : v;
-      }
-    }
+    // the first kE running sums are added to in place in s_extra, each read
+    // just before its output is formed: they take no registers in stage 3
 #pragma unroll
     for (int j = 0; j < K3; j++) {
-      if constexpr (kFuse) {
-        dft_prime_power<R3, kNC>(v3[j], pw[j], inv_n2);
-      } else {
-#pragma unroll
-        for (int k3 = 0; k3 < R3; k3++) {
-          const double p = fma(v3[j][k3].x, v3[j][k3].x, v3[j][k3].y * v3[j][k3].y) * inv_n2;
+      auto put_power = [&](int k3, double p) {
+        const int f = j * R3 + k3;
+        if (kNC && f < kE) {
+          if (act) {
+            double* const a = s_extra + f * T + t;
+            *a = (i == 0 ? 0.0 : *a) + p;
+          }
+        } else {
           pw[j][k3] = kNC ? pw[j][k3] + p : p;
         }
+      };
+      if constexpr (kFuse) {
+        dft_prime_power<R3>(v3[j], put_power, inv_n2);
+      } else {
+#pragma unroll
+        for (int k3 = 0; k3 < R3; k3++)
+          put_power(k3, fma(v3[j][k3].x, v3[j][k3].x, v3[j][k3].y * v3[j][k3].y) * inv_n2);
       }
     }
     if constexpr (L > 0) {
@@ -1112,9 +1136,15 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
       for (int j = 0; j < 2; j++)
         if (P::lvalid(t, j)) {
           const double p = fma(vl[j].x, vl[j].x, vl[j].y * vl[j].y) * inv_n2;
-          pwl[j] = kNC ? pwl[j] + p : p;
+          if constexpr (kPwlRow) {   // in place in the s_extra row after the kE sums
+            double* const a = s_extra + kE * T + j * P::LT + t;
+            *a = (i == 0 ? 0.0 : *a) + p;
+          } else {
+            pwl[j] = kNC ? pwl[j] + p : p;
+          }
         }
     }
+    static_assert(!(DUMP && kNC), "power dumps are coherent-mode only");
     if (DUMP && blk == dump_block && act) {
 #pragma unroll
       for (int j = 0; j < K3; j++) {
@@ -1147,11 +1177,21 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
 #pragma unroll
           for (int k = 0; k < R3; k++) {
             const int f = j * R3 + k;
-            if (f < kE) s_extra[f * T + t] = pw[j][k];
-            else lds[f * T + t] = pw[j][k];
+            if (f >= kE) lds[f * T + t] = pw[j][k];   // f < kE: already in s_extra
           }
       }
     }
+  }
+  if constexpr (kNC) t = wave_base + lane_id_opaque();
+  if constexpr (kE > 0) {
+    const int tt = min(t, T - 1);
+#pragma unroll
+    for (int f = 0; f < kE; f++) pw[f / R3][f % R3] = s_extra[f * T + tt];
+  }
+  if constexpr (kPwlRow) {
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+      pwl[j] = P::lvalid(t, j) ? s_extra[kE * T + j * P::LT + t] : -1.0;
   }
   // ---- row statistics.  Per stage-3 group, the thread's outputs lie
   // SPACING = N/R3 samples apart, so an exclusion window narrower than that
@@ -1194,7 +1234,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
         if (better(pwl[j], kl[j], bv, bk)) { bv = pwl[j]; bk = kl[j]; }
       }
   }
-  block_argmax<P::NW>(bv, bk, s_v, s_k);
+  block_argmax<P::NW>(bv, bk, s_v, s_k, t);
   ACQ64_STAMP(9);
   // second peak: max outside the open circular window (bk - spc, bk + spc)
   auto outside = [&](int k) {
@@ -1223,7 +1263,7 @@ __global__ __launch_bounds__(P::TB) void acq64_corr_kernel(
     for (int j = 0; j < 2; j++)
       if (P::lvalid(t, j) && outside(kl[j])) sv = fmax(sv, pwl[j]);
   }
-  sv = block_max0<P::NW>(sv, s_m);
+  sv = block_max0<P::NW>(sv, s_m, t);
   ACQ64_STAMP(10);
   if (t == 0) {
     gnsscorr_acq_row r;
