@@ -1371,6 +1371,8 @@ int acq_grow(void** p, size_t* cap, size_t need, size_t elem) {
   return GNSSCORR_OK;
 }
 
+static int codes_preload(gnsscorr_acq_ctx* c);
+
 extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cfg* cfg) {
   if (!out || !cfg || cfg->max_freqs < 1 || cfg->max_blocks < 1 || cfg->max_codes < 1 ||
       cfg->samp_rate <= 0 ||
@@ -1433,7 +1435,9 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
     return fail(GNSSCORR_ENOMEM);
   }
   if (c->prec == GNSSCORR_ACQ_F64) {
-    const int rc = acq64_init(c);
+    int rc = acq64_init(c);
+    if (!rc) rc = acq64_preload(c);
+    if (!rc) rc = codes_preload(c);
     if (rc) return fail(rc);
     *out = c;
     return GNSSCORR_OK;
@@ -1463,6 +1467,7 @@ extern "C" int gnsscorr_acq_create(gnsscorr_acq_ctx** out, const gnsscorr_acq_cf
     gnsscorr_set_error("gnsscorr_acq_create: %s", hipGetErrorString(e));
     return fail(GNSSCORR_EDEVICE);
   }
+  if (const int rc = codes_preload(c)) return fail(rc);
   *out = c;
   return GNSSCORR_OK;
 }
@@ -1556,6 +1561,24 @@ __global__ __launch_bounds__(256) void prn_codes_kernel(const int8_t* __restrict
   }
 }
 
+// Once per context (gnsscorr_acq_create): the chip table (32 C/A codes and the
+// ST code), the replica buffer for max_codes codes, and this file's code object
+// loaded, so that the context's first set_codes / set_prn_codes costs what
+// every later one does.
+static int codes_preload(gnsscorr_acq_ctx* c) {
+  int8_t h[33 * 1023] = {};
+  for (int p = 1; p <= 32; p++) gnsscorr_ca_code(p, h + (p - 1) * 1023);
+  gnsscorr_st_code(h + 32 * 1023);
+  HIP_TRY(hipMalloc(&c->d_chips, sizeof h));
+  HIP_TRY(hipMemcpy(c->d_chips, h, sizeof h, hipMemcpyHostToDevice));
+  const int rc = acq_grow((void**)&c->d_codes8, &c->cap_codes8,
+                          (size_t)c->cfg.max_codes * c->cfg.n_samples, 1);
+  if (rc) return rc;
+  hipFuncAttributes a;
+  HIP_TRY(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&prn_codes_kernel)));
+  return GNSSCORR_OK;
+}
+
 extern "C" int gnsscorr_acq_set_prn_codes(gnsscorr_acq_ctx* c, int n_codes,
                                           const int32_t* h_code_ids) {
   if (!c || !h_code_ids || n_codes < 1 || n_codes > c->cfg.max_codes) {
@@ -1570,13 +1593,6 @@ extern "C" int gnsscorr_acq_set_prn_codes(gnsscorr_acq_ctx* c, int n_codes,
       return GNSSCORR_EINVAL;
     }
   HIP_TRY(hipSetDevice(c->cfg.device));
-  if (!c->d_chips) {   // once per context: 32 C/A codes and the ST code
-    int8_t h[33 * 1023] = {};
-    for (int p = 1; p <= 32; p++) gnsscorr_ca_code(p, h + (p - 1) * 1023);
-    gnsscorr_st_code(h + 32 * 1023);
-    HIP_TRY(hipMalloc(&c->d_chips, sizeof h));
-    HIP_TRY(hipMemcpy(c->d_chips, h, sizeof h, hipMemcpyHostToDevice));
-  }
   const int n = c->cfg.n_samples;
   int rc = acq_grow((void**)&c->d_codes8, &c->cap_codes8, (size_t)n_codes * n, 1);
   if (rc) return rc;

@@ -2465,6 +2465,19 @@ int spectra_launch(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks
 
 }  // namespace
 
+// Once per context (gnsscorr_acq_create): the input buffer of max_codes code
+// transforms, and this file's code object loaded on the device (HIP loads a
+// translation unit's kernels on their first use: ~3 ms on the first
+// set_prn_codes of a process otherwise; hipFuncGetAttributes loads it).
+int acq64_preload(gnsscorr_acq_ctx* c) {
+  int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)c->cfg.max_codes * c->cfg.n_samples,
+                    sizeof(double2));
+  if (rc) return rc;
+  hipFuncAttributes a;
+  HIP_TRY(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&acq64_classify_kernel)));
+  return GNSSCORR_OK;
+}
+
 int acq64_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes) {
   int rc = acq_grow((void**)&c->d_in64, &c->cap_in64, (size_t)n_codes * c->cfg.n_samples,
                     sizeof(double2));

@@ -89,6 +89,7 @@ int acq_grow(void** p, size_t* cap, size_t need, size_t elem);
 int acq64_plan_for(int n_samples);
 int acq64_init(gnsscorr_acq_ctx* c);             // device tables for the plan
 void acq64_free(gnsscorr_acq_ctx* c);
+int acq64_preload(gnsscorr_acq_ctx* c);   // code spectra buffers + code-object load
 int acq64_set_codes(gnsscorr_acq_ctx* c, const int8_t* d_codes, int n_codes);
 int acq64_spectra(gnsscorr_acq_ctx* c, const int8_t* d_if, int iq, int n_blocks, int n_freqs,
                   const double* d_freqs);
