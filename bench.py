@@ -118,8 +118,9 @@ def acq_setup(dev, rank, precision=gc.ACQ_F64, records=1):
     # acquisition.sci:91-95 makes caCodesTable and takes conj(fft(caCodesTable(PRN,:)))
     # inside every search; here the 32 replicas are generated on the device from the
     # PRN list and transformed (gnsscorr_acq_set_prn_codes) once, outside the timed
-    # steps: 32 of the ~2 700 transforms of a search.  The cold call (context's first:
-    # chip table upload, buffer allocation, first launches) is timed here; the warm
+    # steps: 32 of the ~2 700 transforms of a search.  The context's first call is
+    # timed here (gnsscorr_acq_create did the one-time work: chip table, buffers,
+    # code objects loaded); the warm
     # cost and a whole cold-start search with the codes inside it are timed in
     # run_acq (single_search.with_codes).
     t0 = time.perf_counter()
