@@ -473,7 +473,9 @@ __device__ __forceinline__ void hc_after_fast(const Chan& c, uint64_t r, float i
   } else {
     const uint32_t m = (uint32_t)(r - c.j1);
     uint32_t e = (uint32_t)((float)m * invD);
-    int q = (int)(m - e * c.D);
+    // e < 2^14 and D < 2^17 (r counts the half-chips of one call): a full-rate
+    // 24-bit multiply, not v_mul_lo_u32
+    int q = (int)(m - __umul24(e, c.D));
     if (q < 0) { q += (int)c.D; e--; }
     if (q >= (int)c.D) { q -= (int)c.D; e++; }
     epoch = 1 + e;
@@ -1532,10 +1534,20 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
     for (int q = 0; q < 6; q++) acc.a[q] = 0;
     int e = -1;   // epoch of acc (-1: nothing yet)
     Seg g;
+    // the carrier and code NCO phases at the lane's first sample, advanced by one
+    // piece (kPieceSpan samples: uniform steps) per piece with full-rate adds, not
+    // a 32 x 32-bit and a 64-bit multiply per piece (quarter rate)
+    // (the carrier phase steps in g.p0 itself where the pair loops do not advance
+    // it, i.e. with the LO words read ahead)
+    const uint32_t p0_step = (uint32_t)kPieceSpan * c.cinc;
+    if constexpr (kPF) g.p0 = c.P0 + (uint32_t)(lane * kPieceLen) * c.cinc - p0_step;
+    uint64_t x_cur = (uint64_t)c.K0 + (uint64_t)(uint32_t)(lane * kPieceLen) * c.kinc2;
+    const uint64_t x_step = (uint64_t)kPieceSpan * c.kinc2;
     for (int p = 0; active && p < n_pieces; p++) {
       const int n0 = p * kPieceSpan + lane * kPieceLen;
       const int L = max(0, min(kPieceLen, nsamp - n0));
-      g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
+      if constexpr (kPF) g.p0 += p0_step;   // c.P0 + n0 cinc
+      else g.p0 = c.P0 + (uint32_t)n0 * c.cinc;
       // the piece's 16 LO word pairs (pair q: carrier phases p0 + 2q cinc and
       // p0 + (2q + 1) cinc, correlator.c:203-204), read before the piece's IF
       // wait so that both LDS round trips overlap
@@ -1595,7 +1607,8 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
       }
       con = __builtin_amdgcn_readfirstlane(con + 1);
       top_up();   // the slot just read takes the next piece
-      const uint64_t X = (uint64_t)c.K0 + (uint64_t)n0 * c.kinc2;
+      const uint64_t X = x_cur;   // c.K0 + n0 kinc2
+      x_cur += x_step;
       const uint64_t r0 = X >> 32;
       g.kph = (uint32_t)X;
       uint32_t ep = (uint32_t)e;   // (lanes past the call's end keep their epoch)
@@ -1623,12 +1636,6 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
         }
         g.ti = g.tq = g.pi = g.pq = 0;
         g.carried = false;
-        // whether any lane's 32 samples hold a dump: its half-chip count at the
-        // window start plus the window's code carries reaches D (one dump per
-        // ~16 k samples, so 7 of 8 pieces have none and skip the dump test at
-        // every interval end)
-        const uint64_t Xe = (uint64_t)c.K0 + (uint64_t)(n0 + L) * c.kinc2;
-        const bool dump_here = g.hc + (uint32_t)((Xe >> 32) - r0) >= c.D;
         // intervals of kIv pairs: 3 (6 samples) whenever a half-chip lasts >= 6
         // samples; 4 (8 samples, 4 interval ends per piece instead of 6) when it
         // lasts >= 8, i.e. 8 kinc2 <= 2^32 (at 16.368 Msps: code rates up to the
@@ -1693,6 +1700,12 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
           }
         };
         if (__all(L == kPieceLen)) {
+          // whether any lane's 32 samples hold a dump: its half-chip count at the
+          // window start plus the window's code carries, (kph + 32 kinc2) >> 32,
+          // reaches D (one dump per ~16 k samples, so 7 of 8 pieces have none and
+          // skip the dump test at every interval end)
+          const bool dump_here =
+              g.hc + (uint32_t)(((uint64_t)g.kph + (uint64_t)kPieceLen * c.kinc2) >> 32) >= c.D;
           uint64_t anyd = __builtin_amdgcn_ballot_w64(dump_here);
           asm volatile("" : "+s"(anyd));
           using I3 = std::integral_constant<int, 3>;
@@ -1707,10 +1720,13 @@ __global__ __launch_bounds__(64 * kStreamCh, CLOSED ? 1 : TRACK_STREAM_WAVES) vo
             // next carry (>= j + 31) is past the piece
             const float r = (4294967296.0f - (float)g.kph) * __builtin_amdgcn_rcpf((float)c.kinc2);
             const int j = min(8, max(1, (int)__builtin_ceilf(r)));
-            auto h = [&](int n) {
-              return (uint32_t)(((uint64_t)g.kph + (uint64_t)(uint32_t)n * c.kinc2) >> 32);
-            };
-            const bool ok = h(j - 1) == 0u && h(j) == 1u && h(j + 23) == 3u && h(j + 24) == 4u;
+            // with Y = kph + j kinc2 and Z = Y + 24 kinc2: h(j) = 1 and h(j + 24) = 4 are
+            // their high words; then h(j - 1) = 0 iff Y - kinc2 < 2^32, i.e. lo(Y) < kinc2,
+            // and h(j + 23) = 3 iff lo(Z) < kinc2 (one 64-bit multiply, not four)
+            const uint64_t Y = (uint64_t)g.kph + (uint64_t)(uint32_t)j * c.kinc2;
+            const uint64_t Z = Y + 24ull * c.kinc2;
+            const bool ok = (uint32_t)(Y >> 32) == 1u && (uint32_t)Y < c.kinc2 &&
+                            (uint32_t)(Z >> 32) == 4u && (uint32_t)Z < c.kinc2;
             uint64_t bad = __builtin_amdgcn_ballot_w64(!ok);
             asm volatile("" : "+s"(bad));
             if (!bad) {
