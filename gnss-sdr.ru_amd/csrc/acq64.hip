@@ -519,7 +519,7 @@ __device__ __forceinline__ void fft_core(double* lds, double* side,
                                          const v2d* __restrict__ twN, int t,
                                          v2d (&v1)[P::K1][P::R1], v2d (&v3)[P::K3][P::R3],
                                          v2d (&vl)[2], const Hook& before_exchange = Hook()) {
-  constexpr int R1 = P::R1, R2 = P::R2, R3 = P::R3, T = P::T, G1 = P::G1, G2 = P::G2;
+  constexpr int R1 = P::R1, R2 = P::R2, R3 = P::R3, T = P::T, G2 = P::G2;
   const bool act = t < T;
   // ---- stage 1
 #pragma unroll
@@ -1959,12 +1959,20 @@ int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, in
 #define M4_T1 4     // m4_rows: rows k1 per workgroup
 #endif
 constexpr int kM4ColThreads = M4_CT, kM4T2 = M4_T2, kM4RowThreads = M4_RT, kM4T1 = M4_T1;
+// The intermediate rows Y[k1][n2] are stored at a pitch of N2 rounded up to whole
+// m4_cols tiles (kM4T2 columns = 256 B): every tile writes whole, aligned 128-byte
+// lines that no other workgroup touches (at the natural pitch N2 = 341 a tile's
+// 256-byte runs straddled three lines shared with the neighbouring tiles, which run
+// on other XCDs)
+__host__ __device__ constexpr int m4_pitch(int n2) { return (n2 + kM4T2 - 1) / kM4T2 * kM4T2; }
 
 // MODE 0: rows in (stride in_rs); MODE 1: the correlation product of unit u0 + row
 template <int A, int B, int MODE>
+// tws: W_N1^j, j < N1 (the inner twiddles, a compact L1-resident table)
 __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__ in, int in_rs,
                                                        v2d* __restrict__ out, int N,
-                                                       const v2d* __restrict__ tw, MixCorr cp) {
+                                                       const v2d* __restrict__ tw,
+                                                       const v2d* __restrict__ tws, MixCorr cp) {
   constexpr int N1 = A * B;
   __shared__ v2d s[N1][kM4T2 + 1];
   const int N2 = N / N1;
@@ -2024,7 +2032,7 @@ __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__
     for (int p = 0; p < A; p++) v[p] = s[B * p + q][t];
     dft<A>(v);
 #pragma unroll
-    for (int u = 1; u < A; u++) v[u] = cmul(v[u], tw[q * u * N2]);   // W_N1^(q u) = W_N^(q u N2)
+    for (int u = 1; u < A; u++) v[u] = cmul(v[u], tws[q * u]);   // W_N1^(q u), q u < N1
 #pragma unroll
     for (int u = 0; u < A; u++) s[B * u + q][t] = v[u];
   }
@@ -2040,20 +2048,27 @@ __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__
     for (int w = 0; w < B; w++) s[B * u + w][t] = v[w];
   }
   __syncthreads();
-  v2d w[kIt];   // W_N^(n2 k1), n2 k1 < N: all loads in flight at once
-#pragma unroll
-  for (int i = 0; i < kIt; i++) {
-    const int idx = threadIdx.x + i * kM4ColThreads;
-    const int k1 = idx / kM4T2, n2 = n2_0 + idx % kM4T2;
-    w[i] = idx < N1 * kM4T2 && n2 < N2 ? tw[n2 * k1] : (v2d){0.0, 0.0};
+  // W_N^(n2 k1): a thread's slots i have one column n2 and k1 = k1_0 + kStep i, so
+  // two table loads (W_N^(n2 k1_0) and the step W_N^(kStep n2)) and a recurrence,
+  // instead of one scattered load from the N-entry table per output (a third of the
+  // pass's loads); ~kIt ulp of rounding drift in the twiddles
+  static_assert(kM4ColThreads % kM4T2 == 0, "m4_cols: a thread keeps one column");
+  constexpr int kStep = kM4ColThreads / kM4T2;
+  const int t0 = threadIdx.x % kM4T2, n2t = n2_0 + t0, k10 = threadIdx.x / kM4T2;
+  v2d wc = (v2d){1.0, 0.0}, ws = (v2d){1.0, 0.0};
+  if (n2t < N2) {
+    wc = tw[n2t * k10];
+    ws = tw[kStep * n2t];
   }
 #pragma unroll
   for (int i = 0; i < kIt; i++) {
     const int idx = threadIdx.x + i * kM4ColThreads;
-    const int k1 = idx / kM4T2, t = idx % kM4T2, n2 = n2_0 + t;
-    if (idx >= N1 * kM4T2 || n2 >= N2) continue;
-    const v2d x = s[B * (k1 % A) + k1 / A][t];
-    out[row * N + (long)k1 * N2 + n2] = cmul(x, w[i]);
+    const int k1 = idx / kM4T2;
+    if (idx < N1 * kM4T2 && n2t < N2) {
+      const v2d x = s[B * (k1 % A) + k1 / A][t0];
+      out[row * (long)N1 * m4_pitch(N2) + (long)k1 * m4_pitch(N2) + n2t] = cmul(x, wc);
+    }
+    wc = cmul(wc, ws);
   }
 }
 
@@ -2084,7 +2099,7 @@ template <int C, int D, int MODE>
 __global__ __launch_bounds__(kM4RowThreads) __attribute__((amdgpu_waves_per_eu(M4_ROWS_WPE)))
 void m4_rows(const v2d* __restrict__ Y,
                                                        v2d* __restrict__ out, int out_rs, int N,
-                                                       const v2d* __restrict__ tw,
+                                                       const v2d* __restrict__ tws,   // W_N2^j
                                                        double* __restrict__ pw, int acc,
                                                        M4Top* __restrict__ top, int store) {
   constexpr int N2 = C * D;
@@ -2099,7 +2114,9 @@ void m4_rows(const v2d* __restrict__ Y,
     for (int i = 0; i < kIt; i++) {
       const int idx = threadIdx.x + i * kM4RowThreads;
       const int r = idx / N2, n2 = idx % N2, k1 = k1_0 + r;
-      xa[i] = idx < kM4T1 * N2 && k1 < N1 ? Y[row * N + (long)k1 * N2 + n2] : (v2d){0.0, 0.0};
+      xa[i] = idx < kM4T1 * N2 && k1 < N1
+                  ? Y[row * (long)N1 * m4_pitch(N2) + (long)k1 * m4_pitch(N2) + n2]
+                  : (v2d){0.0, 0.0};
     }
 #pragma unroll
     for (int i = 0; i < kIt; i++) {
@@ -2115,7 +2132,7 @@ void m4_rows(const v2d* __restrict__ Y,
     for (int p = 0; p < C; p++) v[p] = s[r][D * p + q];
     dft<C>(v);
 #pragma unroll
-    for (int u = 1; u < C; u++) v[u] = cmul(v[u], tw[q * u * N1]);   // W_N2^(q u) = W_N^(q u N1)
+    for (int u = 1; u < C; u++) v[u] = cmul(v[u], tws[q * u]);   // W_N2^(q u), q u < N2
 #pragma unroll
     for (int u = 0; u < C; u++) s[r][D * u + q] = v[u];
   }
@@ -2224,14 +2241,16 @@ int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_r
               const MixCorr& cp, double* pw, int acc, int store = 1) {
   const int N = c->cfg.n_samples;
   const v2d* tw = (const v2d*)c->d_twN;
+  const v2d* tws1 = (const v2d*)c->d_twm4;   // W_N1^j, then W_N2^j from + N1
   v2d* Y = (v2d*)c->d_gA;
   switch (c->m4) {
 #define M4_CASE(I, A, B, C, D)                                                                 \
   case I:                                                                                      \
     hipLaunchKernelGGL((m4_cols<A, B, MODE_IN>), dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows), \
-                       dim3(kM4ColThreads), 0, c->stream, in, in_rs, Y, N, tw, cp);            \
+                       dim3(kM4ColThreads), 0, c->stream, in, in_rs, Y, N, tw, tws1, cp);      \
     hipLaunchKernelGGL((m4_rows<C, D, MODE_OUT>), dim3((A * B + kM4T1 - 1) / kM4T1, rows),     \
-                       dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tw, pw, acc,      \
+                       dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
+                       acc,                                                                     \
                        (M4Top*)c->d_m4top, store);                                              \
     break;
     M4_CASE(1, 7, 16, 11, 31)
@@ -2339,7 +2358,11 @@ int mx_init(gnsscorr_acq_ctx* c) {
   c->g_chunk = (int)((mb << 20) / (N * 16));
   c->g_chunk = chunk_cap(c, c->g_chunk);
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
-  HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)N * c->g_chunk));
+  // (the four-step plan's Y rows at the m4_pitch, a few % above N)
+  const long ya = c->m4 ? (long)kM4Plans[c->m4][0] * kM4Plans[c->m4][1] *
+                              m4_pitch((int)(N / (kM4Plans[c->m4][0] * kM4Plans[c->m4][1])))
+                        : N;
+  HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)ya * c->g_chunk));
   if (!c->m4)   // the four-step plan's passes need one work buffer (Y), the Stockham passes two
     HIP_TRY(hipMalloc(&c->d_gB, sizeof(double2) * (size_t)N * c->g_chunk));
   HIP_TRY(hipMalloc(&c->d_gpw, sizeof(double) * (size_t)N * c->g_chunk));
@@ -2355,6 +2378,18 @@ int mx_init(gnsscorr_acq_ctx* c) {
     h[t] = make_double2(cos(a), sin(a));
   }
   hipError_t e = hipMemcpy(c->d_twN, h, sizeof(double2) * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess && c->m4) {
+    // the passes' inner twiddles as compact tables (the same values as d_twN's)
+    const long N1 = kM4Plans[c->m4][0] * kM4Plans[c->m4][1], N2 = N / N1;
+    double2* ht = (double2*)malloc(sizeof(double2) * (N1 + N2));
+    if (!ht) { free(h); return GNSSCORR_ENOMEM; }
+    for (long j = 0; j < N1; j++) ht[j] = h[j * N2];        // W_N1^j = W_N^(j N2)
+    for (long j = 0; j < N2; j++) ht[N1 + j] = h[j * N1];   // W_N2^j = W_N^(j N1)
+    e = hipMalloc(&c->d_twm4, sizeof(double2) * (N1 + N2));
+    if (e == hipSuccess)
+      e = hipMemcpy(c->d_twm4, ht, sizeof(double2) * (N1 + N2), hipMemcpyHostToDevice);
+    free(ht);
+  }
   free(h);
   HIP_TRY(e);
   return GNSSCORR_OK;
@@ -2418,12 +2453,13 @@ int acq64_init(gnsscorr_acq_ctx* c) {
 void acq64_free(gnsscorr_acq_ctx* c) {
   void* bufs[] = {c->d_F64, c->d_X64,   c->d_in64, c->d_twN, c->d_fmap64, c->d_lead64,
                   c->d_chirp, c->d_vf, c->d_twM, c->d_gA,  c->d_gB,     c->d_gpw,
-                  c->d_m4top};
+                  c->d_m4top, c->d_twm4};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   c->d_chirp = c->d_vf = c->d_twM = c->d_gA = c->d_gB = nullptr;
   c->d_gpw = nullptr;
   c->d_m4top = nullptr;
+  c->d_twm4 = nullptr;
   c->d_F64 = c->d_X64 = c->d_in64 = c->d_twN = nullptr;
   c->d_fmap64 = nullptr;
   c->d_lead64 = nullptr;

@@ -48,6 +48,7 @@ struct gnsscorr_acq_ctx {
   // the four-step plan's per-column top-2 of the power rows (row statistics fused into
   // m4_rows): chunk x N1 entries, or null when the statistics run as their own pass
   void* d_m4top = nullptr;
+  double2* d_twm4 = nullptr;            // four-step: W_N1^j (j < N1) then W_N2^j (j < N2)
   // ---- shared
   int n_codes = 0;
   int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra
