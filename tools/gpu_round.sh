@@ -6,7 +6,7 @@ set -eu
 TAG=${1:-r1}
 PART=${2:-all}
 O=gpurun_out/$TAG
-mkdir -p $O/pmc $O/pmc_acq $O/pmc_track $O/pmc_fullsky $O/pmc_glo_coherent
+mkdir -p $O/pmc $O/pmc_acq $O/pmc_track $O/pmc_fullsky $O/pmc_glo_coherent $O/pmc_acq_generic $O/pmc_gps_scilab
 export TMPDIR=/tmp
 if [ $PART != pmc ]; then
 echo "== pytest -m gpu"
@@ -33,6 +33,8 @@ python3 tools/trace_by_grid.py $O/prof acq64_corr_kernel $O/acq64_trace_by_grid.
 fi
 if [ $PART = main ]; then echo "== done (main)"; exit 0; fi
 echo "== pmc"
+# the committed traffic file is the base: every pass below updates its entries
+cp profiles/pmc_traffic.json $O/pmc_traffic.json
 B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
 i=0
 for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
@@ -44,7 +46,7 @@ for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
 done
 python tools/pmc_summary.py $O/pmc $O/pmc_summary.json --traffic $O/pmc_traffic.json
 # HBM bytes per launch of the kernels several sections share, one section at a time
-for S in acq track fullsky glo_coherent; do
+for S in acq track fullsky glo_coherent acq_generic gps_scilab; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
       python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1

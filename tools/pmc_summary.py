@@ -55,12 +55,11 @@ def main():
     if "--traffic" in sys.argv:
         t = sys.argv[sys.argv.index("--traffic") + 1]
         sec = sys.argv[sys.argv.index("--section") + 1] if "--section" in sys.argv else None
-        keep = {}
+        try:   # merged into the existing file: sections not profiled this time stay
+            keep = json.load(open(t))
+        except (OSError, ValueError):
+            keep = {}
         if sec:
-            try:
-                keep = json.load(open(t))
-            except (OSError, ValueError):
-                keep = {}
             for k, m in s.items():
                 if "hbm_bytes_per_launch" in m:
                     keep[f"{sec}/{k}"] = {"hbm_bytes_per_launch": m["hbm_bytes_per_launch"],
