@@ -1,6 +1,8 @@
 # One GPU session: parity tests, bench, kernel-trace stats, PMC passes.
-# usage (via gpurun): bash tools/gpu_round.sh <tag> [main|pmc|all]
+# usage (via gpurun): bash tools/gpu_round.sh <tag> [main|pmc|pmcA|pmcB|all]
 #   main: tests, smoke, bench, kernel-trace stats; pmc: counter passes and the tracking A/B
+#   (pmcA: the whole-bench passes, pmcB: the per-section passes and the A/B, for two
+#   calls within gpurun's time limit: copy pmcA's pmc_traffic.json to profiles/ first)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -eu
 TAG=${1:-r1}
@@ -8,7 +10,7 @@ PART=${2:-all}
 O=gpurun_out/$TAG
 mkdir -p $O/pmc $O/pmc_acq $O/pmc_track $O/pmc_fullsky $O/pmc_glo_coherent $O/pmc_acq_generic $O/pmc_gps_scilab
 export TMPDIR=/tmp
-if [ $PART != pmc ]; then
+if [ $PART = main ] || [ $PART = all ]; then
 echo "== pytest -m gpu"
 # test failures (rc 1) are recorded and the session goes on; a timeout, abort or
 # crash ends it
@@ -24,6 +26,7 @@ s0=$(date +%s.%N)
 timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
 s1=$(date +%s.%N)
 python3 -c "print('wall_s', round($s1-$s0, 1))" | tee $O/bench.wall
+cp gpurun_out/bench_detail.json $O/bench_detail.json   # (the profiled run below rewrites it)
 cut -c1-400 $O/bench.json
 echo "== rocprofv3 kernel-trace stats"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
@@ -36,6 +39,7 @@ echo "== pmc"
 # the committed traffic file is the base: every pass below updates its entries
 cp profiles/pmc_traffic.json $O/pmc_traffic.json
 B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+if [ $PART != pmcB ]; then
 i=0
 for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
          "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" \
@@ -45,6 +49,8 @@ for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
   echo "pmc pass $i ok"
 done
 python tools/pmc_summary.py $O/pmc $O/pmc_summary.json --traffic $O/pmc_traffic.json
+fi
+if [ $PART = pmcA ]; then echo "== done (pmcA)"; exit 0; fi
 # HBM bytes per launch of the kernels several sections share, one section at a time
 for S in acq track fullsky glo_coherent acq_generic gps_scilab; do
   for C in FETCH_SIZE WRITE_SIZE; do
