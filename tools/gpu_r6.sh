@@ -1,12 +1,12 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r6p
-mkdir -p $O
+O=gpurun_out/r6y
+mkdir -p $O/pmc_fullsky
 export TMPDIR=/tmp BENCH_FULLSKY_PROJECTION=0
-for i in 1 2; do
-  for PC in "1 64" "1 128" "1 256" "0 128" "0 256"; do
-    set -- $PC
-    GNSSCORR_ACQ_M4PIPE=$1 GNSSCORR_ACQ_GCHUNK_MB=$2 timeout -k 10 300 python3 tools/bench_part.py acq_generic 20 > $O/gen_$1_$2_$i.json
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('pipe', sys.argv[2], 'chunk MiB', sys.argv[3], 'ms per search %.4f' % (d['dt']*1e3/20), 'found %s/%s' % (d['found'], d['n_planted']))" $O/gen_$1_$2_$i.json $1 $2
-  done
-done | tee $O/pipe_chunk_ab.log
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_fullsky/$C -o run -- \
+    python3 tools/bench_part.py fullsky 10 > $O/pmc_fullsky/$C.log 2>&1
+done
+cp profiles/pmc_traffic.json $O/pmc_traffic.json
+python tools/pmc_summary.py $O/pmc_fullsky $O/pmc_summary_fullsky.json --traffic $O/pmc_traffic.json --section fullsky --runs 13
+bash tools/gpu_trk_libab.sh "base p1 p2" "cs1_int8 rx12_int8" 3 0 | tee $O/trk_lo_probe.log

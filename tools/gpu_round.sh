@@ -52,6 +52,8 @@ python tools/pmc_summary.py $O/pmc $O/pmc_summary.json --traffic $O/pmc_traffic.
 fi
 if [ $PART = pmcA ]; then echo "== done (pmcA)"; exit 0; fi
 # HBM bytes per launch of the kernels several sections share, one section at a time
+# (the full-sky section without its shard projection: only the world-1 launches)
+export BENCH_FULLSKY_PROJECTION=0
 for S in acq track fullsky glo_coherent acq_generic gps_scilab; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$S/$C -o run -- \
