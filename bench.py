@@ -58,7 +58,7 @@ PEAK_HBM_GBS = 8000.0
 # the OSG tracking correlator of IQ streams (track.hip osg_stream_kernel<packed, waves/channel>)
 TRACK_KERNEL = "osg_stream_kernel<false, false>"      # int8 IQ, open loop
 TRACK_KERNEL_PK = "osg_stream_kernel<true, false>"    # 2-bit packed IQ
-TRACK_KERNEL_CL = "osg_stream_kernel<false, true>"    # closed loop: gpsisr fused
+TRACK_KERNEL_CL = "osg_stream_kernel<false, true>"    # closed loop, GNSSCORR_OSG_FUSED=1: gpsisr fused
 # calls per osg_stream_kernel launch in the tracking lines (replay and closed loop run
 # n calls per launch; a fixed count keeps rocprof per-launch figures comparable)
 TRACK_CPL = 10
@@ -1552,15 +1552,15 @@ def main():
                     "metric": "1ms E/P/L correlations/sec with the gpsisr channel loops on the GPU",
                     "value": C * steps_t * W / trk["dt_cl"],
                     "unit": "channel-ms/s",
-                    "config": f"{C} channels, 1-ms calls: {TRACK_KERNEL_CL} runs "
-                              f"{TRACK_CPL} consecutive calls per launch, every channel's gpsisr "
-                              "step (acquisition / confirm / pull-in / tracking state machine) "
-                              "after its epilogue in the same wave, NCO words fed back on the "
-                              "device, no host round trip",
+                    "config": f"{C} channels, 1-ms calls: per call the correlator "
+                              f"({TRACK_KERNEL}) and then osg_isr_kernel, every channel's gpsisr "
+                              "step (acquisition / confirm / pull-in / tracking state machine, 64 "
+                              "channels per wave), NCO words fed back on the device, no host "
+                              "round trip (GNSSCORR_OSG_FUSED=1: both in one launch of "
+                              f"{TRACK_KERNEL_CL} per {TRACK_CPL} calls, 6 % slower)",
                     "ms_per_call": trk["cl_ms"],
                     "us_per_3072_channel_ms": trk["cl_ms"] * 1e3 * 3072 / C,
-                    "kernel": TRACK_KERNEL_CL, "calls_per_launch": TRACK_CPL,
-                    **pmc_hbm("track", TRACK_KERNEL_CL, trk["cl_ms"] * 1e-3 * TRACK_CPL),
+                    "kernel": TRACK_KERNEL + " + osg_isr_kernel", "launches_per_call": 2,
                 },
             }
         if tio:

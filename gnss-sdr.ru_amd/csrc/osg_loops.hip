@@ -142,9 +142,14 @@ extern "C" int gnsscorr_osg_closed_loop_dev(gnsscorr_track_ctx* ctx,
   }
   hipStream_t s = (hipStream_t)gnsscorr_track_stream(ctx);
   const int64_t bytes_per_call = gnsscorr_track_if_bytes(ctx, nsamp);
-  // GNSSCORR_OSG_FUSED=0: the two-launch form (correlator, then osg_isr_kernel; A/B)
+  // Two launches per call (the open-loop correlator, then osg_isr_kernel with 64
+  // channels per wave) unless GNSSCORR_OSG_FUSED=1: the fused launch (every call and
+  // every channel's gpsisr step in osg_stream_kernel, gpsisr on one lane of each
+  // channel's wave) is byte-identical but, since the open-loop kernel's round-6
+  // set-up work, 6 % slower (0.104 against 0.098 ms per 12 288-channel call: 165
+  // VGPRs and no LO read-ahead, profiles/r6/closed_loop_fused_ab_r6z.log)
   const char* fe = getenv("GNSSCORR_OSG_FUSED");
-  if (!(fe && fe[0] == '0')) {
+  if (fe && fe[0] == '1') {
     // every call and every channel's gpsisr step in ONE launch
     const int rf = gnsscorr_track_dev_isr(ctx, d_if, stream_stride, nsamp, n_calls, d_cmds,
                                           d_res_hist, n_ch, cfg, d_loops, d_loop_hist);

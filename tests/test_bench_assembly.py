@@ -78,7 +78,8 @@ def test_bench_main_assembles_the_json_line(monkeypatch):
     assert t["roofline"]["calls_per_launch"] == bench.TRACK_CPL
     assert t["roofline"]["kernel_ms_per_launch"] == t["roofline"]["kernel_ms_per_call"] * \
         bench.TRACK_CPL
-    assert t["closed_loop"]["kernel"] == bench.TRACK_KERNEL_CL
+    assert t["closed_loop"]["kernel"] == bench.TRACK_KERNEL + " + osg_isr_kernel"
+    assert t["closed_loop"]["launches_per_call"] == 2
     for lay_key in ("cs1_int8", "cs1_packed2", "rx12_packed2"):
         r = t["layouts"][lay_key]["roofline"]
         assert {"hbm_GBs", "hbm_frac", "traffic"} <= set(r), lay_key
