@@ -224,8 +224,12 @@ __device__ __forceinline__ void dft_prime(v2d (&x)[P]) {
 // output k.  Outputs are folded into the powers as each (m, P-m) pair is
 // formed, so the complex outputs are never all live (register pressure of the
 // non-coherent kernel, whose running sums stay live across the transform).
-template <int P, class Put>
-__device__ __forceinline__ void dft_prime_power(v2d (&x)[P], const Put& put_power, double scale) {
+// symmetric prime DFT that hands each output to emit(k, X_k) as its (m, P-m) pair
+// is formed (s_j, d_j in place in x): the 31 complex outputs are never all live
+// SERIAL: one output pair at a time (a scheduling barrier after each): the compiler
+// otherwise interleaves all (P-1)/2 accumulator pairs, 4 P more live registers
+template <int P, bool SERIAL = false, class Emit>
+__device__ __forceinline__ void dft_prime_emit(v2d (&x)[P], const Emit& emit) {
   constexpr int H = (P - 1) / 2;
 #pragma unroll
   for (int j = 1; j <= H; j++) {
@@ -236,7 +240,6 @@ __device__ __forceinline__ void dft_prime_power(v2d (&x)[P], const Put& put_powe
   v2d X0 = x[0];
 #pragma unroll
   for (int j = 1; j <= H; j++) X0 += x[j];
-  auto put = [&](int k, v2d v) { put_power(k, fma(v.x, v.x, v.y * v.y) * scale); };
 #pragma unroll
   for (int m = 1; m <= H; m++) {
     v2d A = x[0], B = (v2d){0.0, 0.0};
@@ -247,10 +250,15 @@ __device__ __forceinline__ void dft_prime_power(v2d (&x)[P], const Put& put_powe
       A = (v2d){fma(c, x[j].x, A.x), fma(c, x[j].y, A.y)};
       B = (v2d){fma(sn, x[P - j].x, B.x), fma(sn, x[P - j].y, B.y)};
     }
-    put(m, (v2d){A.x + B.y, A.y - B.x});       // A - iB
-    put(P - m, (v2d){A.x - B.y, A.y + B.x});   // A + iB
+    emit(m, (v2d){A.x + B.y, A.y - B.x});       // A - iB
+    emit(P - m, (v2d){A.x - B.y, A.y + B.x});   // A + iB
+    if constexpr (SERIAL) __builtin_amdgcn_sched_barrier(0);
   }
-  put(0, X0);
+  emit(0, X0);
+}
+template <int P, class Put>
+__device__ __forceinline__ void dft_prime_power(v2d (&x)[P], const Put& put_power, double scale) {
+  dft_prime_emit<P>(x, [&](int k, v2d v) { put_power(k, fma(v.x, v.x, v.y * v.y) * scale); });
 }
 
 // Good-Thomas R = A * B, gcd(A, B) = 1: n = (a B + b A) mod R, k = CRT(ka, kb)
@@ -1941,7 +1949,7 @@ int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, in
 // W_N1^(n1 k1) x[N2 n1 + n2].  m4_cols runs the N1-point DFTs of a tile of kM4T2
 // columns n2 in LDS (A-point DFTs, twiddle W_N1^(q u), B-point DFTs: the standard
 // two-factor split), multiplies by W_N^(n2 k1) and writes Y[k1 N2 + n2]; m4_rows
-// runs the N2-point DFTs of kM4T1 rows k1 the same way and writes X[k1 + N1 k2].
+// (m4_rows2) runs the N2-point DFTs of kR2 rows k1 the same way and writes X[k1 + N1 k2].
 // Two passes over the rows instead of the four of the mixed-radix plan at
 // N = 38 192 = 112 x 341; the correlation product is formed in the first, |.|^2 /
 // N^2 in the second (acquisition.sci:107-132), as in mx_pass.
@@ -1953,12 +1961,9 @@ int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, in
 #define M4_T2 16    // m4_cols: columns n2 per workgroup
 #endif
 #ifndef M4_RT
-#define M4_RT 64    // m4_rows threads
+#define M4_RT 64    // m4_rows2 threads
 #endif
-#ifndef M4_T1
-#define M4_T1 4     // m4_rows: rows k1 per workgroup
-#endif
-constexpr int kM4ColThreads = M4_CT, kM4T2 = M4_T2, kM4RowThreads = M4_RT, kM4T1 = M4_T1;
+constexpr int kM4ColThreads = M4_CT, kM4T2 = M4_T2, kM4RowThreads = M4_RT;
 // The intermediate rows Y[k1][n2] are stored at a pitch of N2 rounded up to whole
 // m4_cols tiles (kM4T2 columns = 256 B): every tile writes whole, aligned 128-byte
 // lines that no other workgroup touches (at the natural pitch N2 = 341 a tile's
@@ -2072,7 +2077,7 @@ __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__
   }
 }
 
-// Per-column top-2 of a power row (MODE 3 of m4_rows): the column k1 holds the
+// Per-column top-2 of a power row (MODE 3 of m4_rows2): the column k1 holds the
 // samples k1 + N1 k2, N1 apart, so when 2 spc - 1 <= N1 the open window around the
 // row's argmax holds at most one of them and {a1, first index, runner-up} per column
 // give the second peak exactly (g_stats1_kernel's argument with columns for threads).
@@ -2089,106 +2094,120 @@ __device__ __forceinline__ void top2_merge(double& a1, int& ak, double& a2, doub
   a1 = take ? b1 : a1;
 }
 
-// MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added when
-// acc); MODE 3: as 2 on a row's last block, per-column top-2 into top (pw written only
-// when store)
-template <int C, int D, int MODE>
-#ifndef M4_ROWS_WPE
-#define M4_ROWS_WPE 2   // waves per SIMD the register budget of m4_rows allows
+// m4_rows2 MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added
+// to the running sums when ACC); MODE 3: as 2 on a row's last block, per-column top-2
+// into top (pw written only when store)
+// The rows pass (round 6; the round-5 m4_rows kept complex rows in LDS, 21.9 KB per
+// 4-row tile, 7 waves per CU): the C-point stage reads its inputs straight from Y
+// (lanes cover 4 rows x 16 consecutive n2: whole lines), the exchange to the D-point
+// stage goes through ONE fp64 plane at a time (real parts, then imaginary parts:
+// 4 x (N2 + 1) doubles, 10.9 KB), and the prime D-point stage emits its outputs as
+// they are formed (power, statistics or complex rows go out from registers, no LDS
+// round trip).  232 VGPRs: 8 waves per CU.  The arithmetic is m4_rows' except the
+// stage-A twiddles (a recurrence, <= C roundings of drift).  38.192 Msps search
+// 1.14-1.15 -> 1.09-1.11 ms (profiles/r6/acq_generic_rows2_ab_r7b.log).
+#ifndef M4_ROWS2_WPE
+#define M4_ROWS2_WPE 2   // waves per SIMD of m4_rows2 (232 VGPRs; 3 spills ~70)
 #endif
-__global__ __launch_bounds__(kM4RowThreads) __attribute__((amdgpu_waves_per_eu(M4_ROWS_WPE)))
-void m4_rows(const v2d* __restrict__ Y,
-                                                       v2d* __restrict__ out, int out_rs, int N,
-                                                       const v2d* __restrict__ tws,   // W_N2^j
-                                                       double* __restrict__ pw, int acc,
-                                                       M4Top* __restrict__ top, int store) {
-  constexpr int N2 = C * D;
-  __shared__ v2d s[kM4T1][N2 + 1];
+#ifndef M4_ROWS2_ROWS
+#define M4_ROWS2_ROWS 4   // rows k1 per m4_rows2 workgroup (2: 150 VGPRs, 12 waves per CU, but
+                          // 22 of 64 lanes in the 31-point stage: 1.21 against 1.10 ms)
+#endif
+constexpr int kR2 = M4_ROWS2_ROWS;
+template <int C, int D, int MODE, bool ACC>
+__global__ __launch_bounds__(kM4RowThreads) __attribute__((amdgpu_waves_per_eu(M4_ROWS2_WPE)))
+void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int N,
+              const v2d* __restrict__ tws, double* __restrict__ pw, int acc,
+              M4Top* __restrict__ top, int store) {
+  constexpr int N2 = C * D, P2 = m4_pitch(C * D);
+  static_assert(is_prime(D), "m4_rows2: the second stage emits a prime DFT's outputs");
+  static_assert(kM4RowThreads == 64 && D * kR2 <= 2 * 64 && 64 % kR2 == 0 && C * kR2 <= 64,
+                "m4_rows2: two stage-A passes, one stage-B pass per wave");
+  constexpr int LP = N2 + 1;   // plane pitch (doubles)
+  __shared__ double sp[kR2][LP];
   const int N1 = N / N2;
-  const int k1_0 = blockIdx.x * kM4T1;
+  const int k1_0 = blockIdx.x * kR2;
   const long row = blockIdx.y;
-  {   // the tile's loads all in flight at once (see m4_cols)
-    constexpr int kIt = (kM4T1 * N2 + kM4RowThreads - 1) / kM4RowThreads;
-    v2d xa[kIt];
+  const int t = threadIdx.x;
+  const v2d* Yt = Y + row * (long)N1 * P2 + (long)k1_0 * P2;
+  // ---- stage A: task (q, r) = (task / kR2, task % kR2), the C-point DFT over p of
+  // Y[k1_0 + r][D p + q], then W_N2^(q u).  One pass after the other, each pass's real
+  // parts into the plane as soon as they exist: only the imaginary parts stay live
+  // (the other waves of the CU hide the load latency)
+  constexpr int kTA = D * kR2, kItA = (kTA + 63) / 64;
+  double ai[kItA][C];
 #pragma unroll
-    for (int i = 0; i < kIt; i++) {
-      const int idx = threadIdx.x + i * kM4RowThreads;
-      const int r = idx / N2, n2 = idx % N2, k1 = k1_0 + r;
-      xa[i] = idx < kM4T1 * N2 && k1 < N1
-                  ? Y[row * (long)N1 * m4_pitch(N2) + (long)k1 * m4_pitch(N2) + n2]
-                  : (v2d){0.0, 0.0};
-    }
-#pragma unroll
-    for (int i = 0; i < kIt; i++) {
-      const int idx = threadIdx.x + i * kM4RowThreads;
-      if (idx < kM4T1 * N2) s[idx / N2][idx % N2] = xa[i];
-    }
-  }
-  __syncthreads();
-  for (int task = threadIdx.x; task < D * kM4T1; task += kM4RowThreads) {
-    const int q = task / kM4T1, r = task % kM4T1;
+  for (int it = 0; it < kItA; it++) {
+    const int task = t + 64 * it, q = task / kR2, r = task % kR2;
+    const bool ok = task < kTA && k1_0 + r < N1;
     v2d v[C];
 #pragma unroll
-    for (int p = 0; p < C; p++) v[p] = s[r][D * p + q];
+    for (int p = 0; p < C; p++) v[p] = ok ? Yt[(long)r * P2 + D * p + q] : (v2d){0.0, 0.0};
     dft<C>(v);
+    // W_N2^(q u) = (W_N2^q)^u by recurrence: one table load per task instead of C - 1
+    // (all hoisted, they doubled the pass's live registers); <= C roundings of drift
+    const v2d w1 = tws[q < D ? q : 0];
+    v2d wu = w1;
 #pragma unroll
-    for (int u = 1; u < C; u++) v[u] = cmul(v[u], tws[q * u]);   // W_N2^(q u), q u < N2
+    for (int u = 1; u < C; u++) {
+      v[u] = cmul(v[u], wu);
+      wu = cmul(wu, w1);
+    }
 #pragma unroll
-    for (int u = 0; u < C; u++) s[r][D * u + q] = v[u];
+    for (int u = 0; u < C; u++) {
+      if (task < kTA) sp[r][D * u + q] = v[u].x;
+      ai[it][u] = v[u].y;
+    }
+    // the next pass's loads and arithmetic stay behind this one (interleaving the two
+    // passes, the scheduler held both passes' working sets)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // ---- exchange, one plane at a time; stage B: task (u, r) = (t / kR2, t % kR2)
+  const int ub = t / kR2, rb = t % kR2;
+  const bool actB = ub < C && k1_0 + rb < N1;
+  v2d x[D];
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < D; w++) x[w].x = actB ? sp[rb][D * ub + w] : 0.0;
+  __syncthreads();   // the imaginary parts overwrite the plane
+#pragma unroll
+  for (int it = 0; it < kItA; it++) {
+    const int task = t + 64 * it, q = task / kR2, r = task % kR2;
+    if (task < kTA) {
+#pragma unroll
+      for (int u = 0; u < C; u++) sp[r][D * u + q] = ai[it][u];
+    }
   }
   __syncthreads();
-  for (int task = threadIdx.x; task < C * kM4T1; task += kM4RowThreads) {
-    const int u = task / kM4T1, r = task % kM4T1;
-    v2d v[D];
 #pragma unroll
-    for (int q = 0; q < D; q++) v[q] = s[r][D * u + q];
-    dft<D>(v);
-#pragma unroll
-    for (int w = 0; w < D; w++) s[r][D * u + w] = v[w];
-  }
-  __syncthreads();
+  for (int w = 0; w < D; w++) x[w].y = actB ? sp[rb][D * ub + w] : 0.0;
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- stage B: the D-point DFT; output w is element k2 = ub + C w of column k1
+  const int k1 = k1_0 + rb;
   const double sc = 1.0 / ((double)N * (double)N);
-  // MODE 3: a thread's elements all lie in column r = threadIdx.x % kM4T1, k2 ascending
-  static_assert(kM4RowThreads == 64 && 64 % kM4T1 == 0, "m4_rows: one wave, whole columns");
   double a1 = -1.0, a2 = -1.0;
   int ak = INT_MAX;
-  constexpr int kOt = (kM4T1 * N2 + kM4RowThreads - 1) / kM4RowThreads;
-  double prev[(MODE == 2 || MODE == 3) ? kOt : 1];
-  if constexpr (MODE == 2 || MODE == 3) {   // the running power sums, all loads in flight
-#pragma unroll
-    for (int i = 0; i < kOt; i++) {
-      const int idx = threadIdx.x + i * kM4RowThreads;
-      const int k2 = idx / kM4T1, k1 = k1_0 + idx % kM4T1;
-      prev[i] = acc && idx < kM4T1 * N2 && k1 < N1 ? pw[row * N + k1 + (long)N1 * k2] : 0.0;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < kOt; i++) {
-    const int idx = threadIdx.x + i * kM4RowThreads;
-    const int k2 = idx / kM4T1, r = idx % kM4T1, k1 = k1_0 + r;
-    if (idx >= kM4T1 * N2 || k1 >= N1) continue;
-    const v2d x = s[r][D * (k2 % C) + k2 / C];
-    const long d = (long)k1 + (long)N1 * k2;
+  auto emit = [&](int w, v2d v) {
+    if (!actB) return;
+    const long d = (long)k1 + (long)N1 * (ub + C * w);
     if constexpr (MODE == 2 || MODE == 3) {
-      const double q = fma(x.x, x.x, x.y * x.y) * sc;
+      const double q = fma(v.x, v.x, v.y * v.y) * sc;
       double* o = pw + row * N + d;
-      const double v = acc ? prev[i] + q : q;
-      if (MODE == 2 || store) *o = v;
-      if constexpr (MODE == 3) {
-        a2 = v > a1 ? a1 : fmax(a2, v);
-        ak = v > a1 ? (int)d : ak;   // strict: the first index of the thread's maximum
-        a1 = fmax(a1, v);
-      }
+      const double val = ACC ? *o + q : q;   // (ACC: the running sums of earlier blocks)
+      if (MODE == 2 || store) *o = val;
+      if constexpr (MODE == 3) top2_merge(a1, ak, a2, val, (int)d, -1.0);
     } else {
-      out[row * out_rs + d] = x;
+      out[row * out_rs + d] = v;
     }
-  }
+  };
+  dft_prime_emit<D, true>(x, emit);
   if constexpr (MODE == 3) {
+    // the column's C tasks sit in the lanes rb + kR2 u
 #pragma unroll
-    for (int o = kM4T1; o < 64; o <<= 1)
+    for (int o = kR2; o < 64; o <<= 1)
       top2_merge(a1, ak, a2, __shfl_xor(a1, o, 64), __shfl_xor(ak, o, 64), __shfl_xor(a2, o, 64));
-    const int k1 = k1_0 + (int)threadIdx.x;
-    if (threadIdx.x < kM4T1 && k1 < N1) top[row * N1 + k1] = M4Top{a1, a2, ak, 0};
+    if (t < kR2 && k1_0 + t < N1) top[row * N1 + k1_0 + t] = M4Top{a1, a2, ak, 0};
   }
 }
 
@@ -2248,10 +2267,14 @@ int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_r
   case I:                                                                                      \
     hipLaunchKernelGGL((m4_cols<A, B, MODE_IN>), dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows), \
                        dim3(kM4ColThreads), 0, c->stream, in, in_rs, Y, N, tw, tws1, cp);      \
-    hipLaunchKernelGGL((m4_rows<C, D, MODE_OUT>), dim3((A * B + kM4T1 - 1) / kM4T1, rows),     \
-                       dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
-                       acc,                                                                     \
-                       (M4Top*)c->d_m4top, store);                                              \
+    if (acc)                                                                                   \
+      hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, true>), dim3((A * B + kR2 - 1) / kR2, rows),   \
+                         dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
+                         acc, (M4Top*)c->d_m4top, store);                                      \
+    else                                                                                       \
+      hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, false>), dim3((A * B + kR2 - 1) / kR2, rows),  \
+                         dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
+                         acc, (M4Top*)c->d_m4top, store);                                      \
     break;
     M4_CASE(1, 7, 16, 11, 31)
     M4_CASE(2, 3, 16, 11, 31)
@@ -2298,7 +2321,7 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
   const int N = c->cfg.n_samples, P = c->mix_nr;
   const bool nc = mode == GNSSCORR_ACQ_NONCOHERENT;
   const int n_units = n_groups * n_bins * (nc ? 1 : n_blocks);
-  // four-step plans: the row statistics ride on the last block's m4_rows (per-column
+  // four-step plans: the row statistics ride on the last block's m4_rows2 (per-column
   // top-2; its power rows are then not stored) unless the window can hold two samples
   // of a column or the power rows are dumped
   const int N1 = c->m4 ? kM4Plans[c->m4][0] * kM4Plans[c->m4][1] : 0;
