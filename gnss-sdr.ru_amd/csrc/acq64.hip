@@ -1963,6 +1963,14 @@ int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, in
 #ifndef M4_RT
 #define M4_RT 64    // m4_rows2 threads
 #endif
+#ifndef M4_COLS2
+#define M4_COLS2 1   // 0: the column pass with its LDS round trips (m4_cols, A/B builds)
+#endif
+#if M4_COLS2
+#define M4_COLS_KERNEL m4_cols2
+#else
+#define M4_COLS_KERNEL m4_cols
+#endif
 constexpr int kM4ColThreads = M4_CT, kM4T2 = M4_T2, kM4RowThreads = M4_RT;
 // The intermediate rows Y[k1][n2] are stored at a pitch of N2 rounded up to whole
 // m4_cols tiles (kM4T2 columns = 256 B): every tile writes whole, aligned 128-byte
@@ -2077,6 +2085,87 @@ __global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__
   }
 }
 
+// The column pass without its first and last LDS round trips (round 6): the A-point
+// stage reads its inputs (or forms the correlation product) straight from global
+// memory -- a lane's task is (q, t), 64 lanes cover 4 values of q x 16 consecutive
+// columns, whole 256-byte runs -- and the B-point stage writes its outputs, times
+// W_N^(n2 k1), straight to Y.  The LDS holds only the exchange between the stages.
+template <int A, int B, int MODE>
+__global__ __launch_bounds__(kM4ColThreads) void m4_cols2(const v2d* __restrict__ in, int in_rs,
+                                                        v2d* __restrict__ out, int N,
+                                                        const v2d* __restrict__ tw,
+                                                        const v2d* __restrict__ tws, MixCorr cp) {
+  constexpr int N1 = A * B;
+  static_assert(kM4ColThreads % kM4T2 == 0, "m4_cols2: a lane keeps one column");
+  __shared__ v2d s[N1][kM4T2 + 1];
+  const int N2 = N / N1;
+  const int n2_0 = blockIdx.x * kM4T2;
+  const long row = blockIdx.y;
+  const int t = threadIdx.x % kM4T2, n2 = n2_0 + t;
+  const bool col = n2 < N2;
+  const v2d *Xr = nullptr, *Fr = nullptr;
+  int shift = 0;
+  if constexpr (MODE == 1) {
+    const int unit = cp.u0 + (int)row;
+    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
+    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
+    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
+    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
+    Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
+    Fr = cp.F + (long)cp.group_code[g] * cp.rs;
+    shift = fm.y;
+  }
+  // ---- stage A: task (q, t), q = (task / kM4T2) < B: the A-point DFT over p of
+  // x[B p + q], times W_N1^(q u), into LDS slot B u + q
+  constexpr int kLanesQ = kM4ColThreads / kM4T2;   // values of q per pass
+  constexpr int kItA = (B + kLanesQ - 1) / kLanesQ;
+#pragma unroll
+  for (int it = 0; it < kItA; it++) {
+    const int q = threadIdx.x / kM4T2 + kLanesQ * it;
+    if (q >= B) continue;
+    v2d v[A];
+#pragma unroll
+    for (int p = 0; p < A; p++) {
+      const int n = N2 * (B * p + q) + n2;
+      if constexpr (MODE == 1) {
+        int sx = n - shift;
+        sx += sx < 0 ? N : 0;
+        const v2d xv = col ? Xr[sx] : (v2d){0.0, 0.0}, f = col ? Fr[n] : (v2d){0.0, 0.0};
+        v[p] = (v2d){fma(xv.x, f.x, xv.y * f.y), fma(xv.x, f.y, -(xv.y * f.x))};   // conj(X) F
+      } else {
+        v[p] = col ? in[row * in_rs + n] : (v2d){0.0, 0.0};
+      }
+    }
+    dft<A>(v);
+#pragma unroll
+    for (int u = 1; u < A; u++) v[u] = cmul(v[u], tws[q * u]);   // W_N1^(q u), q u < N1
+#pragma unroll
+    for (int u = 0; u < A; u++) s[B * u + q][t] = v[u];
+  }
+  __syncthreads();
+  // ---- stage B: task (u, t), u = threadIdx.x / kM4T2 < A: the B-point DFT over q;
+  // output w is k1 = u + A w, times W_N^(n2 k1) = W_N^(n2 u) (W_N^(A n2))^w
+  constexpr int kItB = (A + kLanesQ - 1) / kLanesQ;
+#pragma unroll
+  for (int it = 0; it < kItB; it++) {
+    const int u = threadIdx.x / kM4T2 + kLanesQ * it;
+    if (u >= A) continue;
+    v2d v[B];
+#pragma unroll
+    for (int q = 0; q < B; q++) v[q] = s[B * u + q][t];
+    dft<B>(v);
+    if (col) {
+      v2d wc = tw[n2 * u], ws = tw[A * n2];   // n2 u < N, A n2 < N
+      const long base = row * (long)N1 * m4_pitch(N2) + n2;
+#pragma unroll
+      for (int w = 0; w < B; w++) {
+        out[base + (long)(u + A * w) * m4_pitch(N2)] = cmul(v[w], wc);
+        wc = cmul(wc, ws);
+      }
+    }
+  }
+}
+
 // Per-column top-2 of a power row (MODE 3 of m4_rows2): the column k1 holds the
 // samples k1 + N1 k2, N1 apart, so when 2 spc - 1 <= N1 the open window around the
 // row's argmax holds at most one of them and {a1, first index, runner-up} per column
@@ -2103,11 +2192,11 @@ __device__ __forceinline__ void top2_merge(double& a1, int& ak, double& a2, doub
 // stage goes through ONE fp64 plane at a time (real parts, then imaginary parts:
 // 4 x (N2 + 1) doubles, 10.9 KB), and the prime D-point stage emits its outputs as
 // they are formed (power, statistics or complex rows go out from registers, no LDS
-// round trip).  232 VGPRs: 8 waves per CU.  The arithmetic is m4_rows' except the
+// round trip).  164 VGPRs: 12 waves per CU.  The arithmetic is m4_rows' except the
 // stage-A twiddles (a recurrence, <= C roundings of drift).  38.192 Msps search
 // 1.14-1.15 -> 1.09-1.11 ms (profiles/r6/acq_generic_rows2_ab_r7b.log).
 #ifndef M4_ROWS2_WPE
-#define M4_ROWS2_WPE 2   // waves per SIMD of m4_rows2 (232 VGPRs; 3 spills ~70)
+#define M4_ROWS2_WPE 3   // waves per SIMD of m4_rows2 (164 VGPRs)
 #endif
 #ifndef M4_ROWS2_ROWS
 #define M4_ROWS2_ROWS 4   // rows k1 per m4_rows2 workgroup (2: 150 VGPRs, 12 waves per CU, but
@@ -2135,8 +2224,11 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
   // parts into the plane as soon as they exist: only the imaginary parts stay live
   // (the other waves of the CU hide the load latency)
   constexpr int kTA = D * kR2, kItA = (kTA + 63) / 64;
+  // the passes as a loop that is NOT unrolled: unrolled, the scheduler overlapped
+  // them (232 VGPRs, 2 waves per SIMD); as a loop, 164 VGPRs: 3 waves per SIMD
+  static_assert(kItA == 2, "m4_rows2: two stage-A passes");
   double ai[kItA][C];
-#pragma unroll
+#pragma unroll 1
   for (int it = 0; it < kItA; it++) {
     const int task = t + 64 * it, q = task / kR2, r = task % kR2;
     const bool ok = task < kTA && k1_0 + r < N1;
@@ -2156,7 +2248,8 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
 #pragma unroll
     for (int u = 0; u < C; u++) {
       if (task < kTA) sp[r][D * u + q] = v[u].x;
-      ai[it][u] = v[u].y;
+      if (it == 0) ai[0][u] = v[u].y;   // (constant register indices)
+      else ai[1][u] = v[u].y;
     }
     // the next pass's loads and arithmetic stay behind this one (interleaving the two
     // passes, the scheduler held both passes' working sets)
@@ -2265,7 +2358,7 @@ int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_r
   switch (c->m4) {
 #define M4_CASE(I, A, B, C, D)                                                                 \
   case I:                                                                                      \
-    hipLaunchKernelGGL((m4_cols<A, B, MODE_IN>), dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows), \
+    hipLaunchKernelGGL((M4_COLS_KERNEL<A, B, MODE_IN>), dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows), \
                        dim3(kM4ColThreads), 0, c->stream, in, in_rs, Y, N, tw, tws1, cp);      \
     if (acc)                                                                                   \
       hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, true>), dim3((A * B + kR2 - 1) / kR2, rows),   \
