@@ -2183,6 +2183,15 @@ __device__ __forceinline__ void top2_merge(double& a1, int& ak, double& a2, doub
   a1 = take ? b1 : a1;
 }
 
+// push one sample into (a1, ak, a2): top2_merge with b2 = -1, in 5 VALU operations
+// (a2 = max(a2, min(v, a1)) holds whether or not v takes the lead)
+__device__ __forceinline__ void top1_push(double& a1, int& ak, double& a2, double v, int k) {
+  const bool take = v > a1 || (v == a1 && k < ak);
+  a2 = fmax(a2, fmin(v, a1));
+  ak = take ? k : ak;
+  a1 = fmax(a1, v);
+}
+
 // m4_rows2 MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added
 // to the running sums when ACC); MODE 3: as 2 on a row's last block, per-column top-2
 // into top (pw written only when store)
@@ -2212,7 +2221,11 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
   static_assert(is_prime(D), "m4_rows2: the second stage emits a prime DFT's outputs");
   static_assert(kM4RowThreads == 64 && D * kR2 <= 2 * 64 && 64 % kR2 == 0 && C * kR2 <= 64,
                 "m4_rows2: two stage-A passes, one stage-B pass per wave");
-  constexpr int LP = N2 + 1;   // plane pitch (doubles)
+  // plane pitch (doubles): LP = 8 mod 32, so the 32 lanes of a half-wave (4 rows x 8
+  // consecutive q, or 4 rows x 8 values of u) fall on 32 distinct bank pairs (at
+  // N2 + 1 = 342 the rows overlapped: 44 % of the LDS cycles were bank conflicts)
+  constexpr int LP = N2 + 1 + ((8 - (N2 + 1)) % 32 + 32) % 32;
+  static_assert(LP % 32 == 8 && LP > N2, "m4_rows2: plane pitch");
   __shared__ double sp[kR2][LP];
   const int N1 = N / N2;
   const int k1_0 = blockIdx.x * kR2;
@@ -2289,7 +2302,7 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
       double* o = pw + row * N + d;
       const double val = ACC ? *o + q : q;   // (ACC: the running sums of earlier blocks)
       if (MODE == 2 || store) *o = val;
-      if constexpr (MODE == 3) top2_merge(a1, ak, a2, val, (int)d, -1.0);
+      if constexpr (MODE == 3) top1_push(a1, ak, a2, val, (int)d);
     } else {
       out[row * out_rs + d] = v;
     }
@@ -2419,8 +2432,11 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
   // of a column or the power rows are dumped
   const int N1 = c->m4 ? kM4Plans[c->m4][0] * kM4Plans[c->m4][1] : 0;
   const bool fused = c->m4 && c->d_m4top && 2 * spc - 1 <= N1 && !d_dump;
-  for (int u0 = 0; u0 < n_units; u0 += c->g_chunk) {
-    const int nu = n_units - u0 < c->g_chunk ? n_units - u0 : c->g_chunk;
+  // equal chunks (7 x 375 rows rather than 6 x 385 + 314 at the bench's 2 624)
+  const int n_ch = (n_units + c->g_chunk - 1) / c->g_chunk;
+  const int step = n_ch > 0 ? (n_units + n_ch - 1) / n_ch : c->g_chunk;
+  for (int u0 = 0; u0 < n_units; u0 += step) {
+    const int nu = n_units - u0 < step ? n_units - u0 : step;
     const int nb = nc ? n_blocks : 1;
     for (int b = 0; b < nb; b++) {
       MixCorr cp{(const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1,
@@ -2465,19 +2481,22 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
 
 int mx_init(gnsscorr_acq_ctx* c) {
   const long N = c->cfg.n_samples;
-  // ~256 MiB per work buffer: 439 rows per chunk at N = 38 192, so each pass launches
-  // ~10 k workgroups and a search takes 6 chunks (64 MiB: 25 chunks, 1.72 against 1.38
-  // ms per search, profiles/r5/acq_generic_chunk_ab_r5ao.log); GNSSCORR_ACQ_GCHUNK_MB:
-  // another size, for A/Bs
-  const char* gm = getenv("GNSSCORR_ACQ_GCHUNK_MB");
-  const long mb = gm && atol(gm) > 0 ? atol(gm) : 256;
-  c->g_chunk = (int)((mb << 20) / (N * 16));
-  c->g_chunk = chunk_cap(c, c->g_chunk);
-  HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
   // (the four-step plan's Y rows at the m4_pitch, a few % above N)
   const long ya = c->m4 ? (long)kM4Plans[c->m4][0] * kM4Plans[c->m4][1] *
                               m4_pitch((int)(N / (kM4Plans[c->m4][0] * kM4Plans[c->m4][1])))
                         : N;
+  // Rows per chunk from the work buffer's size.  Large chunks keep each pass at ~10 k
+  // workgroups (64 MiB: 25 chunks per search, 1.72 against 1.38 ms, round 5,
+  // profiles/r5/acq_generic_chunk_ab_r5ao.log).  The four-step plan's Y is written by
+  // m4_cols2 and read back at once by m4_rows2: at <= 232 MiB (385 rows at N = 38 192)
+  // it stays in the 256 MB memory-side cache between the two passes.  A sweep of the
+  // chunk size gave 0.963-0.965 ms at 242 MB of Y, 1.005 ms at 277 MB (the round-5 size)
+  // and 1.007-1.028 ms at 259 MB (profiles/r6/acq_generic_chunk_sweep_r7h.log).
+  // GNSSCORR_ACQ_GCHUNK_MB: another size in MiB, for A/Bs.
+  const char* gm = getenv("GNSSCORR_ACQ_GCHUNK_MB");
+  const long mb = gm && atol(gm) > 0 ? atol(gm) : (c->m4 ? 232 : 256);
+  c->g_chunk = chunk_cap(c, (int)((mb << 20) / (ya * 16)));
+  HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
   HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)ya * c->g_chunk));
   if (!c->m4)   // the four-step plan's passes need one work buffer (Y), the Stockham passes two
     HIP_TRY(hipMalloc(&c->d_gB, sizeof(double2) * (size_t)N * c->g_chunk));
