@@ -2219,8 +2219,8 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
               M4Top* __restrict__ top, int store) {
   constexpr int N2 = C * D, P2 = m4_pitch(C * D);
   static_assert(is_prime(D), "m4_rows2: the second stage emits a prime DFT's outputs");
-  static_assert(kM4RowThreads == 64 && D * kR2 <= 2 * 64 && 64 % kR2 == 0 && C * kR2 <= 64,
-                "m4_rows2: two stage-A passes, one stage-B pass per wave");
+  static_assert(kM4RowThreads == 64 && D * kR2 <= 3 * 64 && C * kR2 <= 64,
+                "m4_rows2: up to three stage-A passes, one stage-B pass per wave");
   // plane pitch (doubles): LP = 8 mod 32, so the 32 lanes of a half-wave (4 rows x 8
   // consecutive q, or 4 rows x 8 values of u) fall on 32 distinct bank pairs (at
   // N2 + 1 = 342 the rows overlapped: 44 % of the LDS cycles were bank conflicts)
@@ -2239,7 +2239,6 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
   constexpr int kTA = D * kR2, kItA = (kTA + 63) / 64;
   // the passes as a loop that is NOT unrolled: unrolled, the scheduler overlapped
   // them (232 VGPRs, 2 waves per SIMD); as a loop, 164 VGPRs: 3 waves per SIMD
-  static_assert(kItA == 2, "m4_rows2: two stage-A passes");
   double ai[kItA][C];
 #pragma unroll 1
   for (int it = 0; it < kItA; it++) {
@@ -2261,8 +2260,9 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
 #pragma unroll
     for (int u = 0; u < C; u++) {
       if (task < kTA) sp[r][D * u + q] = v[u].x;
-      if (it == 0) ai[0][u] = v[u].y;   // (constant register indices)
-      else ai[1][u] = v[u].y;
+      if (it == 0) ai[0][u] = v[u].y;   // (constant register indices: uniform branches)
+      else if (kItA < 3 || it == 1) ai[kItA > 1 ? 1 : 0][u] = v[u].y;
+      else ai[kItA - 1][u] = v[u].y;
     }
     // the next pass's loads and arithmetic stay behind this one (interleaving the two
     // passes, the scheduler held both passes' working sets)
@@ -2309,10 +2309,14 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
   };
   dft_prime_emit<D, true>(x, emit);
   if constexpr (MODE == 3) {
-    // the column's C tasks sit in the lanes rb + kR2 u
+    // the column's C tasks sit in the lanes rb + kR2 u: a tree over u (step s merges
+    // the disjoint lane ranges [u, u + s) and [u + s, u + 2 s) within the column)
 #pragma unroll
-    for (int o = kR2; o < 64; o <<= 1)
-      top2_merge(a1, ak, a2, __shfl_xor(a1, o, 64), __shfl_xor(ak, o, 64), __shfl_xor(a2, o, 64));
+    for (int st = 1; st < C; st <<= 1) {
+      const double b1 = __shfl_down(a1, kR2 * st, 64), b2 = __shfl_down(a2, kR2 * st, 64);
+      const int bk = __shfl_down(ak, kR2 * st, 64);
+      if (ub + st < C) top2_merge(a1, ak, a2, b1, bk, b2);
+    }
     if (t < kR2 && k1_0 + t < N1) top[row * N1 + k1_0 + t] = M4Top{a1, a2, ak, 0};
   }
 }
