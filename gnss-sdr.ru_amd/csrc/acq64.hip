@@ -1946,7 +1946,7 @@ int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, in
 // ---------------------------------------------------------------------------------
 // Four-step plan (round 5): N = N1 N2 with N1 = A B and N2 = C D, each a pair of
 // compiled radices.  X[k1 + N1 k2] = sum_n2 W_N2^(n2 k2) W_N^(n2 k1) sum_n1
-// W_N1^(n1 k1) x[N2 n1 + n2].  m4_cols runs the N1-point DFTs of a tile of kM4T2
+// W_N1^(n1 k1) x[N2 n1 + n2].  m4_cols2 runs the N1-point DFTs of a tile of kM4T2
 // columns n2 in LDS (A-point DFTs, twiddle W_N1^(q u), B-point DFTs: the standard
 // two-factor split), multiplies by W_N^(n2 k1) and writes Y[k1 N2 + n2]; m4_rows
 // (m4_rows2) runs the N2-point DFTs of kR2 rows k1 the same way and writes X[k1 + N1 k2].
@@ -1955,216 +1955,33 @@ int mx_launch(gnsscorr_acq_ctx* c, int R, const v2d* in, int in_rs, v2d* out, in
 // N^2 in the second (acquisition.sci:107-132), as in mx_pass.
 // ---------------------------------------------------------------------------------
 #ifndef M4_CT
-#define M4_CT 128   // m4_cols threads
+#define M4_CT 128   // m4_cols2 threads
 #endif
 #ifndef M4_T2
-#define M4_T2 16    // m4_cols: columns n2 per workgroup
+#define M4_T2 16    // m4_cols2: columns n2 per workgroup
 #endif
 #ifndef M4_RT
 #define M4_RT 64    // m4_rows2 threads
 #endif
-#ifndef M4_COLS2
-#define M4_COLS2 1   // 0: the column pass with its LDS round trips (m4_cols, A/B builds)
+#ifndef M4_COLS2_PLANE
+#define M4_COLS2_PLANE 1   // m4_cols2: exchange through one fp64 plane at a time (0: complex)
 #endif
-#if M4_COLS2
-#define M4_COLS_KERNEL m4_cols2
+#ifndef M4_COLS2_WPE
+#define M4_COLS2_WPE 4     // m4_cols2: waves per SIMD the allocator is held to (0: free)
+#endif
+#if M4_COLS2_WPE
+#define M4_COLS2_ATTR __attribute__((amdgpu_waves_per_eu(M4_COLS2_WPE)))
 #else
-#define M4_COLS_KERNEL m4_cols
+#define M4_COLS2_ATTR
 #endif
 constexpr int kM4ColThreads = M4_CT, kM4T2 = M4_T2, kM4RowThreads = M4_RT;
 // The intermediate rows Y[k1][n2] are stored at a pitch of N2 rounded up to whole
-// m4_cols tiles (kM4T2 columns = 256 B): every tile writes whole, aligned 128-byte
+// m4_cols2 tiles (kM4T2 columns = 256 B): every tile writes whole, aligned 128-byte
 // lines that no other workgroup touches (at the natural pitch N2 = 341 a tile's
 // 256-byte runs straddled three lines shared with the neighbouring tiles, which run
 // on other XCDs)
 __host__ __device__ constexpr int m4_pitch(int n2) { return (n2 + kM4T2 - 1) / kM4T2 * kM4T2; }
 
-// MODE 0: rows in (stride in_rs); MODE 1: the correlation product of unit u0 + row
-template <int A, int B, int MODE>
-// tws: W_N1^j, j < N1 (the inner twiddles, a compact L1-resident table)
-__global__ __launch_bounds__(kM4ColThreads) void m4_cols(const v2d* __restrict__ in, int in_rs,
-                                                       v2d* __restrict__ out, int N,
-                                                       const v2d* __restrict__ tw,
-                                                       const v2d* __restrict__ tws, MixCorr cp) {
-  constexpr int N1 = A * B;
-  __shared__ v2d s[N1][kM4T2 + 1];
-  const int N2 = N / N1;
-  const int n2_0 = blockIdx.x * kM4T2;
-  const long row = blockIdx.y;
-  const v2d *Xr = nullptr, *Fr = nullptr;
-  int shift = 0;
-  if constexpr (MODE == 1) {
-    const int unit = cp.u0 + (int)row;
-    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
-    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
-    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
-    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
-    Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
-    Fr = cp.F + (long)cp.group_code[g] * cp.rs;
-    shift = fm.y;
-  }
-  // the tile's loads all issued before the first use (a compile-time trip count): a
-  // run-time loop waits one full memory latency per element
-  constexpr int kIt = (N1 * kM4T2 + kM4ColThreads - 1) / kM4ColThreads;
-  v2d xa[kIt], xb[kIt];
-#pragma unroll
-  for (int i = 0; i < kIt; i++) {
-    const int idx = threadIdx.x + i * kM4ColThreads;
-    const int n1 = idx / kM4T2, t = idx % kM4T2, n2 = n2_0 + t;
-    xa[i] = xb[i] = (v2d){0.0, 0.0};
-    if (idx < N1 * kM4T2 && n2 < N2) {
-      const int n = N2 * n1 + n2;
-      if constexpr (MODE == 1) {
-        int sx = n - shift;
-        sx += sx < 0 ? N : 0;
-        xa[i] = Xr[sx];
-        xb[i] = Fr[n];
-      } else {
-        xa[i] = in[row * in_rs + n];
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < kIt; i++) {
-    const int idx = threadIdx.x + i * kM4ColThreads;
-    if (idx < N1 * kM4T2) {
-      v2d x = xa[i];
-      if constexpr (MODE == 1) {
-        const v2d xv = xa[i], f = xb[i];
-        x = (v2d){fma(xv.x, f.x, xv.y * f.y), fma(xv.x, f.y, -(xv.y * f.x))};   // conj(X) F
-      }
-      s[idx / kM4T2][idx % kM4T2] = x;
-    }
-  }
-  __syncthreads();
-  // A-point DFTs over p of x[B p + q], times W_N1^(q u), back into the same slots
-  for (int task = threadIdx.x; task < B * kM4T2; task += kM4ColThreads) {
-    const int q = task / kM4T2, t = task % kM4T2;
-    v2d v[A];
-#pragma unroll
-    for (int p = 0; p < A; p++) v[p] = s[B * p + q][t];
-    dft<A>(v);
-#pragma unroll
-    for (int u = 1; u < A; u++) v[u] = cmul(v[u], tws[q * u]);   // W_N1^(q u), q u < N1
-#pragma unroll
-    for (int u = 0; u < A; u++) s[B * u + q][t] = v[u];
-  }
-  __syncthreads();
-  // B-point DFTs over q: X[u + A v] into slot B u + v
-  for (int task = threadIdx.x; task < A * kM4T2; task += kM4ColThreads) {
-    const int u = task / kM4T2, t = task % kM4T2;
-    v2d v[B];
-#pragma unroll
-    for (int q = 0; q < B; q++) v[q] = s[B * u + q][t];
-    dft<B>(v);
-#pragma unroll
-    for (int w = 0; w < B; w++) s[B * u + w][t] = v[w];
-  }
-  __syncthreads();
-  // W_N^(n2 k1): a thread's slots i have one column n2 and k1 = k1_0 + kStep i, so
-  // two table loads (W_N^(n2 k1_0) and the step W_N^(kStep n2)) and a recurrence,
-  // instead of one scattered load from the N-entry table per output (a third of the
-  // pass's loads); ~kIt ulp of rounding drift in the twiddles
-  static_assert(kM4ColThreads % kM4T2 == 0, "m4_cols: a thread keeps one column");
-  constexpr int kStep = kM4ColThreads / kM4T2;
-  const int t0 = threadIdx.x % kM4T2, n2t = n2_0 + t0, k10 = threadIdx.x / kM4T2;
-  v2d wc = (v2d){1.0, 0.0}, ws = (v2d){1.0, 0.0};
-  if (n2t < N2) {
-    wc = tw[n2t * k10];
-    ws = tw[kStep * n2t];
-  }
-#pragma unroll
-  for (int i = 0; i < kIt; i++) {
-    const int idx = threadIdx.x + i * kM4ColThreads;
-    const int k1 = idx / kM4T2;
-    if (idx < N1 * kM4T2 && n2t < N2) {
-      const v2d x = s[B * (k1 % A) + k1 / A][t0];
-      out[row * (long)N1 * m4_pitch(N2) + (long)k1 * m4_pitch(N2) + n2t] = cmul(x, wc);
-    }
-    wc = cmul(wc, ws);
-  }
-}
-
-// The column pass without its first and last LDS round trips (round 6): the A-point
-// stage reads its inputs (or forms the correlation product) straight from global
-// memory -- a lane's task is (q, t), 64 lanes cover 4 values of q x 16 consecutive
-// columns, whole 256-byte runs -- and the B-point stage writes its outputs, times
-// W_N^(n2 k1), straight to Y.  The LDS holds only the exchange between the stages.
-template <int A, int B, int MODE>
-__global__ __launch_bounds__(kM4ColThreads) void m4_cols2(const v2d* __restrict__ in, int in_rs,
-                                                        v2d* __restrict__ out, int N,
-                                                        const v2d* __restrict__ tw,
-                                                        const v2d* __restrict__ tws, MixCorr cp) {
-  constexpr int N1 = A * B;
-  static_assert(kM4ColThreads % kM4T2 == 0, "m4_cols2: a lane keeps one column");
-  __shared__ v2d s[N1][kM4T2 + 1];
-  const int N2 = N / N1;
-  const int n2_0 = blockIdx.x * kM4T2;
-  const long row = blockIdx.y;
-  const int t = threadIdx.x % kM4T2, n2 = n2_0 + t;
-  const bool col = n2 < N2;
-  const v2d *Xr = nullptr, *Fr = nullptr;
-  int shift = 0;
-  if constexpr (MODE == 1) {
-    const int unit = cp.u0 + (int)row;
-    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
-    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
-    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
-    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
-    Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
-    Fr = cp.F + (long)cp.group_code[g] * cp.rs;
-    shift = fm.y;
-  }
-  // ---- stage A: task (q, t), q = (task / kM4T2) < B: the A-point DFT over p of
-  // x[B p + q], times W_N1^(q u), into LDS slot B u + q
-  constexpr int kLanesQ = kM4ColThreads / kM4T2;   // values of q per pass
-  constexpr int kItA = (B + kLanesQ - 1) / kLanesQ;
-#pragma unroll
-  for (int it = 0; it < kItA; it++) {
-    const int q = threadIdx.x / kM4T2 + kLanesQ * it;
-    if (q >= B) continue;
-    v2d v[A];
-#pragma unroll
-    for (int p = 0; p < A; p++) {
-      const int n = N2 * (B * p + q) + n2;
-      if constexpr (MODE == 1) {
-        int sx = n - shift;
-        sx += sx < 0 ? N : 0;
-        const v2d xv = col ? Xr[sx] : (v2d){0.0, 0.0}, f = col ? Fr[n] : (v2d){0.0, 0.0};
-        v[p] = (v2d){fma(xv.x, f.x, xv.y * f.y), fma(xv.x, f.y, -(xv.y * f.x))};   // conj(X) F
-      } else {
-        v[p] = col ? in[row * in_rs + n] : (v2d){0.0, 0.0};
-      }
-    }
-    dft<A>(v);
-#pragma unroll
-    for (int u = 1; u < A; u++) v[u] = cmul(v[u], tws[q * u]);   // W_N1^(q u), q u < N1
-#pragma unroll
-    for (int u = 0; u < A; u++) s[B * u + q][t] = v[u];
-  }
-  __syncthreads();
-  // ---- stage B: task (u, t), u = threadIdx.x / kM4T2 < A: the B-point DFT over q;
-  // output w is k1 = u + A w, times W_N^(n2 k1) = W_N^(n2 u) (W_N^(A n2))^w
-  constexpr int kItB = (A + kLanesQ - 1) / kLanesQ;
-#pragma unroll
-  for (int it = 0; it < kItB; it++) {
-    const int u = threadIdx.x / kM4T2 + kLanesQ * it;
-    if (u >= A) continue;
-    v2d v[B];
-#pragma unroll
-    for (int q = 0; q < B; q++) v[q] = s[B * u + q][t];
-    dft<B>(v);
-    if (col) {
-      v2d wc = tw[n2 * u], ws = tw[A * n2];   // n2 u < N, A n2 < N
-      const long base = row * (long)N1 * m4_pitch(N2) + n2;
-#pragma unroll
-      for (int w = 0; w < B; w++) {
-        out[base + (long)(u + A * w) * m4_pitch(N2)] = cmul(v[w], wc);
-        wc = cmul(wc, ws);
-      }
-    }
-  }
-}
 
 // Per-column top-2 of a power row (MODE 3 of m4_rows2): the column k1 holds the
 // samples k1 + N1 k2, N1 apart, so when 2 spc - 1 <= N1 the open window around the
@@ -2190,6 +2007,188 @@ __device__ __forceinline__ void top1_push(double& a1, int& ak, double& a2, doubl
   a2 = fmax(a2, fmin(v, a1));
   ak = take ? k : ak;
   a1 = fmax(a1, v);
+}
+
+// one wave: the statistics of unit u0 + r from its per-column top-2 rows
+__device__ __forceinline__ void m4_stats_row(const M4Top* __restrict__ top, int r, int N1, int N,
+                                             int u0, int n_blocks, int nc, int spc,
+                                             gnsscorr_acq_row* __restrict__ stats) {
+  const int lane = threadIdx.x % 64;
+  const int unit = u0 + r;
+  const M4Top* t = top + (long)r * N1;
+  const int rowid = nc ? unit : unit / n_blocks;
+  const int blk0 = nc ? 0 : unit % n_blocks;
+  double bv = -1.0;
+  int bk = INT_MAX;
+  for (int c = lane; c < N1; c += 64)
+    if (better(t[c].a1, t[c].ak, bv, bk)) { bv = t[c].a1; bk = t[c].ak; }
+  wave_argmax(bv, bk);
+  double sv = -1.0;
+  for (int c = lane; c < N1; c += 64) {
+    int d = t[c].ak - bk;
+    d += d < 0 ? N : 0;
+    sv = fmax(sv, (d >= spc && d <= N - spc) ? t[c].a1 : t[c].a2);
+  }
+  sv = wave_max(sv);
+  if (lane == 0) {
+    gnsscorr_acq_row o;
+    o.peak = bv;
+    o.second = sv;
+    o.argmax = bk;
+    o.block = nc ? -1 : blk0;
+    stats[(long)rowid * n_blocks + blk0] = o;
+  }
+}
+
+__global__ __launch_bounds__(64) void m4_stats_kernel(const M4Top* __restrict__ top, int N1,
+                                                      int N, int u0, int n_blocks, int nc,
+                                                      int spc,
+                                                      gnsscorr_acq_row* __restrict__ stats) {
+  m4_stats_row(top, blockIdx.x, N1, N, u0, n_blocks, nc, spc, stats);
+}
+
+// A chunk's statistics pass carried by the next chunk's first m4_cols2 launch: extra
+// rows of workgroups (one statistics row per wave) after the main grid.  Stream order
+// puts them after the chunk's last m4_rows2 (which wrote top) and before the next
+// chunk's (which overwrites it); it saves one launch and its tail per chunk.
+struct M4StatsJob {
+  const M4Top* top = nullptr;
+  gnsscorr_acq_row* stats = nullptr;
+  int n = 0, u0 = 0, N1 = 0, n_blocks = 1, nc = 0, spc = 0;
+  int main_rows = 0;   // the launch's own rows (blockIdx.y below: the column pass)
+};
+
+// The column pass without its first and last LDS round trips (round 6): the A-point
+// stage reads its inputs (or forms the correlation product) straight from global
+// memory -- a lane's task is (q, t), 64 lanes cover 4 values of q x 16 consecutive
+// columns, whole 256-byte runs -- and the B-point stage writes its outputs, times
+// W_N^(n2 k1), straight to Y.  The LDS holds only the exchange between the stages, one
+// fp64 plane at a time (real parts, then imaginary parts: 15.2 KB per tile, 126 VGPRs,
+// 16 waves per CU; complex, 30.5 KB held it to 10).
+template <int A, int B, int MODE>
+__global__ __launch_bounds__(kM4ColThreads) M4_COLS2_ATTR void m4_cols2(const v2d* __restrict__ in, int in_rs,
+                                                        v2d* __restrict__ out, int N,
+                                                        const v2d* __restrict__ tw,
+                                                        const v2d* __restrict__ tws, MixCorr cp,
+                                                        M4StatsJob sj) {
+  constexpr int N1 = A * B;
+  static_assert(kM4ColThreads % kM4T2 == 0, "m4_cols2: a lane keeps one column");
+  if ((int)blockIdx.y >= sj.main_rows) {   // the previous chunk's statistics (whole workgroups)
+    const int r = (((int)blockIdx.y - sj.main_rows) * (int)gridDim.x + (int)blockIdx.x) *
+                      (kM4ColThreads / 64) + (int)threadIdx.x / 64;
+    if (r < sj.n) m4_stats_row(sj.top, r, sj.N1, N, sj.u0, sj.n_blocks, sj.nc, sj.spc, sj.stats);
+    return;
+  }
+#if M4_COLS2_PLANE
+  __shared__ double sp[N1][kM4T2 + 1];   // one fp64 plane: real parts, then imaginary
+#else
+  __shared__ v2d s[N1][kM4T2 + 1];
+#endif
+  const int N2 = N / N1;
+  const int n2_0 = blockIdx.x * kM4T2;
+  const long row = blockIdx.y;
+  const int t = threadIdx.x % kM4T2, n2 = n2_0 + t;
+  const bool col = n2 < N2;
+  const v2d *Xr = nullptr, *Fr = nullptr;
+  int shift = 0;
+  if constexpr (MODE == 1) {
+    const int unit = cp.u0 + (int)row;
+    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
+    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
+    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
+    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
+    Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
+    Fr = cp.F + (long)cp.group_code[g] * cp.rs;
+    shift = fm.y;
+  }
+  // ---- stage A: task (q, t), q = (task / kM4T2) < B: the A-point DFT over p of
+  // x[B p + q], times W_N1^(q u), into LDS slot B u + q
+  constexpr int kLanesQ = kM4ColThreads / kM4T2;   // values of q per pass
+  constexpr int kItA = (B + kLanesQ - 1) / kLanesQ;
+#if M4_COLS2_PLANE
+  double ai[kItA][A];
+#endif
+#pragma unroll
+  for (int it = 0; it < kItA; it++) {
+    const int q = threadIdx.x / kM4T2 + kLanesQ * it;
+    if (q >= B) continue;
+    v2d v[A];
+#pragma unroll
+    for (int p = 0; p < A; p++) {
+      const int n = N2 * (B * p + q) + n2;
+      if constexpr (MODE == 1) {
+        int sx = n - shift;
+        sx += sx < 0 ? N : 0;
+        const v2d xv = col ? Xr[sx] : (v2d){0.0, 0.0}, f = col ? Fr[n] : (v2d){0.0, 0.0};
+        v[p] = (v2d){fma(xv.x, f.x, xv.y * f.y), fma(xv.x, f.y, -(xv.y * f.x))};   // conj(X) F
+      } else {
+        v[p] = col ? in[row * in_rs + n] : (v2d){0.0, 0.0};
+      }
+    }
+    dft<A>(v);
+#pragma unroll
+    for (int u = 1; u < A; u++) v[u] = cmul(v[u], tws[q * u]);   // W_N1^(q u), q u < N1
+#if M4_COLS2_PLANE
+#pragma unroll
+    for (int u = 0; u < A; u++) {
+      sp[B * u + q][t] = v[u].x;
+      ai[it][u] = v[u].y;
+    }
+#else
+#pragma unroll
+    for (int u = 0; u < A; u++) s[B * u + q][t] = v[u];
+#endif
+  }
+  __syncthreads();
+  // ---- stage B: task (u, t), u = threadIdx.x / kM4T2 < A: the B-point DFT over q;
+  // output w is k1 = u + A w, times W_N^(n2 k1) = W_N^(n2 u) (W_N^(A n2))^w
+  constexpr int kItB = (A + kLanesQ - 1) / kLanesQ;
+#if M4_COLS2_PLANE
+  static_assert(kItB == 1, "m4_cols2: one B-point pass (the plane exchange)");
+  v2d vb[B];
+  {
+    const int u = threadIdx.x / kM4T2;
+#pragma unroll
+    for (int q = 0; q < B; q++) vb[q].x = u < A ? sp[B * u + q][t] : 0.0;
+  }
+  __syncthreads();   // the imaginary parts overwrite the plane
+#pragma unroll
+  for (int it = 0; it < kItA; it++) {
+    const int q = threadIdx.x / kM4T2 + kLanesQ * it;
+    if (q < B) {
+#pragma unroll
+      for (int u = 0; u < A; u++) sp[B * u + q][t] = ai[it][u];
+    }
+  }
+  __syncthreads();
+  {
+    const int u = threadIdx.x / kM4T2;
+#pragma unroll
+    for (int q = 0; q < B; q++) vb[q].y = u < A ? sp[B * u + q][t] : 0.0;
+  }
+#endif
+#pragma unroll
+  for (int it = 0; it < kItB; it++) {
+    const int u = threadIdx.x / kM4T2 + kLanesQ * it;
+    if (u >= A) continue;
+#if M4_COLS2_PLANE
+    v2d (&v)[B] = vb;
+#else
+    v2d v[B];
+#pragma unroll
+    for (int q = 0; q < B; q++) v[q] = s[B * u + q][t];
+#endif
+    dft<B>(v);
+    if (col) {
+      v2d wc = tw[n2 * u], ws = tw[A * n2];   // n2 u < N, A n2 < N
+      const long base = row * (long)N1 * m4_pitch(N2) + n2;
+#pragma unroll
+      for (int w = 0; w < B; w++) {
+        out[base + (long)(u + A * w) * m4_pitch(N2)] = cmul(v[w], wc);
+        wc = cmul(wc, ws);
+      }
+    }
+  }
 }
 
 // m4_rows2 MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added
@@ -2325,35 +2324,6 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
 // columns, then the second peak as the maximum of each column's a1 when its argmax lies
 // outside the open circular window (argmax - spc, argmax + spc), else its runner-up.
 // Same results as g_stats1_kernel on the power rows.
-__global__ __launch_bounds__(64) void m4_stats_kernel(const M4Top* __restrict__ top, int N1,
-                                                      int N, int u0, int n_blocks, int nc,
-                                                      int spc,
-                                                      gnsscorr_acq_row* __restrict__ stats) {
-  const int unit = u0 + blockIdx.x;
-  const M4Top* t = top + (long)blockIdx.x * N1;
-  const int rowid = nc ? unit : unit / n_blocks;
-  const int blk0 = nc ? 0 : unit % n_blocks;
-  double bv = -1.0;
-  int bk = INT_MAX;
-  for (int c = threadIdx.x; c < N1; c += 64)
-    if (better(t[c].a1, t[c].ak, bv, bk)) { bv = t[c].a1; bk = t[c].ak; }
-  wave_argmax(bv, bk);
-  double sv = -1.0;
-  for (int c = threadIdx.x; c < N1; c += 64) {
-    int d = t[c].ak - bk;
-    d += d < 0 ? N : 0;
-    sv = fmax(sv, (d >= spc && d <= N - spc) ? t[c].a1 : t[c].a2);
-  }
-  sv = wave_max(sv);
-  if (threadIdx.x == 0) {
-    gnsscorr_acq_row r;
-    r.peak = bv;
-    r.second = sv;
-    r.argmax = bk;
-    r.block = nc ? -1 : blk0;
-    stats[(long)rowid * n_blocks + blk0] = r;
-  }
-}
 
 // the compiled four-step plans: {A, B, C, D}
 constexpr int kM4Plans[][4] = {{0, 0, 0, 0}, {7, 16, 11, 31}, {3, 16, 11, 31}};
@@ -2367,16 +2337,23 @@ int m4_plan(int N) {
 // rows [src] -> DFT rows or the correlation's power rows, one chunk of `rows`
 template <int MODE_IN, int MODE_OUT>
 int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_rs, int rows,
-              const MixCorr& cp, double* pw, int acc, int store = 1) {
+              const MixCorr& cp, double* pw, int acc, int store = 1,
+              const M4StatsJob* stats_job = nullptr) {
   const int N = c->cfg.n_samples;
+  M4StatsJob sj = stats_job ? *stats_job : M4StatsJob{};
+  sj.main_rows = rows;
+  const int per_y = (N / (kM4Plans[c->m4][0] * kM4Plans[c->m4][1]) + kM4T2 - 1) / kM4T2 *
+                    (kM4ColThreads / 64);   // statistics rows per extra grid row
+  const int ey = sj.n > 0 ? (sj.n + per_y - 1) / per_y : 0;
   const v2d* tw = (const v2d*)c->d_twN;
   const v2d* tws1 = (const v2d*)c->d_twm4;   // W_N1^j, then W_N2^j from + N1
   v2d* Y = (v2d*)c->d_gA;
   switch (c->m4) {
 #define M4_CASE(I, A, B, C, D)                                                                 \
   case I:                                                                                      \
-    hipLaunchKernelGGL((M4_COLS_KERNEL<A, B, MODE_IN>), dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows), \
-                       dim3(kM4ColThreads), 0, c->stream, in, in_rs, Y, N, tw, tws1, cp);      \
+    hipLaunchKernelGGL((m4_cols2<A, B, MODE_IN>),                                              \
+                       dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows + ey), dim3(kM4ColThreads), \
+                       0, c->stream, in, in_rs, Y, N, tw, tws1, cp, sj);                       \
     if (acc)                                                                                   \
       hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, true>), dim3((A * B + kR2 - 1) / kR2, rows),   \
                          dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
@@ -2439,6 +2416,7 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
   // equal chunks (7 x 375 rows rather than 6 x 385 + 314 at the bench's 2 624)
   const int n_ch = (n_units + c->g_chunk - 1) / c->g_chunk;
   const int step = n_ch > 0 ? (n_units + n_ch - 1) / n_ch : c->g_chunk;
+  M4StatsJob pend;   // fused statistics of the previous chunk, not yet launched
   for (int u0 = 0; u0 < n_units; u0 += step) {
     const int nu = n_units - u0 < step ? n_units - u0 : step;
     const int nb = nc ? n_blocks : 1;
@@ -2446,10 +2424,13 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
       MixCorr cp{(const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1,
                  n_bins, u0, d_gcode, d_gfreq, (const int2*)c->d_fmap64};
       if (c->m4) {
-        const int rc = fused && b == nb - 1
-                           ? m4_launch<1, 3>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, 0)
-                           : m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0);
+        const M4StatsJob* sj = b == 0 && pend.n > 0 ? &pend : nullptr;
+        const int rc =
+            fused && b == nb - 1
+                ? m4_launch<1, 3>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, 0, sj)
+                : m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, 1, sj);
         if (rc) return rc;
+        if (sj) pend.n = 0;
         continue;
       }
       v2d *A = (v2d*)c->d_gA, *B = (v2d*)c->d_gB;
@@ -2466,10 +2447,15 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
         Ns *= c->mix_r[i];
       }
     }
-    if (fused) {
-      hipLaunchKernelGGL(m4_stats_kernel, dim3(nu), dim3(64), 0, c->stream,
-                         (const M4Top*)c->d_m4top, N1, N, u0, n_blocks, (int)nc, spc,
-                         c->d_stats);
+    if (fused) {   // carried by the next chunk's first column pass, or launched below
+      pend.top = (const M4Top*)c->d_m4top;
+      pend.stats = c->d_stats;
+      pend.n = nu;
+      pend.u0 = u0;
+      pend.N1 = N1;
+      pend.n_blocks = n_blocks;
+      pend.nc = (int)nc;
+      pend.spc = spc;
     } else if (stats1_exact(N, spc))
       hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, c->stream,
                          (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
@@ -2478,6 +2464,11 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
       hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
                          (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
                          d_dump, dump_block);
+    HIP_TRY(hipGetLastError());
+  }
+  if (pend.n > 0) {   // the last chunk's statistics
+    hipLaunchKernelGGL(m4_stats_kernel, dim3(pend.n), dim3(64), 0, c->stream, pend.top, N1, N,
+                       pend.u0, n_blocks, (int)nc, spc, c->d_stats);
     HIP_TRY(hipGetLastError());
   }
   return GNSSCORR_OK;

@@ -1,10 +1,10 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r7k
+O=gpurun_out/r7m
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py tests/test_acq_prn_codes_gpu.py tests/test_acq_16m_gpu.py -q -x --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 tail -1 $O/pytest.log
-GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_rows5.so timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py -q -x --timeout 200 --timeout-method thread > $O/pytest_rows5.log 2>&1
-tail -1 $O/pytest_rows5.log
-bash tools/gpu_acq_ab.sh r7k "base rows5" "acq_generic" 3 0 | tee $O/ab.log
+GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_fplane.so timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py tests/test_acq_prn_codes_gpu.py tests/test_acq_16m_gpu.py -q -x --timeout 200 --timeout-method thread > $O/pytest_fplane.log 2>&1
+tail -1 $O/pytest_fplane.log
+bash tools/gpu_acq_ab.sh r7m "base fplane prev" "acq_generic" 3 0 | tee $O/ab.log
