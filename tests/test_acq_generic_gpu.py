@@ -162,7 +162,7 @@ def test_mixed_radix_equals_bluestein(gpu, fs, monkeypatch):
 @pytest.mark.parametrize("mode", ["best", "noncoherent"])
 @pytest.mark.parametrize("fs,generic", [(38.192e6, "0"), (16.368e6, "1")])
 def test_four_step_equals_mixed_radix_passes(gpu, fs, generic, mode, monkeypatch):
-    """The four-step plan (m4_cols / m4_rows: 112 x 341 at 38.192 Msps, 48 x 341 at
+    """The four-step plan (m4_cols2 / m4_rows2: 112 x 341 at 38.192 Msps, 48 x 341 at
     16.368 Msps on the generic engine) against the four mixed-radix passes
     (GNSSCORR_ACQ_MIX4=0) on one search: decisions identical, peaks and second
     peaks within 1e-9 relative (both fp64 DFTs of the same rows)."""
@@ -192,7 +192,7 @@ def test_four_step_equals_mixed_radix_passes(gpu, fs, generic, mode, monkeypatch
 @pytest.mark.parametrize("fs,generic", [(38.192e6, "0"), (16.368e6, "1")])
 @pytest.mark.parametrize("mode", ["best", "noncoherent"])
 def test_four_step_fused_statistics_equal_stats_pass(gpu, fs, generic, mode, monkeypatch):
-    """The row statistics fused into the four-step plan's last m4_rows (per-column
+    """The row statistics fused into the four-step plan's last m4_rows2 (per-column
     top-2, then m4_stats_kernel over the N1 columns) against the separate one-pass
     statistics kernel over the stored power rows (GNSSCORR_ACQ_M4STATS=0): the same
     power values feed both, so every peak, second peak, argmax and block is equal
@@ -223,8 +223,9 @@ def test_generic_multi_chunk_38192(gpu, mode, m4stats, monkeypatch):
     """The generic engine's chunk loop: GNSSCORR_ACQ_GCHUNK_MB=2 gives
     3 rows per chunk at N = 38192, so the 4-code spectra take 2 chunks, the 4 class rows
     2, and the 4 x 9 (x 2 blocks) units 12-24 chunks: every chunk after the first runs
-    with u0 > 0 in MixCorr, m4_launch and m4_stats_kernel (fused statistics on) or
-    g_stats1_kernel (off).  Against the fp64 oracle (SCI/GPS/L1/acquisition.sci:98-169)."""
+    with u0 > 0 in MixCorr, m4_launch and the fused statistics (fused on: carried by
+    the next chunk's m4_cols2, the last chunk's by m4_stats_kernel) or g_stats1_kernel
+    (off).  Against the fp64 oracle (SCI/GPS/L1/acquisition.sci:98-169)."""
     monkeypatch.setenv("GNSSCORR_ACQ_GCHUNK_MB", "2")
     monkeypatch.setenv("GNSSCORR_ACQ_M4STATS", m4stats)
     fs, n, nb = 38.192e6, 38192, 2
