@@ -1436,7 +1436,9 @@ def main():
     sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps // 5, 5), 2)
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
     gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps // 5, 5), 2)
-    gen = None if a.skip_track else run_acq_generic(dist, dev, max(a.steps // 2, 5), 2)
+    # (20 timed searches after 5 warmups: at 10 after 2 the first, clock-ramping ones read
+    # ~8 % slow against the steady state, profiles/r6/acq_generic_* A/Bs at 20 after 3)
+    gen = None if a.skip_track else run_acq_generic(dist, dev, max(a.steps, 10), 5)
     gsc = None if a.skip_track else run_gps_scilab(dist, dev, max(a.steps // 5, 5), 2)
 
     if dist.rank == 0:
