@@ -1433,11 +1433,13 @@ def main():
     tio = None if a.skip_track else run_track_io(dist, dev, max(a.steps, 20), a.warmup)
     sgt = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup)
     sgt_c4 = None if a.skip_track else run_sgt(dist, dev, max(a.steps, 20), a.warmup, FS)
-    sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps // 5, 5), 2)
+    # (20 timed searches after 5 warmups: 5 timed after 2 read 1.44 ms against 1.37-1.39
+    # in steady state, profiles/r6/fullsky_generic_steps_r7o.log)
+    sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps, 10), 5)
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
     gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps // 5, 5), 2)
-    # (20 timed searches after 5 warmups: at 10 after 2 the first, clock-ramping ones read
-    # ~8 % slow against the steady state, profiles/r6/acq_generic_* A/Bs at 20 after 3)
+    # (20 timed searches after 5 warmups: 10 timed after 3 read 0.99-1.00 ms against
+    # 0.94-0.95 at 20, profiles/r6/fullsky_generic_steps_r7o.log)
     gen = None if a.skip_track else run_acq_generic(dist, dev, max(a.steps, 10), 5)
     gsc = None if a.skip_track else run_gps_scilab(dist, dev, max(a.steps // 5, 5), 2)
 
