@@ -1437,11 +1437,11 @@ def main():
     # in steady state, profiles/r6/fullsky_generic_steps_r7o.log)
     sky = None if a.skip_track else run_fullsky(dist, dev, max(a.steps, 10), 5)
     sdr = None if a.skip_track else run_sdr(dist, dev, max(a.steps // 2, 10), 2)
-    gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps // 5, 5), 2)
+    gco = None if a.skip_track else run_glo_coherent(dist, dev, max(a.steps, 10), 5)
     # (20 timed searches after 5 warmups: 10 timed after 3 read 0.99-1.00 ms against
     # 0.94-0.95 at 20, profiles/r6/fullsky_generic_steps_r7o.log)
     gen = None if a.skip_track else run_acq_generic(dist, dev, max(a.steps, 10), 5)
-    gsc = None if a.skip_track else run_gps_scilab(dist, dev, max(a.steps // 5, 5), 2)
+    gsc = None if a.skip_track else run_gps_scilab(dist, dev, max(a.steps, 10), 5)
 
     if dist.rank == 0:
         W = dist.world
