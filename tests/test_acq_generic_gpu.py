@@ -276,3 +276,34 @@ def test_second_peak_window_across_the_wrap(gpu, engine, monkeypatch):
     r = ref_rows[0][2]
     assert r["argmax"] == p1 + 1 and r["second"] < 0.1 * r["peak"]   # the trap is set
     check_rows(res, rows, ref, ref_rows, True, label=f"wrap-window-{engine}")
+
+
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
+def test_generic_bench_scale_38192(gpu, mode):
+    """The bench's generic-rate search at full scale (bench.py run_acq_generic): 32 PRNs
+    x 41 bins x 2 blocks at 38.192 Msps with the default work buffer, i.e. the chunking
+    the bench runs (best: 2 624 units in 7 equal chunks of 375, each chunk's statistics
+    carried by the next chunk's first column pass; non-coherent: 1 312 rows in 4 chunks),
+    every row's statistics against the fp64 oracle (SCI/GPS/L1/acquisition.sci:98-169)."""
+    fs, n, nb = 38.192e6, 38192, 2
+    rng = np.random.default_rng(300)
+    planted = rng.choice(np.arange(1, 33), 8, replace=False)
+    sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
+                 doppler=float(rng.uniform(-5000, 5000)), cn0=49.0, data_bits=1) for p in planted]
+    IF = gpu.ifgen(nb * n, sigs, fs=fs, seed=0x5EED0030)
+    ctx = gpu.AcqCtx(fs, n, max_freqs=41, max_blocks=nb, max_codes=32)
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in range(1, 33)])
+    ctx.set_codes(codes)
+    freqs = 2.42e6 - 10000.0 + 500.0 * np.arange(41)
+    gf = np.tile(np.arange(41), (32, 1))
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    res, rows = ctx.search(IF, nb, freqs, np.arange(32), gf, spc=37, mode=m)
+    ref, ref_rows = A.acquire(IF, fs, codes, freqs, gf, spc=37, n_blocks=nb,
+                              noncoherent=mode == "noncoherent", return_rows=True)
+    if mode == "noncoherent":
+        for rr in ref_rows:
+            for r in rr:
+                r["block"] = -1
+    worst = check_rows(res, rows, ref, ref_rows, True, label=f"bench-scale-38192-{mode}")
+    print(f"[generic bench scale {mode}] worst rel {worst:.3e}")
+    assert all(res[p - 1]["metric"] > 2.5 for p in planted)

@@ -1,15 +1,7 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r7o
+O=gpurun_out/r7p
 mkdir -p $O
-export TMPDIR=/tmp BENCH_FULLSKY_PROJECTION=0
-for i in 1 2; do
-for S in 5 10 20; do
-  timeout -k 10 300 python3 tools/bench_part.py fullsky $S > $O/fs_$S.json 2> $O/fs_$S.err
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('fullsky steps', sys.argv[2], 'ms per search %.4f' % (d['dt']*1e3/d['steps']))" $O/fs_$S.json $S
-done
-for S in 10 20; do
-  timeout -k 10 300 python3 tools/bench_part.py acq_generic $S > $O/g_$S.json 2> $O/g_$S.err
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('generic steps', sys.argv[2], 'ms per search %.4f' % (d['dt']*1e3/d['steps']))" $O/g_$S.json $S
-done
-done
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py -v -x -s --timeout 200 --timeout-method thread -k "bench_scale or multi_chunk" > $O/pytest.log 2>&1
+grep -E "PASS|FAIL|worst|passed|failed" $O/pytest.log | tail -12
