@@ -1,7 +1,8 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r7p
+O=gpurun_out/r7q
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py -v -x -s --timeout 200 --timeout-method thread -k "bench_scale or multi_chunk" > $O/pytest.log 2>&1
-grep -E "PASS|FAIL|worst|passed|failed" $O/pytest.log | tail -12
+GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_nserial.so timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py -q -x --timeout 200 --timeout-method thread > $O/pytest_nserial.log 2>&1
+tail -1 $O/pytest_nserial.log
+bash tools/gpu_acq_ab.sh r7q "base nserial" "acq_generic" 3 0 | tee $O/ab.log
