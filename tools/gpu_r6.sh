@@ -1,8 +1,11 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r7s
+O=gpurun_out/r7z
 mkdir -p $O
 export TMPDIR=/tmp
-GNSSCORR_LIB=$PWD/gnss-sdr.ru_amd/ab/libgnsscorr_xcd.so timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py -q -x --timeout 200 --timeout-method thread > $O/pytest_xcd.log 2>&1
-echo "xcd $(tail -1 $O/pytest_xcd.log)"
-bash tools/gpu_acq_ab.sh r7s "base xcd" "acq_generic" 4 0 | tee $O/ab.log
+s0=$(date +%s.%N)
+timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+s1=$(date +%s.%N)
+python3 -c "print('wall_s', round($s1-$s0, 1))" | tee $O/bench.wall
+cp gpurun_out/bench_detail.json $O/bench_detail.json
+cut -c1-300 $O/bench.json
