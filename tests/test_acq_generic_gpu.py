@@ -219,6 +219,35 @@ def test_four_step_fused_statistics_equal_stats_pass(gpu, fs, generic, mode, mon
 
 @pytest.mark.parametrize("m4stats", ["1", "0"])
 @pytest.mark.parametrize("mode", ["best", "noncoherent"])
+def test_generic_multi_chunk_16368(gpu, mode, m4stats, monkeypatch):
+    """The chunk loop on the other four-step plan (48 x 341: m4_cols2<3, 16>): the
+    generic engine forced at 16.368 Msps with 1 MiB of Y per chunk (3 rows of 48 x 352
+    complex), so the carried statistics and u0 > 0 run with A = 3 as well."""
+    monkeypatch.setenv("GNSSCORR_ACQ_GENERIC", "1")
+    monkeypatch.setenv("GNSSCORR_ACQ_GCHUNK_MB", "1")
+    monkeypatch.setenv("GNSSCORR_ACQ_M4STATS", m4stats)
+    fs, n, nb = 16.368e6, 16368, 2
+    ctx = gpu.AcqCtx(fs, n, max_freqs=16, max_blocks=nb, max_codes=4)
+    prns = [6, 11, 19, 25]
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in prns])
+    ctx.set_codes(codes)
+    IF = _scene(gpu, fs, nb, 0x5EED0029)
+    freqs = 2.42e6 + 500.0 * np.arange(-4, 5)
+    gf = np.tile(np.arange(len(freqs)), (4, 1))
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    res, rows = ctx.search(IF, nb, freqs, np.arange(4), gf, spc=16, mode=m)
+    ref, ref_rows = A.acquire(IF, fs, codes, freqs, gf, spc=16, n_blocks=nb,
+                              noncoherent=mode == "noncoherent", return_rows=True)
+    if mode == "noncoherent":
+        for rr in ref_rows:
+            for r in rr:
+                r["block"] = -1
+    check_rows(res, rows, ref, ref_rows, True, label=f"chunked-16368-{mode}-m4stats{m4stats}")
+    assert res[0]["metric"] > 2.5 and res[2]["metric"] > 2.5
+
+
+@pytest.mark.parametrize("m4stats", ["1", "0"])
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
 def test_generic_multi_chunk_38192(gpu, mode, m4stats, monkeypatch):
     """The generic engine's chunk loop: GNSSCORR_ACQ_GCHUNK_MB=2 gives
     3 rows per chunk at N = 38192, so the 4-code spectra take 2 chunks, the 4 class rows
