@@ -2193,7 +2193,7 @@ __global__ __launch_bounds__(kM4ColThreads) M4_COLS2_ATTR void m4_cols2(const v2
 
 // m4_rows2 MODE 0: complex rows out (stride out_rs); MODE 2: |.|^2 / N^2 into pw (added
 // to the running sums when ACC); MODE 3: as 2 on a row's last block, per-column top-2
-// into top (pw written only when store)
+// into top (the power row is not stored)
 // The rows pass (round 6; the round-5 m4_rows kept complex rows in LDS, 21.9 KB per
 // 4-row tile, 7 waves per CU): the C-point stage reads its inputs straight from Y
 // (lanes cover 4 rows x 16 consecutive n2: whole lines), the exchange to the D-point
@@ -2215,7 +2215,7 @@ template <int C, int D, int MODE, bool ACC>
 __global__ __launch_bounds__(kM4RowThreads) __attribute__((amdgpu_waves_per_eu(M4_ROWS2_WPE)))
 void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int N,
               const v2d* __restrict__ tws, double* __restrict__ pw, int acc,
-              M4Top* __restrict__ top, int store) {
+              M4Top* __restrict__ top) {
   constexpr int N2 = C * D, P2 = m4_pitch(C * D);
   static_assert(is_prime(D), "m4_rows2: the second stage emits a prime DFT's outputs");
   static_assert(kM4RowThreads == 64 && D * kR2 <= 3 * 64 && C * kR2 <= 64,
@@ -2271,10 +2271,13 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
   // ---- exchange, one plane at a time; stage B: task (u, r) = (t / kR2, t % kR2)
   const int ub = t / kR2, rb = t % kR2;
   const bool actB = ub < C && k1_0 + rb < N1;
+  // the exchange reads are not predicated: an inactive lane reads a valid slot (ub
+  // clamped) and runs the D-point DFT on it, but emits nothing
+  const int ubc = min(ub, C - 1);
   v2d x[D];
   __syncthreads();
 #pragma unroll
-  for (int w = 0; w < D; w++) x[w].x = actB ? sp[rb][D * ub + w] : 0.0;
+  for (int w = 0; w < D; w++) x[w].x = sp[rb][D * ubc + w];
   __syncthreads();   // the imaginary parts overwrite the plane
 #pragma unroll
   for (int it = 0; it < kItA; it++) {
@@ -2286,7 +2289,7 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
   }
   __syncthreads();
 #pragma unroll
-  for (int w = 0; w < D; w++) x[w].y = actB ? sp[rb][D * ub + w] : 0.0;
+  for (int w = 0; w < D; w++) x[w].y = sp[rb][D * ubc + w];
   __builtin_amdgcn_sched_barrier(0);
   // ---- stage B: the D-point DFT; output w is element k2 = ub + C w of column k1
   const int k1 = k1_0 + rb;
@@ -2295,13 +2298,13 @@ void m4_rows2(const v2d* __restrict__ Y, v2d* __restrict__ out, int out_rs, int 
   int ak = INT_MAX;
   auto emit = [&](int w, v2d v) {
     if (!actB) return;
-    const long d = (long)k1 + (long)N1 * (ub + C * w);
+    const int d = k1 + N1 * (ub + C * w);   // < N
     if constexpr (MODE == 2 || MODE == 3) {
       const double q = fma(v.x, v.x, v.y * v.y) * sc;
       double* o = pw + row * N + d;
       const double val = ACC ? *o + q : q;   // (ACC: the running sums of earlier blocks)
-      if (MODE == 2 || store) *o = val;
-      if constexpr (MODE == 3) top1_push(a1, ak, a2, val, (int)d);
+      if constexpr (MODE == 2) *o = val;
+      else top1_push(a1, ak, a2, val, d);    // (the row's power is not stored)
     } else {
       out[row * out_rs + d] = v;
     }
@@ -2337,7 +2340,7 @@ int m4_plan(int N) {
 // rows [src] -> DFT rows or the correlation's power rows, one chunk of `rows`
 template <int MODE_IN, int MODE_OUT>
 int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_rs, int rows,
-              const MixCorr& cp, double* pw, int acc, int store = 1,
+              const MixCorr& cp, double* pw, int acc,
               const M4StatsJob* stats_job = nullptr) {
   const int N = c->cfg.n_samples;
   M4StatsJob sj = stats_job ? *stats_job : M4StatsJob{};
@@ -2357,11 +2360,11 @@ int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_r
     if (acc)                                                                                   \
       hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, true>), dim3((A * B + kR2 - 1) / kR2, rows),   \
                          dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
-                         acc, (M4Top*)c->d_m4top, store);                                      \
+                         acc, (M4Top*)c->d_m4top);                                             \
     else                                                                                       \
       hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, false>), dim3((A * B + kR2 - 1) / kR2, rows),  \
                          dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
-                         acc, (M4Top*)c->d_m4top, store);                                      \
+                         acc, (M4Top*)c->d_m4top);                                             \
     break;
     M4_CASE(1, 7, 16, 11, 31)
     M4_CASE(2, 3, 16, 11, 31)
@@ -2427,8 +2430,8 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
         const M4StatsJob* sj = b == 0 && pend.n > 0 ? &pend : nullptr;
         const int rc =
             fused && b == nb - 1
-                ? m4_launch<1, 3>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, 0, sj)
-                : m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, 1, sj);
+                ? m4_launch<1, 3>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, sj)
+                : m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, sj);
         if (rc) return rc;
         if (sj) pend.n = 0;
         continue;
