@@ -2341,7 +2341,8 @@ int m4_plan(int N) {
 template <int MODE_IN, int MODE_OUT>
 int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_rs, int rows,
               const MixCorr& cp, double* pw, int acc,
-              const M4StatsJob* stats_job = nullptr) {
+              const M4StatsJob* stats_job = nullptr, int lane = 0,
+              hipEvent_t after_cols = nullptr) {
   const int N = c->cfg.n_samples;
   M4StatsJob sj = stats_job ? *stats_job : M4StatsJob{};
   sj.main_rows = rows;
@@ -2350,21 +2351,24 @@ int m4_launch(gnsscorr_acq_ctx* c, const v2d* in, int in_rs, v2d* out, int out_r
   const int ey = sj.n > 0 ? (sj.n + per_y - 1) / per_y : 0;
   const v2d* tw = (const v2d*)c->d_twN;
   const v2d* tws1 = (const v2d*)c->d_twm4;   // W_N1^j, then W_N2^j from + N1
-  v2d* Y = (v2d*)c->d_gA;
+  v2d* Y = (v2d*)(lane ? c->d_gA2 : c->d_gA);
+  M4Top* top = (M4Top*)(lane ? c->d_m4top2 : c->d_m4top);
+  hipStream_t st = lane ? c->m4_s2 : c->stream;
   switch (c->m4) {
 #define M4_CASE(I, A, B, C, D)                                                                 \
   case I:                                                                                      \
     hipLaunchKernelGGL((m4_cols2<A, B, MODE_IN>),                                              \
                        dim3((N / (A * B) + kM4T2 - 1) / kM4T2, rows + ey), dim3(kM4ColThreads), \
-                       0, c->stream, in, in_rs, Y, N, tw, tws1, cp, sj);                       \
+                       0, st, in, in_rs, Y, N, tw, tws1, cp, sj);                              \
+    if (after_cols) HIP_TRY(hipEventRecord(after_cols, st));                                   \
     if (acc)                                                                                   \
       hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, true>), dim3((A * B + kR2 - 1) / kR2, rows),   \
-                         dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
-                         acc, (M4Top*)c->d_m4top);                                             \
+                         dim3(kM4RowThreads), 0, st, Y, out, out_rs, N, tws1 + A * B, pw,        \
+                         acc, top);                                                            \
     else                                                                                       \
       hipLaunchKernelGGL((m4_rows2<C, D, MODE_OUT, false>), dim3((A * B + kR2 - 1) / kR2, rows),  \
-                         dim3(kM4RowThreads), 0, c->stream, Y, out, out_rs, N, tws1 + A * B, pw, \
-                         acc, (M4Top*)c->d_m4top);                                             \
+                         dim3(kM4RowThreads), 0, st, Y, out, out_rs, N, tws1 + A * B, pw,        \
+                         acc, top);                                                            \
     break;
     M4_CASE(1, 7, 16, 11, 31)
     M4_CASE(2, 3, 16, 11, 31)
@@ -2416,22 +2420,36 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
   // of a column or the power rows are dumped
   const int N1 = c->m4 ? kM4Plans[c->m4][0] * kM4Plans[c->m4][1] : 0;
   const bool fused = c->m4 && c->d_m4top && 2 * spc - 1 <= N1 && !d_dump;
-  // equal chunks (7 x 375 rows rather than 6 x 385 + 314 at the bench's 2 624)
-  const int n_ch = (n_units + c->g_chunk - 1) / c->g_chunk;
+  // equal chunks (7 x 375 rows rather than 6 x 385 + 314 at the bench's 2 624); with
+  // two lanes an even count, chunk i on lane i % 2 (stream, Y, power rows, top-2 of
+  // its own), forked from and joined back to the context stream
+  const int lanes = c->m4 ? c->m4_lanes : 1;
+  int n_ch = (n_units + c->g_chunk - 1) / c->g_chunk;
+  if (lanes == 2 && n_ch > 1 && n_ch % 2) n_ch++;
   const int step = n_ch > 0 ? (n_units + n_ch - 1) / n_ch : c->g_chunk;
-  M4StatsJob pend;   // fused statistics of the previous chunk, not yet launched
-  for (int u0 = 0; u0 < n_units; u0 += step) {
+  // lane 1 starts after lane 0's first column pass, so from then on one lane's column
+  // pass (memory-bound) runs beside the other's row pass (fp64-issue-bound); started
+  // together, the lanes ran the same pass at the same time
+  M4StatsJob pends[2];   // per lane: fused statistics of its previous chunk, not yet launched
+  int ci = 0;
+  for (int u0 = 0; u0 < n_units; u0 += step, ci++) {
     const int nu = n_units - u0 < step ? n_units - u0 : step;
     const int nb = nc ? n_blocks : 1;
+    const int lane = lanes == 2 ? ci % 2 : 0;
+    M4StatsJob& pend = pends[lane];
+    double* const pw = lane ? c->d_gpw2 : c->d_gpw;
+    hipStream_t const st = lane ? c->m4_s2 : c->stream;
+    if (lanes == 2 && ci == 1) HIP_TRY(hipStreamWaitEvent(c->m4_s2, c->m4_ev[0], 0));
     for (int b = 0; b < nb; b++) {
       MixCorr cp{(const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1,
                  n_bins, u0, d_gcode, d_gfreq, (const int2*)c->d_fmap64};
       if (c->m4) {
         const M4StatsJob* sj = b == 0 && pend.n > 0 ? &pend : nullptr;
+        hipEvent_t const fork = lanes == 2 && ci == 0 && b == 0 ? c->m4_ev[0] : nullptr;
         const int rc =
             fused && b == nb - 1
-                ? m4_launch<1, 3>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, sj)
-                : m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, c->d_gpw, b > 0, sj);
+                ? m4_launch<1, 3>(c, nullptr, 0, nullptr, 0, nu, cp, pw, b > 0, sj, lane, fork)
+                : m4_launch<1, 2>(c, nullptr, 0, nullptr, 0, nu, cp, pw, b > 0, sj, lane, fork);
         if (rc) return rc;
         if (sj) pend.n = 0;
         continue;
@@ -2450,8 +2468,8 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
         Ns *= c->mix_r[i];
       }
     }
-    if (fused) {   // carried by the next chunk's first column pass, or launched below
-      pend.top = (const M4Top*)c->d_m4top;
+    if (fused) {   // carried by the lane's next column pass, or launched below
+      pend.top = (const M4Top*)(lane ? c->d_m4top2 : c->d_m4top);
       pend.stats = c->d_stats;
       pend.n = nu;
       pend.u0 = u0;
@@ -2460,19 +2478,25 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
       pend.nc = (int)nc;
       pend.spc = spc;
     } else if (stats1_exact(N, spc))
-      hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, c->stream,
-                         (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
+      hipLaunchKernelGGL(g_stats1_kernel, dim3(nu), dim3(kStatsThreads), 0, st,
+                         (const double*)pw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
                          d_dump, dump_block);
     else
-      hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, c->stream,
-                         (const double*)c->d_gpw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
+      hipLaunchKernelGGL(g_stats_kernel, dim3(nu), dim3(kGThreads), 0, st,
+                         (const double*)pw, N, u0, n_blocks, (int)nc, spc, c->d_stats,
                          d_dump, dump_block);
     HIP_TRY(hipGetLastError());
   }
-  if (pend.n > 0) {   // the last chunk's statistics
-    hipLaunchKernelGGL(m4_stats_kernel, dim3(pend.n), dim3(64), 0, c->stream, pend.top, N1, N,
-                       pend.u0, n_blocks, (int)nc, spc, c->d_stats);
-    HIP_TRY(hipGetLastError());
+  for (int l = 0; l < 2; l++)
+    if (pends[l].n > 0) {   // each lane's last chunk's statistics
+      hipLaunchKernelGGL(m4_stats_kernel, dim3(pends[l].n), dim3(64), 0,
+                         l ? c->m4_s2 : c->stream, pends[l].top, N1, N, pends[l].u0, n_blocks,
+                         (int)nc, spc, c->d_stats);
+      HIP_TRY(hipGetLastError());
+    }
+  if (lanes == 2) {
+    HIP_TRY(hipEventRecord(c->m4_ev[1], c->m4_s2));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->m4_ev[1], 0));
   }
   return GNSSCORR_OK;
 }
@@ -2491,8 +2515,18 @@ int mx_init(gnsscorr_acq_ctx* c) {
   // chunk size gave 0.963-0.965 ms at 242 MB of Y, 1.005 ms at 277 MB (the round-5 size)
   // and 1.007-1.028 ms at 259 MB (profiles/r6/acq_generic_chunk_sweep_r7h.log).
   // GNSSCORR_ACQ_GCHUNK_MB: another size in MiB, for A/Bs.
+  // Two chunk lanes (four-step plan; GNSSCORR_ACQ_M4LANES=1: one) split that budget:
+  // 116 MiB of Y each, so both lanes' Y stay in the cache together, and one chunk's
+  // column pass (memory-bound) overlaps the other's row pass (fp64-issue-bound).  Two
+  // whole searches on two streams ran 0.783-0.785 ms per search against 0.903-0.908 ms
+  // on one (profiles/r6/acq_generic_overlap_r8c.log); the lanes of one search gain
+  // 3 % (0.906-0.912 against 0.930-0.946 ms; 58 / 87 / 145 / 232 MiB per lane chunk
+  // slower, profiles/r6/acq_generic_lanes_ab_r8f.log): the search's own set-up and
+  // selection still run alone before the fork and after the join.
+  const char* gl = getenv("GNSSCORR_ACQ_M4LANES");
+  c->m4_lanes = c->m4 && !(gl && gl[0] == '1') ? 2 : 1;
   const char* gm = getenv("GNSSCORR_ACQ_GCHUNK_MB");
-  const long mb = gm && atol(gm) > 0 ? atol(gm) : (c->m4 ? 232 : 256);
+  const long mb = gm && atol(gm) > 0 ? atol(gm) : (c->m4 ? 232 / c->m4_lanes : 256);
   c->g_chunk = chunk_cap(c, (int)((mb << 20) / (ya * 16)));
   HIP_TRY(hipMalloc(&c->d_twN, sizeof(double2) * N));
   HIP_TRY(hipMalloc(&c->d_gA, sizeof(double2) * (size_t)ya * c->g_chunk));
@@ -2501,9 +2535,16 @@ int mx_init(gnsscorr_acq_ctx* c) {
   HIP_TRY(hipMalloc(&c->d_gpw, sizeof(double) * (size_t)N * c->g_chunk));
   // GNSSCORR_ACQ_M4STATS=0: the four-step plan keeps the separate statistics pass
   const char* fs = getenv("GNSSCORR_ACQ_M4STATS");
-  if (c->m4 && !(fs && fs[0] == '0'))
-    HIP_TRY(hipMalloc(&c->d_m4top, sizeof(M4Top) * (size_t)kM4Plans[c->m4][0] *
-                                       kM4Plans[c->m4][1] * c->g_chunk));
+  const size_t top_bytes = sizeof(M4Top) * (size_t)(c->m4 ? kM4Plans[c->m4][0] * kM4Plans[c->m4][1] : 0) *
+                           c->g_chunk;
+  if (c->m4 && !(fs && fs[0] == '0')) HIP_TRY(hipMalloc(&c->d_m4top, top_bytes));
+  if (c->m4_lanes == 2) {
+    HIP_TRY(hipMalloc(&c->d_gA2, sizeof(double2) * (size_t)ya * c->g_chunk));
+    HIP_TRY(hipMalloc(&c->d_gpw2, sizeof(double) * (size_t)N * c->g_chunk));
+    if (c->d_m4top) HIP_TRY(hipMalloc(&c->d_m4top2, top_bytes));
+    HIP_TRY(hipStreamCreateWithFlags(&c->m4_s2, hipStreamNonBlocking));
+    for (hipEvent_t& ev : c->m4_ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
   double2* h = (double2*)malloc(sizeof(double2) * N);
   if (!h) return GNSSCORR_ENOMEM;
   for (long t = 0; t < N; t++) {   // W_N^t = exp(-2 pi i t / N)
@@ -2586,9 +2627,19 @@ int acq64_init(gnsscorr_acq_ctx* c) {
 void acq64_free(gnsscorr_acq_ctx* c) {
   void* bufs[] = {c->d_F64, c->d_X64,   c->d_in64, c->d_twN, c->d_fmap64, c->d_lead64,
                   c->d_chirp, c->d_vf, c->d_twM, c->d_gA,  c->d_gB,     c->d_gpw,
-                  c->d_m4top, c->d_twm4};
+                  c->d_m4top, c->d_twm4, c->d_gA2, c->d_gpw2, c->d_m4top2};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  c->d_gA2 = nullptr;
+  c->d_gpw2 = nullptr;
+  c->d_m4top2 = nullptr;
+  for (hipEvent_t& ev : c->m4_ev)
+    if (ev) {
+      (void)hipEventDestroy(ev);
+      ev = nullptr;
+    }
+  if (c->m4_s2) (void)hipStreamDestroy(c->m4_s2);
+  c->m4_s2 = nullptr;
   c->d_chirp = c->d_vf = c->d_twM = c->d_gA = c->d_gB = nullptr;
   c->d_gpw = nullptr;
   c->d_m4top = nullptr;

@@ -49,6 +49,16 @@ struct gnsscorr_acq_ctx {
   // m4_rows): chunk x N1 entries, or null when the statistics run as their own pass
   void* d_m4top = nullptr;
   double2* d_twm4 = nullptr;            // four-step: W_N1^j (j < N1) then W_N2^j (j < N2)
+  // four-step plan, two chunk lanes: odd chunks run on a second stream with their own
+  // Y, power rows and column top-2 (m4_lanes == 2), so one chunk's column pass overlaps
+  // the other's row pass
+  int m4_lanes = 1;
+  hipStream_t m4_s2 = nullptr;
+  hipEvent_t m4_ev[3] = {nullptr, nullptr, nullptr};   // fork (after lane 0's first column
+                                                       // pass), join, spare
+  double2* d_gA2 = nullptr;
+  double* d_gpw2 = nullptr;
+  void* d_m4top2 = nullptr;
   // ---- shared
   int n_codes = 0;
   int spec_blocks = 0, spec_freqs = 0;  // shape of the resident IF spectra

@@ -336,3 +336,30 @@ def test_generic_bench_scale_38192(gpu, mode):
     worst = check_rows(res, rows, ref, ref_rows, True, label=f"bench-scale-38192-{mode}")
     print(f"[generic bench scale {mode}] worst rel {worst:.3e}")
     assert all(res[p - 1]["metric"] > 2.5 for p in planted)
+
+
+@pytest.mark.parametrize("m4stats", ["1", "0"])
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
+def test_two_lanes_equal_one_lane(gpu, mode, m4stats, monkeypatch):
+    """The four-step plan's two chunk lanes (odd chunks on a second stream with their own
+    Y, power rows and column top-2) give byte-identical rows and results to one lane
+    (GNSSCORR_ACQ_M4LANES=1), over many chunks (2 MiB: 6 rows per lane chunk)."""
+    fs, n, nb = 38.192e6, 38192, 2
+    prns = [6, 11, 19, 25]
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in prns])
+    IF = _scene(gpu, fs, nb, 0x5EED002A)
+    freqs = 2.42e6 + 500.0 * np.arange(-6, 7)
+    gf = np.tile(np.arange(len(freqs)), (4, 1))
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    monkeypatch.setenv("GNSSCORR_ACQ_GCHUNK_MB", "4")
+    monkeypatch.setenv("GNSSCORR_ACQ_M4STATS", m4stats)
+    out = {}
+    for lanes in ("2", "1"):
+        monkeypatch.setenv("GNSSCORR_ACQ_M4LANES", lanes)
+        ctx = gpu.AcqCtx(fs, n, max_freqs=16, max_blocks=nb, max_codes=4)
+        ctx.set_codes(codes)
+        out[lanes] = ctx.search(IF, nb, freqs, np.arange(4), gf, spc=37, mode=m)
+    (r2, w2), (r1, w1) = out["2"], out["1"]
+    assert r2.tobytes() == r1.tobytes()
+    assert w2.tobytes() == w1.tobytes()
+    assert r1[0]["metric"] > 2.5 and r1[2]["metric"] > 2.5

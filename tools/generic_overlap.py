@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import numpy as np  # noqa: E402
 import gnsscorr as gc  # noqa: E402
 
-FS, NB, NPRN, NBIN, K = 38.192e6, 2, 32, 41, 10
+FS, NB, NPRN, NBIN, K = 38.192e6, 2, 32, 41, 20
 N = int(round(FS / 1000.0))
 SPC = int(round(FS / 1.023e6))
 

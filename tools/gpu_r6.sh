@@ -1,8 +1,13 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r8b
+O=gpurun_out/r8f
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_acq_generic_gpu.py tests/test_acq_prn_codes_gpu.py tests/test_acq_16m_gpu.py -q -x --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
-tail -1 $O/pytest.log
-bash tools/gpu_acq_ab.sh r8b "base prev" "acq_generic" 4 0 | tee $O/ab.log
+for i in 1 2; do
+for MB in 58 87 116 145 232; do
+  GNSSCORR_ACQ_GCHUNK_MB=$MB timeout -k 10 300 python3 tools/bench_part.py acq_generic 20 > $O/g_$MB.json 2> $O/g_$MB.err
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('lanes 2, MiB of Y per lane chunk', sys.argv[2], 'ms per search %.4f' % (d['dt']*1e3/d['steps']))" $O/g_$MB.json $MB
+done
+GNSSCORR_ACQ_M4LANES=1 timeout -k 10 300 python3 tools/bench_part.py acq_generic 20 > $O/g_l1.json 2> $O/g_l1.err
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('lanes 1, 232 MiB', 'ms per search %.4f' % (d['dt']*1e3/d['steps']))" $O/g_l1.json
+done | tee $O/ab.log
