@@ -311,9 +311,10 @@ def test_second_peak_window_across_the_wrap(gpu, engine, monkeypatch):
 def test_generic_bench_scale_38192(gpu, mode):
     """The bench's generic-rate search at full scale (bench.py run_acq_generic): 32 PRNs
     x 41 bins x 2 blocks at 38.192 Msps with the default work buffer, i.e. the chunking
-    the bench runs (best: 2 624 units in 7 equal chunks of 375, each chunk's statistics
-    carried by the next chunk's first column pass; non-coherent: 1 312 rows in 4 chunks),
-    every row's statistics against the fp64 oracle (SCI/GPS/L1/acquisition.sci:98-169)."""
+    the bench runs (best: 2 624 units in 14 equal chunks of 188 on two chunk lanes, each
+    chunk's statistics carried by its lane's next column pass; non-coherent: 1 312 rows in
+    8 chunks), every row's statistics against the fp64 oracle
+    (SCI/GPS/L1/acquisition.sci:98-169)."""
     fs, n, nb = 38.192e6, 38192, 2
     rng = np.random.default_rng(300)
     planted = rng.choice(np.arange(1, 33), 8, replace=False)
