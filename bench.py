@@ -216,26 +216,35 @@ def run_acq(dist, dev, steps, warmup, precision=gc.ACQ_F64, records=None):
 GENERIC_FS = 38.192e6   # the classic SoftGNSS front end (acquisition.sci: samplesPerCode 38192)
 
 
-def run_acq_generic(dist, dev, steps, warmup, fs=GENERIC_FS):
-    """Config 2's search at a rate without a compiled plan: the generic fp64 engine,
-    mixed-radix Stockham passes (38192 = 16 x 7 x 11 x 31) with the correlation
-    product fused into the first pass and |.|^2 into the last."""
+GENERIC_RECORDS = int(os.environ.get("BENCH_GENERIC_RECORDS", "16"))   # searches per step (as ACQ_RECORDS)
+
+
+def run_acq_generic(dist, dev, steps, warmup, fs=GENERIC_FS, records=None):
+    """Config 2's search at a rate without a compiled plan: the generic fp64 engine
+    (38192 = 112 x 341: the four-step plan, the correlation product fused into the
+    column pass and |.|^2 with the row statistics into the row pass), `records`
+    consecutive 2-ms records of one stream per step (gnsscorr_acq_set_records, as the
+    config-2 line): ms per search = step time / records."""
+    records = GENERIC_RECORDS if records is None else records
     n = int(round(fs / 1000.0))
     spc = int(round(fs / 1.023e6))   # samplesPerCodeChip (GPS/L1/acquisition.sci:147), the exclusion window
     rng = np.random.default_rng(300 + dist.rank)
     planted = rng.choice(np.arange(1, 33), 8, replace=False)
     sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
                  doppler=float(rng.uniform(-5000, 5000)), cn0=49.0, data_bits=1) for p in planted]
-    IF = gc.ifgen(N_BLK * n, sigs, fs=fs, seed=0x5EED0030 + dist.rank)
+    IF = gc.ifgen(records * N_BLK * n, sigs, fs=fs, seed=0x5EED0030 + dist.rank)
     codes = np.stack([gc.sample_code(gc.ca_code(p), 1.023e6, fs, n) for p in range(1, 33)])
     freqs = 2.42e6 - 10000.0 + 500.0 * np.arange(N_BINS)
-    ctx = gc.AcqCtx(fs, n, device=dev, max_freqs=N_BINS, max_blocks=N_BLK, max_codes=N_PRN)
+    ctx = gc.AcqCtx(fs, n, device=dev, max_freqs=N_BINS, max_blocks=N_BLK * records,
+                    max_codes=N_PRN)
     ctx.set_codes(codes)
+    if records > 1:
+        ctx.set_records(records)
     b = dict(d_if=gc.DevBuf.from_array(IF, dev), d_freqs=gc.DevBuf.from_array(freqs, dev),
              d_gcode=gc.DevBuf.from_array(np.arange(N_PRN, dtype=np.int32), dev),
              d_gfreq=gc.DevBuf.from_array(np.tile(np.arange(N_BINS, dtype=np.int32), N_PRN), dev),
-             d_rows=gc.DevBuf(N_PRN * N_BINS * gc.ACQ_ROW.itemsize, dev),
-             d_res=gc.DevBuf(N_PRN * gc.ACQ_RESULT.itemsize, dev))
+             d_rows=gc.DevBuf(records * N_PRN * N_BINS * gc.ACQ_ROW.itemsize, dev),
+             d_res=gc.DevBuf(records * N_PRN * gc.ACQ_RESULT.itemsize, dev))
 
     def step():
         ctx.spectra_dev(b["d_if"].ptr, N_BLK, N_BINS, b["d_freqs"].ptr)
@@ -247,8 +256,8 @@ def run_acq_generic(dist, dev, steps, warmup, fs=GENERIC_FS):
     for _ in range(warmup):
         step()
     ctx.sync()
-    res = b["d_res"].download(gc.ACQ_RESULT)
-    found = sum(1 for p in planted if res[p - 1]["metric"] > 2.5)
+    res = b["d_res"].download(gc.ACQ_RESULT).reshape(records, N_PRN)
+    found = sum(1 for r in range(records) for p in planted if res[r][p - 1]["metric"] > 2.5)
     dist.barrier()
     gc.dev_synchronize(dev)
     t0 = time.perf_counter()
@@ -257,7 +266,8 @@ def run_acq_generic(dist, dev, steps, warmup, fs=GENERIC_FS):
     ctx.sync()
     gc.dev_synchronize(dev)
     dt = dist.max(time.perf_counter() - t0)
-    return dict(dt=dt, steps=steps, n=n, fs=fs, found=found, n_planted=len(planted))
+    return dict(dt=dt, steps=steps, n=n, fs=fs, found=found, n_planted=records * len(planted),
+                records=records)
 
 
 def _track_steps(steps):
@@ -1512,16 +1522,17 @@ def main():
             out["acquisition_generic"] = {
                 "metric": "acquisition cells/sec (config-2 search at a rate without a compiled "
                           "plan: fp64 generic engine)",
-                "value": N_PRN * N_BINS * gen["n"] * gen["steps"] * W / gen["dt"],
+                "value": N_PRN * N_BINS * gen["n"] * gen["steps"] * gen["records"] * W / gen["dt"],
                 "unit": "cells/s", "dtype": "f64",
-                "ms_per_search": gen["dt"] / gen["steps"] * 1e3,
-                # rocprof HBM bytes of one whole search (every per-search kernel, PMC pass of
+                "ms_per_search": gen["dt"] / (gen["steps"] * gen["records"]) * 1e3,
+                "records_per_step": gen["records"],
+                # rocprof HBM bytes of one whole step (every per-step kernel, PMC pass of
                 # this section) over its time
                 "roofline": {"bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
-                             "traffic_per_search": pmc_run_bytes("acq_generic"),
+                             "traffic_per_search": (pmc_run_bytes("acq_generic") or 0) / gen["records"] or None,
                              **hbm_fields(pmc_run_bytes("acq_generic"), gen["dt"] / gen["steps"])},
                 "config": f"fs = {gen['fs'] / 1e6:.3f} Msps (N = {gen['n']}): 32 PRN x 41 bins x "
-                          "2 blocks, every length-N DFT as a four-step N1 x N2 = 112 x 341 "
+                          "2 blocks per record, every length-N DFT as a four-step 112 x 341 "
                           "plan (two LDS passes, product fused into the first, |.|^2 and "
                           "per-column top-2 row statistics into the second)",
                 "planted_found": f"{gen['found']}/{gen['n_planted']}",

@@ -1995,9 +1995,12 @@ extern "C" int gnsscorr_acq_set_records(gnsscorr_acq_ctx* c, int n_records) {
     gnsscorr_set_error("gnsscorr_acq_set_records: need 1 <= n_records <= max_blocks");
     return GNSSCORR_EINVAL;
   }
-  if (n_records > 1 && (c->prec != GNSSCORR_ACQ_F64 || c->plan64 == 3)) {
+  // the generic engine takes records on its mixed-radix / four-step plans (the units of
+  // every record in one chunk loop), not on Bluestein's
+  if (n_records > 1 && (c->prec != GNSSCORR_ACQ_F64 || (c->plan64 == 3 && !c->mix_nr))) {
     gnsscorr_set_error("gnsscorr_acq_set_records: several records per search need the fp64 "
-                       "precision and a compiled plan (n_samples %d or %d)", 16368, 16000);
+                       "precision and a compiled plan (n_samples %d or %d) or a mixed-radix "
+                       "generic plan (no prime factor above 31)", 16368, 16000);
     return GNSSCORR_EINVAL;
   }
   // a per-group record table was made for the previous record count: set it again

@@ -1832,7 +1832,23 @@ struct MixCorr {
   const int* group_code;
   const int* group_freq;
   const int2* fmap;
+  // records (gnsscorr_acq_set_records): virtual group g = rec * n_groups + g0 searches
+  // group g0 on record rec, whose blocks are rec * n_blocks ... of the spectra's nbT
+  int n_groups = 1 << 30, nbT = 0;
 };
+
+// a correlation unit's class spectrum row and code spectrum row (MODE 1 of the passes)
+__device__ __forceinline__ void mix_unit_rows(const MixCorr& cp, int unit, const v2d*& Xr,
+                                              const v2d*& Fr, int& shift) {
+  const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
+  const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
+  const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
+  const int rec = g / cp.n_groups, g0 = g - rec * cp.n_groups;
+  const int2 fm = cp.fmap[cp.group_freq[g0 * cp.n_bins + bin]];
+  Xr = cp.X + ((long)fm.x * cp.nbT + rec * cp.n_blocks + blk) * cp.rs;
+  Fr = cp.F + (long)cp.group_code[g0] * cp.rs;
+  shift = fm.y;
+}
 
 // MODE 0: rows in (stride in_rs) -> rows out (stride out_rs)
 // MODE 1: first pass of a correlation chunk: the input is y[n] = conj(X[n - m]) F[n] of
@@ -1856,17 +1872,13 @@ __global__ __launch_bounds__(kMixThreads, mx_waves<R>()) void mx_pass(const v2d*
   const int NR = N / R;
   v2d v[R];
   if constexpr (MODE == 1) {
-    const int unit = cp.u0 + (int)row;
-    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
-    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
-    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
-    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
-    const v2d* Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
-    const v2d* Fr = cp.F + (long)cp.group_code[g] * cp.rs;
+    const v2d *Xr, *Fr;
+    int shift;
+    mix_unit_rows(cp, cp.u0 + (int)row, Xr, Fr, shift);
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const int n = j + r * NR;
-      int s = n - fm.y;
+      int s = n - shift;
       s += s < 0 ? N : 0;
       const v2d x = Xr[s], f = Fr[n];
       v[r] = (v2d){fma(x.x, f.x, x.y * f.y), fma(x.x, f.y, -(x.y * f.x))};
@@ -2091,16 +2103,7 @@ __global__ __launch_bounds__(kM4ColThreads) M4_COLS2_ATTR void m4_cols2(const v2
   const bool col = n2 < N2;
   const v2d *Xr = nullptr, *Fr = nullptr;
   int shift = 0;
-  if constexpr (MODE == 1) {
-    const int unit = cp.u0 + (int)row;
-    const int rowid = cp.nc_blk >= 0 ? unit : unit / cp.n_blocks;
-    const int blk = cp.nc_blk >= 0 ? cp.nc_blk : unit % cp.n_blocks;
-    const int g = rowid / cp.n_bins, bin = rowid % cp.n_bins;
-    const int2 fm = cp.fmap[cp.group_freq[g * cp.n_bins + bin]];
-    Xr = cp.X + ((long)fm.x * cp.n_blocks + blk) * cp.rs;
-    Fr = cp.F + (long)cp.group_code[g] * cp.rs;
-    shift = fm.y;
-  }
+  if constexpr (MODE == 1) mix_unit_rows(cp, cp.u0 + (int)row, Xr, Fr, shift);
   // ---- stage A: task (q, t), q = (task / kM4T2) < B: the A-point DFT over p of
   // x[B p + q], times W_N1^(q u), into LDS slot B u + q
   constexpr int kLanesQ = kM4ColThreads / kM4T2;   // values of q per pass
@@ -2414,7 +2417,9 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
                  int dump_block) {
   const int N = c->cfg.n_samples, P = c->mix_nr;
   const bool nc = mode == GNSSCORR_ACQ_NONCOHERENT;
-  const int n_units = n_groups * n_bins * (nc ? 1 : n_blocks);
+  // records: every group on every record of the resident spectra (virtual groups)
+  const int nrec = c->spec_recs;
+  const int n_units = nrec * n_groups * n_bins * (nc ? 1 : n_blocks);
   // four-step plans: the row statistics ride on the last block's m4_rows2 (per-column
   // top-2; its power rows are then not stored) unless the window can hold two samples
   // of a column or the power rows are dumped
@@ -2442,7 +2447,8 @@ int mx_correlate(gnsscorr_acq_ctx* c, int n_blocks, int mode, int n_groups, int 
     if (lanes == 2 && ci == 1) HIP_TRY(hipStreamWaitEvent(c->m4_s2, c->m4_ev[0], 0));
     for (int b = 0; b < nb; b++) {
       MixCorr cp{(const v2d*)c->d_X64, (const v2d*)c->d_F64, c->rs64, n_blocks, nc ? b : -1,
-                 n_bins, u0, d_gcode, d_gfreq, (const int2*)c->d_fmap64};
+                 n_bins, u0, d_gcode, d_gfreq, (const int2*)c->d_fmap64, n_groups,
+                 n_blocks * nrec};
       if (c->m4) {
         const M4StatsJob* sj = b == 0 && pend.n > 0 ? &pend : nullptr;
         hipEvent_t const fork = lanes == 2 && ci == 0 && b == 0 ? c->m4_ev[0] : nullptr;

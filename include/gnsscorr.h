@@ -357,11 +357,13 @@ int gnsscorr_acq_select_dev(gnsscorr_acq_ctx *ctx, int n_groups, int n_bins, con
  * first code period of |ifft|^2 as acquisition.sci keeps them.  Needs
  * n_blocks * coh_ms <= max_blocks.  Default 1. */
 int gnsscorr_acq_set_coherent(gnsscorr_acq_ctx *ctx, int coh_ms);
-/* Several records per search (fp64 precision, n_samples 16368 or 16000): the
- * following searches read n_records IF records laid end to end, record r at
+/* Several records per search (fp64 precision; n_samples 16368 or 16000, or a
+ * generic n_samples with no prime factor above 31): the following searches read
+ * n_records IF records laid end to end, record r at
  * sample r * n_blocks * coh_ms * n_samples (IQ pairs counted as one sample),
  * and search every record with the same frequencies and groups -- as
- * n_records separate acquisition.sci calls, in one correlation launch.
+ * n_records separate acquisition.sci calls, in one correlation launch (the
+ * generic engine: one chunk loop over every record's units).
  * Outputs are record-major: res[r * n_groups + g], rows[(r * n_groups + g) *
  * n_bins + b]; d_rows / d_res (and h_rows / h_res) hold n_records times as
  * many entries.  Needs n_records * n_blocks * coh_ms <= max_blocks.

@@ -52,6 +52,38 @@ def test_records_equal_single_searches(gpu, fs, n, mode):
         assert res[r][[3, 8, 13, 19].index(3 + 5 * r)]["metric"] > 2.5
 
 
+@pytest.mark.parametrize("fs,n,chunk_mb", [(38.192e6, 38192, "2"), (38.192e6, 38192, "0"),
+                                           (5.0e6, 5000, "0")])
+@pytest.mark.parametrize("mode", ["best", "noncoherent"])
+def test_generic_records_equal_single_searches(gpu, fs, n, chunk_mb, mode, monkeypatch):
+    """Records on the generic engine (the four-step plan at 38 192, with 2 MiB chunks so
+    the records' units cross chunk and lane boundaries; the mixed-radix passes at 5000):
+    every record bit-identical to its own single-record search."""
+    if chunk_mb != "0":
+        monkeypatch.setenv("GNSSCORR_ACQ_GCHUNK_MB", chunk_mb)
+    R, nb = 3, 2 if mode == "best" else 4
+    m = gpu.ACQ_NONCOHERENT if mode == "noncoherent" else gpu.ACQ_BEST_OF_BLOCKS
+    recs = _records(gpu, fs, n, nb, R, 0x5EED0058)
+    prns = [3, 8, 13, 19]
+    codes = np.stack([A.make_ca_table_row(p, fs) for p in prns])
+    freqs = A.gps_bins(2.42e6, 8, 1)
+    gf = np.tile(np.arange(len(freqs)), (len(prns), 1))
+    single = gpu.AcqCtx(fs, n, max_freqs=64, max_blocks=nb, max_codes=8)
+    single.set_codes(codes)
+    ref = [single.search(x, nb, freqs, np.arange(len(prns)), gf, mode=m) for x in recs]
+    batch = gpu.AcqCtx(fs, n, max_freqs=64, max_blocks=nb * R, max_codes=8)
+    batch.set_codes(codes)
+    batch.set_records(R)
+    res, rows = batch.search(np.concatenate(recs), nb, freqs, np.arange(len(prns)), gf, mode=m)
+    assert res.shape == (R, len(prns)) and rows.shape == (R, len(prns), len(freqs))
+    for r in range(R):
+        assert res[r].tobytes() == ref[r][0].tobytes(), f"record {r} results"
+        assert rows[r].tobytes() == ref[r][1].tobytes(), f"record {r} rows"
+    # (the single-record searches themselves are held to the oracle in
+    # test_acq_generic_gpu.py; the scenes here are the compiled-plan test's, weaker at
+    # these rates, so no detection threshold is asserted)
+
+
 def test_records_vs_oracle(gpu):
     fs, n, nb, R = 16.368e6, 16368, 2, 2
     recs = _records(gpu, fs, n, nb, R, 0x5EED0060)
@@ -101,8 +133,8 @@ def test_records_coherent_packed_and_dev(gpu):
 def test_records_refused(gpu):
     with pytest.raises(gpu.GnssCorrError):      # fp32 fast path: one record
         gpu.AcqCtx(16.368e6, 16368, max_blocks=4, precision=gpu.ACQ_F32).set_records(2)
-    with pytest.raises(gpu.GnssCorrError):      # Bluestein engine: one record
-        gpu.AcqCtx(5.0e6, 5000, max_blocks=4).set_records(2)
+    with pytest.raises(gpu.GnssCorrError):      # Bluestein engine (N = 4111, prime): one record
+        gpu.AcqCtx(4.111e6, 4111, max_blocks=4).set_records(2)
     ctx = gpu.AcqCtx(16.368e6, 16368, max_freqs=4, max_blocks=4, max_codes=1)
     ctx.set_codes(A.make_ca_table_row(1, 16.368e6)[None])
     ctx.set_records(3)

@@ -1,13 +1,11 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r8f
+O=gpurun_out/r8i
 mkdir -p $O
 export TMPDIR=/tmp
 for i in 1 2; do
-for MB in 58 87 116 145 232; do
-  GNSSCORR_ACQ_GCHUNK_MB=$MB timeout -k 10 300 python3 tools/bench_part.py acq_generic 20 > $O/g_$MB.json 2> $O/g_$MB.err
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('lanes 2, MiB of Y per lane chunk', sys.argv[2], 'ms per search %.4f' % (d['dt']*1e3/d['steps']))" $O/g_$MB.json $MB
+for R in 8 16; do
+  BENCH_GENERIC_RECORDS=$R timeout -k 10 300 python3 tools/bench_part.py acq_generic 20 > $O/g_$R.json 2> $O/g_$R.err
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('records', d['records'], 'ms per search %.4f' % (d['dt']*1e3/(d['steps']*d['records'])), 'found %s/%s' % (d['found'], d['n_planted']))" $O/g_$R.json
 done
-GNSSCORR_ACQ_M4LANES=1 timeout -k 10 300 python3 tools/bench_part.py acq_generic 20 > $O/g_l1.json 2> $O/g_l1.err
-python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('lanes 1, 232 MiB', 'ms per search %.4f' % (d['dt']*1e3/d['steps']))" $O/g_l1.json
 done | tee $O/ab.log
