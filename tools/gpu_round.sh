@@ -49,6 +49,7 @@ for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTI
   echo "pmc pass $i ok"
 done
 python tools/pmc_summary.py $O/pmc $O/pmc_summary.json --traffic $O/pmc_traffic.json
+rm -rf $O/pmc/p[0-9]*/   # raw counter CSVs (tens of MiB at 16-record steps): the summary stays
 fi
 if [ $PART = pmcA ]; then echo "== done (pmcA)"; exit 0; fi
 # HBM bytes per launch of the kernels several sections share, one section at a time
@@ -60,6 +61,7 @@ for S in acq track fullsky glo_coherent acq_generic gps_scilab; do
       python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1
   done
   python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S --runs 13
+  rm -rf $O/pmc_$S/FETCH_SIZE/ $O/pmc_$S/WRITE_SIZE/
   echo "pmc section $S ok"
 done
 # the tracking layouts one at a time (the layouts share kernel instantiations)
@@ -70,6 +72,7 @@ for L in cs1_int8 cs1_packed2 rx12_packed2; do
       python3 tools/trk_layout.py $L 10 > $O/pmc_trk_$L/$C.log 2>&1
   done
   python tools/pmc_summary.py $O/pmc_trk_$L $O/pmc_summary_trk_$L.json --traffic $O/pmc_traffic.json --section trk_$L
+  rm -rf $O/pmc_trk_$L/FETCH_SIZE/ $O/pmc_trk_$L/WRITE_SIZE/
   echo "pmc layout $L ok"
 done
 for S in sgt sdr; do
@@ -79,6 +82,7 @@ for S in sgt sdr; do
       python3 tools/bench_part.py $S 10 > $O/pmc_$S/$C.log 2>&1
   done
   python tools/pmc_summary.py $O/pmc_$S $O/pmc_summary_$S.json --traffic $O/pmc_traffic.json --section $S
+  rm -rf $O/pmc_$S/FETCH_SIZE/ $O/pmc_$S/WRITE_SIZE/
   echo "pmc section $S ok"
 done
 echo "== tracking A/B (same box): stream kernel, TRACK_LO_SPLIT=0 build, per-call workgroup kernel"
