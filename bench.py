@@ -599,14 +599,19 @@ def fullsky_shard_projection(dev, if_gps, if_glo, steps, t1):
 GLO_COH, GLO_BAND_KHZ = 5, 12.0   # GLONASS initSettings.sci: acqCohIntegration 5, acqSearchBand 12
 
 
-def run_glo_coherent(dist, dev, steps, warmup):
+GLO_COH_RECORDS = int(os.environ.get("BENCH_GLO_COH_RECORDS", "16"))   # searches per step
+
+
+def run_glo_coherent(dist, dev, steps, warmup, records=None):
     """The GLONASS receiver's default acquisition (initSettings.sci:88-96): 14 FCH x 121 bins
-    (12 kHz at 100 Hz) x 2 blocks of 5 ms coherent, resident IF, one search per step."""
+    (12 kHz at 100 Hz) x 2 blocks of 5 ms coherent, resident IF, `records` consecutive
+    records of one stream per step (gnsscorr_acq_set_records, as the config-2 line)."""
+    records = GLO_COH_RECORDS if records is None else records
     rng = np.random.default_rng(0x5EED0009 + dist.rank)
     glo = rng.choice(np.arange(-7, 7), 4, replace=False)
     sl = [dict(system=1, fch=int(k), code_phase=float(rng.uniform(0, 511)),
                doppler=float(rng.uniform(-5000, 5000)), cn0=39.0) for k in glo]
-    IF = gc.ifgen(2 * GLO_COH * N, sl, fs=FS, if_glo=1.0e6, seed=0x5EED000A + dist.rank)
+    IF = gc.ifgen(records * 2 * GLO_COH * N, sl, fs=FS, if_glo=1.0e6, seed=0x5EED000A + dist.rank)
     nb = int(round(GLO_BAND_KHZ * 2 * GLO_COH)) + 1
     freqs, gf = [], []
     for k in range(-7, 7):                                # acquisition.sci:105-108
@@ -614,15 +619,18 @@ def run_glo_coherent(dist, dev, steps, warmup):
         gf.append(np.arange(len(freqs), len(freqs) + nb))
         freqs.extend(c0 - (GLO_BAND_KHZ / 2) * 1000 + (1000 / (2 * GLO_COH)) * np.arange(nb))
     freqs, gf = np.array(freqs), np.array(gf, np.int32)
-    ctx = gc.AcqCtx(FS, N, device=dev, max_freqs=len(freqs), max_blocks=2 * GLO_COH, max_codes=1)
+    ctx = gc.AcqCtx(FS, N, device=dev, max_freqs=len(freqs), max_blocks=2 * GLO_COH * records,
+                    max_codes=1)
     ctx.set_codes(gc.sample_code(gc.st_code(), 0.511e6, FS, N)[None])   # makeStTable.sci
     ctx.set_coherent(GLO_COH)
+    if records > 1:
+        ctx.set_records(records)
     d_if = gc.DevBuf.from_array(IF, dev)
     d_f = gc.DevBuf.from_array(freqs, dev)
     d_gc = gc.DevBuf.from_array(np.zeros(14, np.int32), dev)
     d_gf = gc.DevBuf.from_array(gf, dev)
-    d_rows = gc.DevBuf(14 * nb * gc.ACQ_ROW.itemsize, dev)
-    d_res = gc.DevBuf(14 * gc.ACQ_RESULT.itemsize, dev)
+    d_rows = gc.DevBuf(records * 14 * nb * gc.ACQ_ROW.itemsize, dev)
+    d_res = gc.DevBuf(records * 14 * gc.ACQ_RESULT.itemsize, dev)
 
     def step():
         ctx.search_dev(d_if.ptr, 2, len(freqs), d_f.ptr, 14, nb, d_gc.ptr, d_gf.ptr, d_rows.ptr,
@@ -636,37 +644,46 @@ def run_glo_coherent(dist, dev, steps, warmup):
         step()
     ctx.sync()
     dt = dist.max(time.perf_counter() - t0)
-    res = d_res.download(np.uint8).view(gc.ACQ_RESULT)
-    found = int(sum(res[int(k) + 7]["metric"] > 2.5 for k in glo))
-    return dict(dt=dt, steps=steps, nb=nb, found=found, n_planted=len(glo))
+    res = d_res.download(np.uint8).view(gc.ACQ_RESULT).reshape(records, 14)
+    found = int(sum(res[r][int(k) + 7]["metric"] > 2.5 for r in range(records) for k in glo))
+    return dict(dt=dt, steps=steps, nb=nb, found=found, n_planted=records * len(glo),
+                records=records)
 
 
 GPS_SCI_FS, GPS_SCI_COH, GPS_SCI_BAND = 16.0e6, 4, 14.0   # SCI/GPS/L1/initSettings.sci:68-87
 
 
-def run_gps_scilab(dist, dev, steps, warmup):
+GPS_SCI_RECORDS = int(os.environ.get("BENCH_GPS_SCI_RECORDS", "16"))   # searches per step (as ACQ_RECORDS)
+
+
+def run_gps_scilab(dist, dev, steps, warmup, records=None):
     """The Scilab GPS receiver's own default acquisition (initSettings.sci:68-87):
     fs 16 MHz (samplesPerCode 16000: the 40 x 40 x 10 fp64 plan), 32 PRN x 113 bins
-    (14 kHz at 125 Hz) x 2 blocks of 4 ms coherent, resident IF, one search per step
-    (acquisition.sci:46-192; parity in tests/test_acq_16m_gpu.py)."""
+    (14 kHz at 125 Hz) x 2 blocks of 4 ms coherent, resident IF, `records` consecutive
+    records of one stream per step (gnsscorr_acq_set_records, as the config-2 line;
+    acquisition.sci:46-192 per record; parity in tests/test_acq_16m_gpu.py)."""
+    records = GPS_SCI_RECORDS if records is None else records
     fs, n = GPS_SCI_FS, int(round(GPS_SCI_FS / 1000.0))
     rng = np.random.default_rng(0x5EED0040 + dist.rank)
     planted = rng.choice(np.arange(1, 33), 6, replace=False)
     sigs = [dict(system=0, prn=int(p), code_phase=float(rng.uniform(0, 1023)),
                  doppler=float(rng.uniform(-5000, 5000)), cn0=44.0, data_bits=1) for p in planted]
-    IF = gc.ifgen(2 * GPS_SCI_COH * n, sigs, fs=fs, seed=0x5EED0041 + dist.rank)
+    IF = gc.ifgen(records * 2 * GPS_SCI_COH * n, sigs, fs=fs, seed=0x5EED0041 + dist.rank)
     nb = int(round(GPS_SCI_BAND * 2 * GPS_SCI_COH)) + 1         # acquisition.sci:101-104
     freqs = 2.42e6 - (GPS_SCI_BAND / 2) * 1000 + (1000 / (2 * GPS_SCI_COH)) * np.arange(nb)
     codes = np.stack([gc.sample_code(gc.ca_code(p), 1.023e6, fs, n) for p in range(1, 33)])
-    ctx = gc.AcqCtx(fs, n, device=dev, max_freqs=nb, max_blocks=2 * GPS_SCI_COH, max_codes=32)
+    ctx = gc.AcqCtx(fs, n, device=dev, max_freqs=nb, max_blocks=2 * GPS_SCI_COH * records,
+                    max_codes=32)
     ctx.set_codes(codes)
     ctx.set_coherent(GPS_SCI_COH)
+    if records > 1:
+        ctx.set_records(records)
     d_if = gc.DevBuf.from_array(IF, dev)
     d_f = gc.DevBuf.from_array(freqs, dev)
     d_gc = gc.DevBuf.from_array(np.arange(32, dtype=np.int32), dev)
     d_gf = gc.DevBuf.from_array(np.tile(np.arange(nb, dtype=np.int32), 32), dev)
-    d_rows = gc.DevBuf(32 * nb * gc.ACQ_ROW.itemsize, dev)
-    d_res = gc.DevBuf(32 * gc.ACQ_RESULT.itemsize, dev)
+    d_rows = gc.DevBuf(records * 32 * nb * gc.ACQ_ROW.itemsize, dev)
+    d_res = gc.DevBuf(records * 32 * gc.ACQ_RESULT.itemsize, dev)
 
     def step():
         ctx.search_dev(d_if.ptr, 2, nb, d_f.ptr, 32, nb, d_gc.ptr, d_gf.ptr, d_rows.ptr,
@@ -680,9 +697,10 @@ def run_gps_scilab(dist, dev, steps, warmup):
         step()
     ctx.sync()
     dt = dist.max(time.perf_counter() - t0)
-    res = d_res.download(np.uint8).view(gc.ACQ_RESULT)
-    found = int(sum(res[int(p) - 1]["metric"] > 2.5 for p in planted))
-    return dict(dt=dt, steps=steps, nb=nb, n=n, found=found, n_planted=len(planted))
+    res = d_res.download(np.uint8).view(gc.ACQ_RESULT).reshape(records, 32)
+    found = int(sum(res[r][int(p) - 1]["metric"] > 2.5 for r in range(records) for p in planted))
+    return dict(dt=dt, steps=steps, nb=nb, n=n, found=found, n_planted=records * len(planted),
+                records=records)
 
 
 SDR_REC, SDR_SV, SDR_ROWS, SDR_N = 64, 32, 120, 2048
@@ -1687,42 +1705,42 @@ def main():
         if gsc:
             cells = 32 * gsc["nb"] * gsc["n"]
             fl = cells * N_BLK * (5.0 * np.log2(gsc["n"]) + 10)
+            ts = gsc["dt"] / (gsc["steps"] * gsc["records"])   # seconds per search
             out["gps_acquisition_scilab"] = {
                 "metric": "acquisition cells/sec (the Scilab GPS receiver's default search)",
-                "value": cells * gsc["steps"] * W / gsc["dt"], "unit": "cells/s",
-                "ms_per_search": gsc["dt"] / gsc["steps"] * 1e3,
+                "value": cells * W / ts, "unit": "cells/s",
+                "ms_per_search": ts * 1e3, "records_per_step": gsc["records"],
                 "config": f"SCI/GPS/L1/initSettings.sci defaults: 32 PRN x {gsc['nb']} bins (14 kHz "
                           f"at 125 Hz) x 16000 code phases, 2 blocks of {GPS_SCI_COH} ms coherent, "
                           "16 Msps, fp64 (40 x 40 x 10 plan), IF resident in HBM",
                 "planted_found": f"{gsc['found']}/{gsc['n_planted']}",
                 "dtype": "f64",
                 "roofline": {"bound": "valu", "kernel": "acq64 (whole search)",
-                             "achieved": fl / (gsc["dt"] / gsc["steps"]) / 1e12,
+                             "achieved": fl / ts / 1e12,
                              "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
-                             "frac": fl / (gsc["dt"] / gsc["steps"]) / 1e12 / PEAK_FP64_TFLOPS,
-                             "traffic_per_search": pmc_run_bytes("gps_scilab"),
+                             "frac": fl / ts / 1e12 / PEAK_FP64_TFLOPS,
+                             "traffic_per_search": (pmc_run_bytes("gps_scilab") or 0) / gsc["records"] or None,
                              **hbm_fields(pmc_run_bytes("gps_scilab"), gsc["dt"] / gsc["steps"])},
             }
         if gco:
             cells = 14 * gco["nb"] * N
+            tg = gco["dt"] / (gco["steps"] * gco["records"])   # seconds per search
             out["glonass_acquisition_5ms"] = {
                 "metric": "acquisition cells/sec (GLONASS, 5 ms coherent, acquisition.sci)",
-                "value": cells * gco["steps"] * W / gco["dt"], "unit": "cells/s",
-                "ms_per_search": gco["dt"] / gco["steps"] * 1e3,
+                "value": cells * W / tg, "unit": "cells/s",
+                "ms_per_search": tg * 1e3, "records_per_step": gco["records"],
                 "config": f"GLONASS initSettings.sci defaults: 14 FCH x {gco['nb']} bins (12 kHz "
                           f"at 100 Hz) x 16368 code phases, 2 blocks of {GLO_COH} ms coherent, "
-                          "16.368 Msps, IF resident in HBM; one search per GPU per step",
+                          "16.368 Msps, IF resident in HBM",
                 "planted_found": f"{gco['found']}/{gco['n_planted']}",
                 "dtype": "f64",
                 "roofline": {"bound": "valu", "kernel": "acq64 (whole search)",
-                             "achieved": cells * N_BLK * FLOP_PER_CELL_BLOCK
-                             / (gco["dt"] / gco["steps"]) / 1e12,
+                             "achieved": cells * N_BLK * FLOP_PER_CELL_BLOCK / tg / 1e12,
                              "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s (fp64)",
-                             "frac": cells * N_BLK * FLOP_PER_CELL_BLOCK
-                             / (gco["dt"] / gco["steps"]) / 1e12 / PEAK_FP64_TFLOPS,
-                             "timing": "whole search per step (the 5-ms folding wipe-off and "
-                                       "forward spectra included)",
-                             "traffic_per_search": pmc_run_bytes("glo_coherent"),
+                             "frac": cells * N_BLK * FLOP_PER_CELL_BLOCK / tg / 1e12 / PEAK_FP64_TFLOPS,
+                             "timing": "whole search (the 5-ms folding wipe-off and forward "
+                                       "spectra included)",
+                             "traffic_per_search": (pmc_run_bytes("glo_coherent") or 0) / gco["records"] or None,
                              **hbm_fields(pmc_run_bytes("glo_coherent"),
                                           gco["dt"] / gco["steps"])},
             }
