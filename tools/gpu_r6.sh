@@ -1,11 +1,11 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r8l
+O=gpurun_out/r8y
 mkdir -p $O
 export TMPDIR=/tmp
-for i in 1 2; do
-for R in 1 4 16; do
-  BENCH_GLO_COH_RECORDS=$R timeout -k 10 300 python3 tools/bench_part.py glo_coherent 10 > $O/s_$R.json 2> $O/s_$R.err
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('records', d['records'], 'ms per search %.4f' % (d['dt']*1e3/(d['steps']*d['records'])), 'found %s/%s' % (d['found'], d['n_planted']))" $O/s_$R.json
-done
-done | tee $O/ab.log
+s0=$(date +%s.%N)
+timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+s1=$(date +%s.%N)
+python3 -c "print('wall_s', round($s1-$s0, 1))" | tee $O/bench.wall
+cp gpurun_out/bench_detail.json $O/bench_detail.json
+cut -c1-200 $O/bench.json
