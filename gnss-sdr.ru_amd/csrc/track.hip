@@ -1105,7 +1105,10 @@ __global__ __launch_bounds__(kMaxThreads, 8) void osg_track_kernel(
 // Channels sharing a stream (receivers) read it through L2, which the
 // XCD-aware channel order keeps on one XCD.
 // ============================================================================
-constexpr int kStreamCh = 4;      // channels (wavefronts) per workgroup
+#ifndef TRACK_STREAM_CH
+#define TRACK_STREAM_CH 4
+#endif
+constexpr int kStreamCh = TRACK_STREAM_CH;   // channels (wavefronts) per workgroup
 #ifndef TRACK_PF
 #define TRACK_PF 1                // LO words and row bytes read ahead (pair2r, interval_end_s)
 #endif
