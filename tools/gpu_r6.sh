@@ -1,11 +1,13 @@
 # Scratch session script of round 6 (the current GPU call; earlier sessions are in git history)
 set -eu
-O=gpurun_out/r9b
+O=gpurun_out/r9c
 mkdir -p $O
 export TMPDIR=/tmp
-for i in 1 2; do
-for MB in 87 116 145; do
-  GNSSCORR_ACQ_GCHUNK_MB=$MB timeout -k 10 300 python3 tools/bench_part.py acq_generic 10 > $O/g_$MB.json 2> $O/g_$MB.err
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('16 records, MiB of Y per lane chunk', sys.argv[2], 'ms per search %.4f' % (d['dt']*1e3/(d['steps']*d['records'])))" $O/g_$MB.json $MB
-done
-done | tee $O/ab.log
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 tools/bench_part.py acq_generic 5 > $O/kt.log 2>&1
+python3 - <<PY
+import csv,glob
+f=glob.glob("$O/kt/*kernel_stats.csv")[0]
+for r in csv.DictReader(open(f)):
+    print(r["Name"][:60], r["Calls"], round(float(r["AverageNs"])/1e3,2), round(float(r["TotalDurationNs"])/1e3,1))
+PY
+rm -f $O/kt/*kernel_trace.csv
